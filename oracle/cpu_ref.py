@@ -1,0 +1,309 @@
+"""CPU fp32 restatement of the reference's video->spike training hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is the parity *checker*: only `tests/`,
+`__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may import it.  The product
+path (`video-spike_amd/vspike`) never imports it and has no CPU fallback.
+
+Every function restates one piece of the reference with plain torch CPU fp32 ops (autograd
+supplies the backward for the checker).  Parity of this restatement is PINNED by golden
+fixtures generated from the reference itself (`oracle/gen_fixtures.py` imports
+`/root/reference/src/model/linear.py` and the installed HF `transformers.VideoMAEModel`, the
+third-party encoder the reference runs) — see `tests/test_oracle_golden.py`.
+
+Reference citations (paths relative to the reference repo root):
+  * `src/model/linear.py:3-56`                       Linear plugin (flatten -> MLP enc -> MLP dec -> reshape)
+  * `src/model/videomae.py:16-32`                    VideoMAE plugin forward (encoder -> flatten -> Linear -> Linear)
+  * `src/model/videomae/modeling_videomae.py:101-112` fixed sinusoid position table
+  * `src/model/videomae/modeling_videomae.py:183-196` tubelet Conv3d patch embedding
+  * `src/model/videomae/modeling_videomae.py:230-266` self-attention (q/v bias, k bias == 0, softmax(QK^T/sqrt(dh))V)
+  * `src/model/videomae/modeling_videomae.py:419-445` pre-LN block
+  * `src/train.py:59` + `src/trainer/base.py:141-143` PoissonNLLLoss(log_input=True).mean()
+  * `src/train.py:44-57` + `src/trainer/base.py:144-159` AdamW + OneCycleLR train step
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from . import prng
+
+
+# ----------------------------------------------------------------------------------------------
+# configuration
+# ----------------------------------------------------------------------------------------------
+@dataclasses.dataclass(frozen=True)
+class ViTCfg:
+    """Encoder geometry (keys mirror `config/model/videomae/videomae.yaml` of the reference)."""
+    image_size: int = 224
+    patch_size: int = 16
+    num_channels: int = 3
+    num_frames: int = 16
+    tubelet_size: int = 2
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    layer_norm_eps: float = 1e-12
+
+    @property
+    def num_tokens(self) -> int:
+        g = self.image_size // self.patch_size
+        return (self.num_frames // self.tubelet_size) * g * g
+
+    @property
+    def patch_dim(self) -> int:
+        return self.num_channels * self.tubelet_size * self.patch_size * self.patch_size
+
+
+VIT_BASE = ViTCfg()
+VIT_TINY = ViTCfg(hidden_size=192, num_attention_heads=3, intermediate_size=768)
+VIT_SMALL_FIXTURE = ViTCfg(image_size=112, num_frames=8, hidden_size=128, num_hidden_layers=2,
+                           num_attention_heads=2, intermediate_size=512)
+
+
+# ----------------------------------------------------------------------------------------------
+# deterministic parameters / inputs (names follow the reference plugin's state_dict)
+# ----------------------------------------------------------------------------------------------
+def vit_param_shapes(cfg: ViTCfg, enc_out: int, n_out: int) -> Dict[str, Tuple[int, ...]]:
+    D, F = cfg.hidden_size, cfg.intermediate_size
+    s: Dict[str, Tuple[int, ...]] = {
+        "video_mae.embeddings.patch_embeddings.projection.weight":
+            (D, cfg.num_channels, cfg.tubelet_size, cfg.patch_size, cfg.patch_size),
+        "video_mae.embeddings.patch_embeddings.projection.bias": (D,),
+    }
+    for i in range(cfg.num_hidden_layers):
+        p = f"video_mae.encoder.layer.{i}."
+        s.update({
+            p + "attention.attention.query.weight": (D, D), p + "attention.attention.query.bias": (D,),
+            p + "attention.attention.key.weight": (D, D),
+            p + "attention.attention.value.weight": (D, D), p + "attention.attention.value.bias": (D,),
+            p + "attention.output.dense.weight": (D, D), p + "attention.output.dense.bias": (D,),
+            p + "intermediate.dense.weight": (F, D), p + "intermediate.dense.bias": (F,),
+            p + "output.dense.weight": (D, F), p + "output.dense.bias": (D,),
+            p + "layernorm_before.weight": (D,), p + "layernorm_before.bias": (D,),
+            p + "layernorm_after.weight": (D,), p + "layernorm_after.bias": (D,),
+        })
+    s["encoder.weight"] = (enc_out, cfg.num_tokens * D)
+    s["encoder.bias"] = (enc_out,)
+    s["decoder.weight"] = (n_out * 100, enc_out)
+    s["decoder.bias"] = (n_out * 100,)
+    return s
+
+
+def make_vit_params(cfg: ViTCfg, enc_out: int, n_out: int, seed: int = 2) -> Dict[str, np.ndarray]:
+    """Seeded weights.  Matrices ~ N(0, 0.02) like HF `_init_weights` (modeling_videomae.py:512-522);
+    biases and LayerNorm affine terms are perturbed away from 0/1 so that every term is exercised."""
+    out = {}
+    for name, shape in vit_param_shapes(cfg, enc_out, n_out).items():
+        if name.endswith("layernorm_before.weight") or name.endswith("layernorm_after.weight"):
+            out[name] = prng.normal(seed, shape, name, std=0.1, mean=1.0)
+        elif name in ("encoder.weight",):
+            out[name] = prng.normal(seed, shape, name, std=1.0 / math.sqrt(shape[1]))
+        elif name in ("decoder.weight",):
+            out[name] = prng.normal(seed, shape, name, std=0.5 / math.sqrt(shape[1]))
+        elif len(shape) == 1:
+            out[name] = prng.normal(seed, shape, name, std=0.02)
+        else:
+            out[name] = prng.normal(seed, shape, name, std=0.02)
+    return out
+
+
+def linear_param_shapes(input_dim: int, enc_hidden: List[int], enc_out: int,
+                        dec_hidden: List[int], output_dim: int) -> Dict[str, Tuple[int, ...]]:
+    """Names of `src/model/linear.py:17-56` (nn.Sequential indices 0,2,4 hold the Linear layers)."""
+    s = {}
+    dims = [input_dim] + list(enc_hidden) + [enc_out]
+    for j in range(len(dims) - 1):
+        s[f"encoder.layers.{2 * j}.weight"] = (dims[j + 1], dims[j])
+        s[f"encoder.layers.{2 * j}.bias"] = (dims[j + 1],)
+    dims = [enc_out] + list(dec_hidden) + [output_dim]
+    for j in range(len(dims) - 1):
+        s[f"decoder.layers.{2 * j}.weight"] = (dims[j + 1], dims[j])
+        s[f"decoder.layers.{2 * j}.bias"] = (dims[j + 1],)
+    return s
+
+
+def make_linear_params(shapes: Dict[str, Tuple[int, ...]], seed: int = 2,
+                       input_scale: float = 1.0 / 128.0) -> Dict[str, np.ndarray]:
+    """std 0.5/sqrt(fan_in); the first layer also absorbs `input_scale` because the plugin's raw
+    inputs are 0..255 pixel values (base.py:64-67 feeds them unnormalised)."""
+    out = {}
+    for name, shape in shapes.items():
+        fan_in = shape[1] if len(shape) == 2 else shapes[name.replace(".bias", ".weight")][1]
+        std = 0.5 / math.sqrt(fan_in) * (input_scale if name == "encoder.layers.0.weight" else 1.0)
+        out[name] = prng.normal(seed, shape, name, std=std)
+    return out
+
+
+def make_pixels(cfg: ViTCfg, batch: int, seed: int = 0) -> np.ndarray:
+    return prng.normal(seed, (batch, cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size),
+                       "pixel_values")
+
+
+# ----------------------------------------------------------------------------------------------
+# encoder restatement
+# ----------------------------------------------------------------------------------------------
+def sinusoid_table(n_position: int, d_hid: int) -> torch.Tensor:
+    """Fixed position table, `modeling_videomae.py:101-112` (float64 angles, cast to float32)."""
+    pos = np.arange(n_position, dtype=np.float64)[:, None]
+    j = np.arange(d_hid)[None, :]
+    angle = pos / np.power(10000.0, 2 * (j // 2) / d_hid)
+    table = np.empty_like(angle)
+    table[:, 0::2] = np.sin(angle[:, 0::2])
+    table[:, 1::2] = np.cos(angle[:, 1::2])
+    return torch.from_numpy(table.astype(np.float32))
+
+
+def im2col(pixels: torch.Tensor, cfg: ViTCfg) -> torch.Tensor:
+    """(B, F, C, H, W) -> (B*N, C*t*p*p).  Token n = (f', hp, wp) row-major (the Conv3d output's
+    `flatten(2).transpose(1, 2)` order, `modeling_videomae.py:194-195`); column = (c, t, i, j),
+    the Conv3d weight's flatten order."""
+    B, F, C, H, W = pixels.shape
+    t, p = cfg.tubelet_size, cfg.patch_size
+    x = pixels.reshape(B, F // t, t, C, H // p, p, W // p, p)
+    x = x.permute(0, 1, 4, 6, 3, 2, 5, 7)          # B, f', hp, wp, C, t, i, j
+    return x.reshape(B * (F // t) * (H // p) * (W // p), C * t * p * p)
+
+
+def layer_norm(x, g, b, eps):
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), g, b, eps)
+
+
+def vit_layer(x: torch.Tensor, P: Dict[str, torch.Tensor], prefix: str, cfg: ViTCfg) -> torch.Tensor:
+    """One pre-LN block, `modeling_videomae.py:419-445` with `VideoMAESelfAttention` :230-266."""
+    B, N, D = x.shape
+    H = cfg.num_attention_heads
+    dh = D // H
+    h = layer_norm(x, P[prefix + "layernorm_before.weight"], P[prefix + "layernorm_before.bias"],
+                   cfg.layer_norm_eps)
+    q = h @ P[prefix + "attention.attention.query.weight"].T + P[prefix + "attention.attention.query.bias"]
+    k = h @ P[prefix + "attention.attention.key.weight"].T            # k bias is identically zero
+    v = h @ P[prefix + "attention.attention.value.weight"].T + P[prefix + "attention.attention.value.bias"]
+    q, k, v = (t.reshape(B, N, H, dh).permute(0, 2, 1, 3) for t in (q, k, v))
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    pr = torch.softmax(s, dim=-1)
+    o = (pr @ v).permute(0, 2, 1, 3).reshape(B, N, D)
+    y = x + o @ P[prefix + "attention.output.dense.weight"].T + P[prefix + "attention.output.dense.bias"]
+    h2 = layer_norm(y, P[prefix + "layernorm_after.weight"], P[prefix + "layernorm_after.bias"],
+                    cfg.layer_norm_eps)
+    a = torch.nn.functional.gelu(h2 @ P[prefix + "intermediate.dense.weight"].T + P[prefix + "intermediate.dense.bias"])
+    return y + a @ P[prefix + "output.dense.weight"].T + P[prefix + "output.dense.bias"]
+
+
+def videomae_encoder(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTCfg) -> torch.Tensor:
+    """`VideoMAEModel.forward` (modeling_videomae.py:592-715): patch-embed + sinusoid, 12 blocks,
+    no final LayerNorm because `use_mean_pooling=True` (:571-574)."""
+    B = pixels.shape[0]
+    N, D = cfg.num_tokens, cfg.hidden_size
+    cols = im2col(pixels, cfg)
+    w = P["video_mae.embeddings.patch_embeddings.projection.weight"].reshape(D, -1)
+    x = cols @ w.T + P["video_mae.embeddings.patch_embeddings.projection.bias"]
+    x = x.reshape(B, N, D) + sinusoid_table(N, D)
+    for i in range(cfg.num_hidden_layers):
+        x = vit_layer(x, P, f"video_mae.encoder.layer.{i}.", cfg)
+    return x
+
+
+def videomae_plugin_forward(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTCfg,
+                            freeze_encoder: bool = True) -> torch.Tensor:
+    """`src/model/videomae.py:16-32` from `pixel_values` on (the CPU preprocessing K0 is outside)."""
+    B = pixels.shape[0]
+    if freeze_encoder:
+        with torch.no_grad():
+            hid = videomae_encoder(pixels, P, cfg)
+    else:
+        hid = videomae_encoder(pixels, P, cfg)
+    z = hid.flatten(1) @ P["encoder.weight"].T + P["encoder.bias"]
+    r = z @ P["decoder.weight"].T + P["decoder.bias"]
+    return r.reshape(B, 100, -1)
+
+
+def linear_plugin_forward(x: torch.Tensor, P: Dict[str, torch.Tensor]) -> torch.Tensor:
+    """`src/model/linear.py:10-15`: ReLU after every hidden Linear, none after the encoder's
+    output layer nor the decoder's output layer."""
+    def mlp(h, prefix):
+        idx = sorted(int(k.split(".")[2]) for k in P if k.startswith(prefix) and k.endswith(".weight"))
+        for j, i in enumerate(idx):
+            h = h @ P[f"{prefix}{i}.weight"].T + P[f"{prefix}{i}.bias"]
+            if j < len(idx) - 1:
+                h = torch.relu(h)
+        return h
+    B = x.shape[0]
+    h = mlp(x.flatten(1), "encoder.layers.")
+    r = mlp(h, "decoder.layers.")
+    return r.reshape(B, 100, -1)
+
+
+def poisson_nll_mean(log_rate: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """`PoissonNLLLoss(reduction='none', log_input=True)(...).mean()`: mean(exp(x) - y*x)."""
+    return (torch.exp(log_rate) - target * log_rate).mean()
+
+
+# ----------------------------------------------------------------------------------------------
+# train-step restatement (loss curve oracle)
+# ----------------------------------------------------------------------------------------------
+def to_torch(params: Dict[str, np.ndarray], requires_grad=True) -> Dict[str, torch.Tensor]:
+    return {k: torch.tensor(v, dtype=torch.float32, requires_grad=requires_grad) for k, v in params.items()}
+
+
+def train_curve(forward, params: Dict[str, torch.Tensor], batches, lr=5e-5, wd=0.01, eps=1e-8,
+                warmup_pct=0.15, div_factor=10.0, trainable=None) -> List[float]:
+    """`src/train.py:44-57` (AdamW + OneCycleLR, total_steps = len(batches)) and the loop body of
+    `src/trainer/base.py:144-159`.  Returns the per-step training loss."""
+    names = list(params) if trainable is None else [n for n in params if trainable(n)]
+    opt = torch.optim.AdamW([params[n] for n in names], lr=lr, weight_decay=wd, eps=eps)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=len(batches), max_lr=lr,
+                                                pct_start=warmup_pct, div_factor=div_factor)
+    losses = []
+    for x, y in batches:
+        loss = poisson_nll_mean(forward(x, params), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(float(loss.item()))
+    return losses
+
+
+# ----------------------------------------------------------------------------------------------
+# fixture comparison helpers
+# ----------------------------------------------------------------------------------------------
+FULL_GRAD_LIMIT = 65536
+
+
+def summarize(name: str, t: np.ndarray, seed: int = 7) -> Dict[str, np.ndarray]:
+    """Full tensor when small, else (norm, 3 seeded projections, first 512 values)."""
+    t = np.array(t, dtype=np.float32, copy=True)       # never keep a view of a live .grad
+    if t.size <= FULL_GRAD_LIMIT:
+        return {"full/" + name: t}
+    flat = t.reshape(-1).astype(np.float64)
+    projs = np.array([float(flat @ prng.normal(seed, (flat.size,), f"{name}#proj{i}").astype(np.float64))
+                      for i in range(3)])
+    return {"norm/" + name: np.array([np.linalg.norm(flat)]), "proj/" + name: projs,
+            "head/" + name: t.reshape(-1)[:512].copy()}
+
+
+def compare_summary(name: str, t: np.ndarray, fx: Dict[str, np.ndarray], rtol: float, atol: float,
+                    seed: int = 7) -> Tuple[bool, str]:
+    t = np.asarray(t, dtype=np.float32)
+    if "full/" + name in fx:
+        ref = fx["full/" + name]
+        err = np.abs(t - ref)
+        ok = bool(np.all(err <= atol + rtol * np.abs(ref)))
+        return ok, f"{name}: max|d|={err.max():.3e} max|ref|={np.abs(ref).max():.3e}"
+    mine = summarize(name, t, seed)
+    msgs, ok = [], True
+    for key in ("norm/", "proj/", "head/"):
+        ref, got = fx[key + name], mine[key + name]
+        # a random projection of an error vector e has magnitude ~||e||, so projections (and the
+        # norm itself) are judged against the tensor norm; leading values against their own max.
+        scale = float(fx["norm/" + name][0]) if key != "head/" else float(np.abs(ref).max())
+        err = np.abs(got - ref).max()
+        good = err <= atol + rtol * max(scale, 1e-30)
+        ok &= bool(good)
+        msgs.append(f"{key}{name} max|d|={err:.3e} scale={scale:.3e}")
+    return ok, "; ".join(msgs)

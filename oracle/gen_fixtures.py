@@ -1,0 +1,227 @@
+"""Generate the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+TEST INFRASTRUCTURE ONLY.  Run once, in the build container where `/root/reference` exists:
+
+    python -m oracle.gen_fixtures
+
+What runs the reference here (nothing is copied out of it, only outputs are saved):
+  * `Linear` plugin: imported from `/root/reference/src/model/linear.py` and built from a
+    model YAML with the reference's own loader `src/utils/config_utils.py:59-75`.
+  * `VideoMAE` plugin: `src/model/videomae.py:4-32` cannot be constructed offline
+    (`from_pretrained("MCG-NJU/videomae-base")` at :7-8 needs the Hub, and :24 hard-codes
+    `.cuda()`), so its forward from `pixel_values` on is composed from the third-party encoder the
+    reference executes — the installed HF `transformers.VideoMAEModel` (5.15.0; reference pins
+    4.38.2, env.yaml:30) with eager attention and k-bias zeroed (4.38 uses a fixed zero k-bias,
+    modeling_videomae.py:233) — plus two `nn.Linear` layers exactly as `videomae.py:13-14,28-31`.
+  * Train loop: the body of `src/trainer/base.py:144-159` with the optimiser/scheduler of
+    `src/train.py:44-57` driving those modules.
+  * Config loader: the reference's `update_config`/`config_from_kwargs` over this repo's YAMLs.
+
+Inputs and weights come from `oracle.prng` (seeded by name), so only outputs are committed.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.dont_write_bytecode = True          # never write into /root/reference
+
+from oracle import cpu_ref, prng  # noqa: E402
+
+REF_SRC = "/root/reference/src"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden")
+CFG = os.path.join(ROOT, "video-spike_amd", "config")
+
+
+def _ref_imports():
+    if REF_SRC not in sys.path:
+        sys.path.insert(0, REF_SRC)
+    from model.linear import Linear                      # noqa: E402
+    from utils.config_utils import update_config, config_from_kwargs   # noqa: E402
+    return Linear, update_config, config_from_kwargs
+
+
+def _grads_summary(named_grads):
+    out = {}
+    for name, g in named_grads.items():
+        out.update(cpu_ref.summarize(name, g.detach().numpy()))
+    return out
+
+
+def _ref_train_loop(module, batches, trainable, lr, wd=0.01, eps=1e-8, warmup_pct=0.15, div_factor=10):
+    """Body of src/trainer/base.py:144-159 with src/train.py:44-59's optimiser/scheduler/criterion."""
+    for p in module.parameters():                         # start from a clean slate (no stale .grad)
+        p.grad = None
+    optimizer = torch.optim.AdamW(trainable, lr=lr, weight_decay=wd, eps=eps)
+    sched = torch.optim.lr_scheduler.OneCycleLR(optimizer=optimizer, total_steps=len(batches), max_lr=lr,
+                                                pct_start=warmup_pct, div_factor=div_factor)
+    criterion = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)
+    losses = []
+    module.train()
+    for x, y in batches:
+        outputs = module(x)
+        loss = criterion(outputs, y).mean()
+        loss.backward()
+        optimizer.step()
+        sched.step()
+        optimizer.zero_grad()
+        losses.append(loss.item())
+    return np.array(losses, dtype=np.float64)
+
+
+# ----------------------------------------------------------------------------------------------
+def gen_linear():
+    Linear, update_config, config_from_kwargs = _ref_imports()
+    B, T, HW, n = 4, 8, 64, 16
+    config = config_from_kwargs({"model": "include:" + os.path.join(CFG, "model", "linear_video.yaml")})
+    config = update_config(os.path.join(CFG, "train", "linear_video.yaml"), config)
+    config["model"]["encoder"]["input_dim"] = T * HW * HW
+    config["model"]["decoder"]["output_dim"] = 100 * n
+    module = Linear(config.model)
+    shapes = {k: tuple(v.shape) for k, v in module.state_dict().items()}
+    params = cpu_ref.make_linear_params(shapes)
+    module.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+
+    video = np.floor(prng.uniform(0, B * T * HW * HW, "video") * 256.0).astype(np.float32).reshape(B, T, 1, HW, HW)
+    ap = prng.spike_targets(1, (B, 100, n))
+    x, y = torch.from_numpy(video), torch.from_numpy(ap)
+    inp = x.flatten(1)                                   # base.py:64-67 (Linear: cat of flattened modalities)
+    out = module(inp)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(_grads_summary({k: p.grad for k, p in module.named_parameters()}))
+
+    # 5-step loss curve (fresh weights); lr small because the raw 0..255 inputs make the first layer stiff
+    module.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    batches = []
+    for s in range(5):
+        v = np.floor(prng.uniform(100 + s, B * T * HW * HW, "video") * 256.0).astype(np.float32)
+        batches.append((torch.from_numpy(v.reshape(B, T, 1, HW, HW)).flatten(1),
+                        torch.from_numpy(prng.spike_targets(200 + s, (B, 100, n)))))
+    fx["curve"] = _ref_train_loop(module, batches, list(module.parameters()), lr=1e-6)
+    np.savez(os.path.join(OUT, "linear_f.npz"), **fx)
+    print("linear_f", fx["loss"], fx["curve"])
+
+
+def _hf_encoder(cfg: cpu_ref.ViTCfg):
+    from transformers import VideoMAEConfig, VideoMAEModel
+    hc = VideoMAEConfig(image_size=cfg.image_size, patch_size=cfg.patch_size, num_channels=cfg.num_channels,
+                        num_frames=cfg.num_frames, tubelet_size=cfg.tubelet_size, hidden_size=cfg.hidden_size,
+                        num_hidden_layers=cfg.num_hidden_layers, num_attention_heads=cfg.num_attention_heads,
+                        intermediate_size=cfg.intermediate_size, hidden_act="gelu", hidden_dropout_prob=0.0,
+                        attention_probs_dropout_prob=0.0, layer_norm_eps=cfg.layer_norm_eps, qkv_bias=True,
+                        use_mean_pooling=True)
+    hc._attn_implementation = "eager"
+    return VideoMAEModel(hc)
+
+
+class _RefVideoMAEHead(torch.nn.Module):
+    """`src/model/videomae.py:13-14,26-31` from pixel_values on (encoder = HF VideoMAEModel)."""
+
+    def __init__(self, cfg, enc_out, n_out):
+        super().__init__()
+        self.video_mae = _hf_encoder(cfg)
+        self.encoder = torch.nn.Linear(cfg.num_tokens * cfg.hidden_size, enc_out)
+        self.decoder = torch.nn.Linear(enc_out, 100 * n_out)
+        self.freeze = True
+
+    def forward(self, pixel_values):
+        B = pixel_values.shape[0]
+        if self.freeze:
+            with torch.no_grad():
+                outputs = self.video_mae(pixel_values=pixel_values).last_hidden_state.flatten(1)
+        else:
+            outputs = self.video_mae(pixel_values=pixel_values).last_hidden_state.flatten(1)
+        outputs = self.encoder(outputs)
+        outputs = self.decoder(outputs)
+        return outputs.reshape(B, 100, -1)
+
+
+def _load_vit(module, cfg, enc_out, n_out):
+    params = cpu_ref.make_vit_params(cfg, enc_out, n_out)
+    sd = {k: torch.from_numpy(v) for k, v in params.items()}
+    for i in range(cfg.num_hidden_layers):                # installed HF has a learnable k bias: pin to 0
+        sd[f"video_mae.encoder.layer.{i}.attention.attention.key.bias"] = torch.zeros(cfg.hidden_size)
+    missing, unexpected = module.load_state_dict(sd, strict=False)
+    assert not unexpected and not missing, (missing, unexpected)
+    return params
+
+
+def gen_vit_small():
+    cfg, B, enc_out, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 64, 16
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    m.freeze = False                                      # north-star: encoder fwd+bwd
+    hid = m.video_mae(pixel_values=px).last_hidden_state
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"last_hidden": hid.detach().numpy(), "log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    grads = {k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}
+    fx.update(_grads_summary(grads))
+
+    def batches(base):
+        return [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=base + s)),
+                 torch.from_numpy(prng.spike_targets(base + 50 + s, (B, 100, n)))) for s in range(4)]
+    # frozen (reference default): AdamW over model.parameters(); frozen ones have grad None
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = True
+    for p in m.video_mae.parameters():
+        p.requires_grad = False
+    fx["curve_frozen"] = _ref_train_loop(m, batches(300), list(m.parameters()), lr=1e-5)
+    # trainable encoder (north-star flag); k bias excluded (4.38 has none)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    for k, p in m.named_parameters():
+        p.requires_grad = ".key.bias" not in k
+    fx["curve_train"] = _ref_train_loop(m, batches(300), [p for p in m.parameters() if p.requires_grad], lr=1e-5)
+    np.savez(os.path.join(OUT, "vit_small.npz"), **fx)
+    print("vit_small", fx["loss"], fx["curve_frozen"], fx["curve_train"])
+
+
+def gen_vit_tiny1l():
+    cfg = cpu_ref.ViTCfg(hidden_size=192, num_attention_heads=3, intermediate_size=768, num_hidden_layers=1)
+    B, enc_out, n = 1, 64, 8
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    with torch.no_grad():
+        hid = m.video_mae(pixel_values=px).last_hidden_state
+        out = m(px)
+        loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    fx = {"log_rates": out.numpy(), "loss": np.array([loss.item()])}
+    fx.update(cpu_ref.summarize("last_hidden", hid.numpy()))
+    np.savez(os.path.join(OUT, "vit_tiny1l.npz"), **fx)
+    print("vit_tiny1l", fx["loss"])
+
+
+def gen_configs():
+    _, update_config, config_from_kwargs = _ref_imports()
+    res = {}
+    for m in ("linear_video", "vmae_video", "vmae_tiny"):
+        t = "vmae_video" if m.startswith("vmae") else m
+        config = config_from_kwargs({"model": "include:" + os.path.join(CFG, "model", m + ".yaml")})
+        config = update_config(os.path.join(CFG, "train", t + ".yaml"), config)
+        res[f"{m}+{t}"] = json.loads(json.dumps(config))
+    with open(os.path.join(OUT, "configs.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("configs", list(res))
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l"]
+    for w in which:
+        globals()["gen_" + w]()

@@ -1,0 +1,100 @@
+"""Pin the CPU restatement (oracle/cpu_ref.py) to fixtures generated from the reference itself
+(oracle/gen_fixtures.py).  Runs on CPU, no GPU, no /root/reference needed."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, prng
+
+
+def test_prng_is_deterministic_and_sane():
+    a = prng.normal(3, (1000,), "x")
+    b = prng.normal(3, (1000,), "x")
+    c = prng.normal(3, (1000,), "y")
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+    z = prng.normal(0, (200000,), "z")
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    y = prng.spike_targets(1, (4, 100, 16))
+    assert y.min() >= 0 and np.all(y == np.round(y))
+
+
+def test_linear_plugin_matches_reference(golden):
+    fx = golden("linear_f.npz")
+    B, T, HW, n = 4, 8, 64, 16
+    shapes = cpu_ref.linear_param_shapes(T * HW * HW, [256, 128], 64, [128, 256], 100 * n)
+    P = cpu_ref.to_torch(cpu_ref.make_linear_params(shapes))
+    video = np.floor(prng.uniform(0, B * T * HW * HW, "video") * 256.0).astype(np.float32).reshape(B, T, 1, HW, HW)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    out = cpu_ref.linear_plugin_forward(torch.from_numpy(video), P)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    loss.backward()
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-5, atol=1e-5)
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-6 * abs(fx["loss"][0])
+    for k, p in P.items():
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=1e-4, atol=1e-7)
+        assert ok, msg
+
+
+def test_linear_loss_curve_matches_reference(golden):
+    fx = golden("linear_f.npz")
+    B, T, HW, n = 4, 8, 64, 16
+    shapes = cpu_ref.linear_param_shapes(T * HW * HW, [256, 128], 64, [128, 256], 100 * n)
+    P = cpu_ref.to_torch(cpu_ref.make_linear_params(shapes))
+    batches = []
+    for s in range(5):
+        v = np.floor(prng.uniform(100 + s, B * T * HW * HW, "video") * 256.0).astype(np.float32)
+        batches.append((torch.from_numpy(v.reshape(B, T, 1, HW, HW)),
+                        torch.from_numpy(prng.spike_targets(200 + s, (B, 100, n)))))
+    curve = cpu_ref.train_curve(cpu_ref.linear_plugin_forward, P, batches, lr=1e-6)
+    np.testing.assert_allclose(curve, fx["curve"], rtol=1e-5)
+
+
+def _vit_small_setup(trainable_encoder=True):
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    return cfg, P, px, y
+
+
+def test_vit_small_forward_backward_matches_reference(golden):
+    fx = golden("vit_small.npz")
+    cfg, P, px, y = _vit_small_setup()
+    hid = cpu_ref.videomae_encoder(px, P, cfg)
+    np.testing.assert_allclose(hid.detach().numpy(), fx["last_hidden"], rtol=1e-4, atol=1e-5)
+    out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-5 * abs(fx["loss"][0])
+    loss.backward()
+    for k, p in P.items():
+        if ".key.bias" in k:
+            continue
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=2e-4, atol=1e-7)
+        assert ok, msg
+
+
+@pytest.mark.parametrize("frozen", [True, False])
+def test_vit_small_loss_curve_matches_reference(golden, frozen):
+    fx = golden("vit_small.npz")
+    cfg, P, _, _ = _vit_small_setup()
+    B, n = 2, 16
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=300 + s)),
+                torch.from_numpy(prng.spike_targets(350 + s, (B, 100, n)))) for s in range(4)]
+    fwd = lambda x, PP: cpu_ref.videomae_plugin_forward(x, PP, cfg, freeze_encoder=frozen)  # noqa: E731
+    trainable = (lambda k: not k.startswith("video_mae.")) if frozen else None
+    curve = cpu_ref.train_curve(fwd, P, batches, lr=1e-5, trainable=trainable)
+    np.testing.assert_allclose(curve, fx["curve_frozen" if frozen else "curve_train"], rtol=1e-4)
+
+
+def test_vit_tiny_full_tokens_matches_reference(golden):
+    fx = golden("vit_tiny1l.npz")
+    cfg = cpu_ref.ViTCfg(hidden_size=192, num_attention_heads=3, intermediate_size=768, num_hidden_layers=1)
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, 8), requires_grad=False)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 1))
+    with torch.no_grad():
+        hid = cpu_ref.videomae_encoder(px, P, cfg)
+        out = cpu_ref.videomae_plugin_forward(px, P, cfg)
+    ok, msg = cpu_ref.compare_summary("last_hidden", hid.numpy(), fx, rtol=1e-4, atol=1e-6)
+    assert ok, msg
+    np.testing.assert_allclose(out.numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
