@@ -1,0 +1,221 @@
+/*
+ * vspike.h — C-ABI of the MI355X-native video->spike training hot path (libvspike.so).
+ *
+ * Plain pointers and sizes only: no torch, no HIP types in the signatures.  Every entry point
+ * enqueues work on the caller's HIP stream (`stream` is a hipStream_t, NULL = legacy default
+ * stream), never allocates, never synchronises, and is therefore hipGraph-capturable.  Device
+ * buffers are owned by the caller (the PyTorch caching allocator on the Python side).
+ *
+ * Return value: VS_OK (0) on success, VS_EINVAL (-1) for a rejected argument (shape, dtype,
+ * alignment, null pointer — nothing was launched), or a positive hipError_t from the launch.
+ * `vs_last_error()` returns a static string describing the last rejection.
+ *
+ * The reference (PPWangyc/video-spike) is pure Python; every op here replaces a torch/cuBLAS/
+ * cuDNN kernel that its hot path runs.  Each declaration cites the reference line it replaces
+ * (paths relative to the reference repo root; "mv" = src/model/videomae/modeling_videomae.py,
+ * the vendored spec of the HF encoder the reference executes).
+ */
+#ifndef VSPIKE_H
+#define VSPIKE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VS_OK 0
+#define VS_EINVAL (-1)
+
+/* element types */
+#define VS_F32 0
+#define VS_BF16 1
+
+int vs_version(void);                 /* ABI version (monotonic) */
+const char* vs_last_error(void);      /* static string, last VS_EINVAL reason */
+int vs_device_arch(char* buf, int n); /* writes gcnArchName of the current device */
+/* sizeof() of the ABI structs, so bindings can verify their mirrors: 0 = vs_gemm_desc,
+ * 1 = vs_vit_layer, 2 = vs_vit_layer_grad; -1 for an unknown id */
+int vs_struct_size(int which);
+
+/* ------------------------------------------------------------------------------------------
+ * GEMM with fused epilogue:  C[M,N] = epilogue( alpha * sum_k A(m,k) * B(k,n) )
+ * Replaces every nn.Linear / F.linear on the path and its autograd backward:
+ *   mv:233-236 (Q,K,V projections), mv:312-319 (attention output dense), mv:373-383 (fc1+GELU),
+ *   mv:390-397 (fc2 + residual), mv:176-181/194-195 (Conv3d patch-embed as im2col GEMM, + the
+ *   sinusoid table mv:135 via VS_EPI_POS), src/model/videomae.py:13-14,28-31 (head Linears),
+ *   src/model/linear.py:24-32,45-53 (Linear plugin MLP + ReLU), and their dX/dW products
+ *   (accelerator.backward, src/trainer/base.py:150).
+ * Operand layouts:
+ *   a_kcontig=1: A(m,k) = a[m*lda + k]        a_kcontig=0: A(m,k) = a[k*lda + m]
+ *   b_kcontig=1: B(k,n) = b[n*ldb + k]  (nn.Linear weight [N,K])   b_kcontig=0: B(k,n) = b[k*ldb + n]
+ * Operands are VS_F32 (exact f32 MFMA 16x16x4) or VS_BF16 (MFMA 16x16x32, f32 accumulate).
+ * Contiguous extents and leading dims must be multiples of 8 (bf16) / 4 (f32) elements and
+ * base pointers 16-byte aligned.
+ * ------------------------------------------------------------------------------------------ */
+#define VS_EPI_BIAS      0x001u  /* + bias[n] (f32)                                            */
+#define VS_EPI_GELU      0x002u  /* aux_out(m,n) = v (pre-activation); v = gelu_erf(v)          */
+#define VS_EPI_RELU      0x004u  /* v = max(v, 0)                                              */
+#define VS_EPI_RESIDUAL  0x008u  /* + residual[m*ld_residual + n] (f32)                        */
+#define VS_EPI_POS       0x010u  /* + pos[(m % pos_rows)*N + n] (f32)                          */
+#define VS_EPI_GELU_BWD  0x020u  /* v *= gelu_erf'(aux_in(m,n))                                */
+#define VS_EPI_RELU_BWD  0x040u  /* v = aux_in(m,n) > 0 ? v : 0                                */
+#define VS_EPI_ATOMIC    0x080u  /* C(m,n) += v by f32 atomics (split-K); C must be f32       */
+#define VS_EPI_ACCUM     0x100u  /* C(m,n) += v (plain read-modify-write); C must be f32      */
+
+typedef struct vs_gemm_desc {
+  int32_t dtype;        /* operand element type, VS_F32 or VS_BF16 */
+  int32_t out_dtype;    /* C element type */
+  int32_t a_kcontig;
+  int32_t b_kcontig;
+  int64_t M, N, K;
+  const void* a;   int64_t lda;
+  const void* b;   int64_t ldb;
+  void* c;         int64_t ldc;
+  uint32_t epilogue;    /* VS_EPI_* bits */
+  float alpha;
+  const float* bias;                          /* [N] */
+  const float* residual; int64_t ld_residual; /* [M, ld] f32 */
+  const float* pos;      int64_t pos_rows;    /* [pos_rows, N] f32 */
+  const void* aux_in;    int64_t ld_aux_in;   /* operand dtype */
+  void* aux_out;         int64_t ld_aux_out;  /* operand dtype */
+  int32_t split_k;      /* 0 = auto; >1 needs VS_EPI_ATOMIC */
+  int32_t reserved;
+} vs_gemm_desc;
+
+int vs_gemm(const vs_gemm_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LayerNorm over the last dim, eps = 1e-12 in the reference (mv:416-417, nn.LayerNorm).
+ * x is the f32 residual stream; y is written in `y_dtype`; mean/rstd [rows] f32 are saved for
+ * the backward.  Backward: dx = dres + LN'(dy); dgamma/dbeta are ACCUMULATED (f32 atomics).
+ * dx_lp (optional) receives a bf16 copy of dx for the next bf16 GEMM.
+ * ------------------------------------------------------------------------------------------ */
+int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, const float* x, int64_t ldx,
+                     const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
+                     float* mean, float* rstd, void* stream);
+int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, const float* x,
+                     int64_t ldx, const float* mean, const float* rstd, const float* gamma,
+                     const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
+                     float* dgamma, float* dbeta, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Non-causal multi-head attention, head dim 64 (mv:243-258; SDPA variant mv:286-294):
+ *   O = softmax(Q K^T * scale) V per (batch, head), scale = 1/sqrt(64) = 0.125.
+ * qkv: [B*N, 3*H*64] rows; Q of head h at column h*64, K at (H+h)*64, V at (2H+h)*64.
+ * o: [B*N, H*64]; lse: [B, H, N] f32 natural-log sum-exp of the scaled scores (saved for bwd).
+ * Backward writes dQ, dK, dV into dqkv (same layout as qkv); workspace is f32 scratch of
+ * vs_attn_bwd_workspace_bytes().  dtype VS_BF16 runs the MFMA flash kernels; VS_F32 runs exact
+ * f32 reference-grade kernels (the 1e-4 parity mode).
+ * ------------------------------------------------------------------------------------------ */
+int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv,
+                int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, void* stream);
+size_t vs_attn_bwd_workspace_bytes(int64_t B, int64_t N, int64_t H, int64_t Dh);
+int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv,
+                int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
+                const float* lse, void* dqkv, int64_t ld_dqkv, void* workspace, float scale,
+                void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Tubelet patch gather (im2col) for the Conv3d patch embedding (mv:176-181, 194-195):
+ * pixels (B, F, C, H, W) f32 -> cols [B*N, C*t*p*p] in `out_dtype`; token n = (f', hp, wp),
+ * column = (c, t, i, j) = the Conv3d weight's flatten order.
+ * ------------------------------------------------------------------------------------------ */
+int vs_patch_im2col(int32_t out_dtype, int64_t B, int64_t F, int64_t C, int64_t H, int64_t W,
+                    int64_t tubelet, int64_t patch, const float* pixels, void* cols, void* stream);
+
+/* Fixed sinusoid position table (mv:101-112), f32 [n_pos, dim] (computed in f64, rounded). */
+int vs_sinusoid_table(int64_t n_pos, int64_t dim, float* out, void* stream);
+
+/* out[c] += sum_r x[r*ldx + c] for c < cols (bias gradients); x in `dtype`. */
+int vs_colsum(int32_t dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, float* out,
+              void* stream);
+
+/* element-wise cast between VS_F32 and VS_BF16 (round to nearest even) */
+int vs_cast(int32_t in_dtype, int32_t out_dtype, int64_t n, const void* in, void* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused PoissonNLLLoss(log_input=True) + mean + gradient (src/train.py:59,
+ * src/trainer/base.py:141-143):  loss = mean(exp(x) - y*x);  dx = grad_scale*(exp(x) - y)/n.
+ * loss_out: one f32 (deterministic two-stage reduction).  dx may be NULL (forward only).
+ * workspace: >= vs_poisson_workspace_bytes(n).
+ * ------------------------------------------------------------------------------------------ */
+size_t vs_poisson_workspace_bytes(int64_t n);
+int vs_poisson_nll(int64_t n, const float* log_rate, const float* target, float* loss_out,
+                   float* dx, float grad_scale, void* workspace, void* stream);
+/* dx = g[0] * (exp(x) - y) / n with the upstream scalar gradient read from device memory */
+int vs_poisson_nll_bwd(int64_t n, const float* log_rate, const float* target,
+                       const float* grad_out, float* dx, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Fused AdamW step (torch.optim.AdamW semantics, src/train.py:44-49) over a flat f32 buffer.
+ * hyper (device f32[8]): lr, beta1, beta2, eps, weight_decay, step (>=1), grad_scale, unused.
+ * param_lp (optional): bf16 shadow of param written in the same pass.
+ * ------------------------------------------------------------------------------------------ */
+int vs_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+             void* param_lp, const float* hyper, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * One pre-LN ViT block (mv:419-445) as a native executor: LN1 -> QKV GEMM -> attention ->
+ * out-proj + residual -> LN2 -> fc1+GELU -> fc2 + residual, and its backward.  All tensors are
+ * caller-owned; `dtype` is the activation/weight element type (residual stream, LN statistics,
+ * softmax statistics and gradients of weights are f32 in both modes).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vs_vit_layer {
+  int32_t dtype;
+  int32_t heads;
+  int64_t batch, tokens, hidden, mlp;        /* M = batch*tokens rows */
+  float ln_eps;
+  float attn_scale;
+  /* weights: matrices in `dtype` ([out, in] nn.Linear layout), vectors f32 */
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  const void* w_qkv;  const float* b_qkv;    /* [3D, D], [3D] (k third == 0) */
+  const void* w_proj; const float* b_proj;   /* [D, D] */
+  const void* w_fc1;  const float* b_fc1;    /* [F, D] */
+  const void* w_fc2;  const float* b_fc2;    /* [D, F] */
+  /* activations (saved for the backward) */
+  const float* x_in;                         /* [M, D] f32 */
+  void* h1;  float* mean1; float* rstd1;     /* [M, D] dtype; [M] */
+  void* qkv; void* attn_o; float* lse;       /* [M, 3D]; [M, D]; [B, H, N] */
+  float* y;                                  /* [M, D] f32 (after attention residual) */
+  void* h2;  float* mean2; float* rstd2;
+  void* a_pre; void* a_act;                  /* [M, F] dtype */
+  float* x_out;                              /* [M, D] f32 */
+} vs_vit_layer;
+
+typedef struct vs_vit_layer_grad {
+  /* weight gradients (f32, ACCUMULATED) */
+  float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  float *w_qkv, *b_qkv, *w_proj, *b_proj, *w_fc1, *b_fc1, *w_fc2, *b_fc2;
+  /* activation gradients */
+  const float* dx_out;  const void* dx_out_lp;   /* [M, D] f32 and a `dtype` copy (bf16 mode) */
+  float* dx_in;         void* dx_in_lp;          /* outputs, same shapes */
+  /* scratch (caller-owned): */
+  void* d_a;            /* [M, F] dtype: d(pre-activation of fc1) */
+  float* d_h;           /* [M, D] f32: grad wrt LN outputs */
+  float* dy;  void* dy_lp;                       /* [M, D] f32 + dtype copy */
+  void* d_o;            /* [M, D] dtype */
+  void* d_qkv;          /* [M, 3D] dtype */
+  void* attn_ws;        /* vs_attn_bwd_workspace_bytes */
+} vs_vit_layer_grad;
+
+int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
+int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Kernel timing (bench instrumentation).  When enabled, the executor brackets every launch of
+ * the tracked kernels with hipEvents on the launch stream.  vs_timing_collect() synchronises on
+ * the recorded events and returns per-kernel launch count and total milliseconds.
+ * ------------------------------------------------------------------------------------------ */
+#define VS_TIMER_ATTN_FWD 0
+#define VS_TIMER_ATTN_BWD 1
+#define VS_TIMER_GEMM     2
+#define VS_TIMER_COUNT    3
+int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
+int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VSPIKE_H */

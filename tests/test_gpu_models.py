@@ -1,0 +1,183 @@
+"""Model-level parity: the plugins (through libvspike) vs golden fixtures generated from the
+reference (oracle/gen_fixtures.py) and vs the CPU restatement (oracle/cpu_ref.py).
+
+Tolerances (north star: outputs within 1e-4 relative in fp32, loss curve within 1e-3):
+  * fp32 mode: log-rates / hidden states 1e-4 relative to max|ref|; grads 1e-3 of the tensor norm
+    (norm-relative, see cpu_ref.compare_summary); loss curves 1e-3 relative.
+  * bf16 mode: log-rates 3e-2 relative to max|ref|, loss 1e-2 relative (bf16 activations).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _vit_model(cfg: cpu_ref.ViTCfg, enc_out, n, dtype="fp32", freeze=False):
+    from vspike import VideoMAE
+    conf = {"model_class": "VideoMAE", "freeze_encoder": freeze, "compute_dtype": dtype,
+            "backbone": {k: getattr(cfg, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                       "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                       "num_attention_heads", "intermediate_size",
+                                                       "layer_norm_eps")},
+            "encoder": {"output_dim": enc_out}, "decoder": {"output_dim": 100 * n}}
+    m = VideoMAE(conf).to(DEV)
+    m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_vit_params(cfg, enc_out, n).items()})
+    return m
+
+
+def _maxrel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_vit_small_fp32_forward_backward_matches_reference(golden):
+    from vspike import poisson_nll_mean
+    fx = golden("vit_small.npz")
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    out = m(px)
+    assert _maxrel(out.detach().cpu(), fx["log_rates"]) < 1e-4
+    loss = poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) < 1e-5 * abs(fx["loss"][0])
+    loss.backward()
+    sd = {}
+    # map flat grads back to reference names
+    for name, which, slot, rows in m.layout.hf_items():
+        flat = m.enc_flat.grad if which == "enc" else m.head_flat.grad
+        t = (m.layout.enc if which == "enc" else m.layout.head).view(flat, slot)
+        sd[name] = (t if rows is None else t[rows]).detach().cpu().numpy()
+    for name, g in sd.items():
+        shape = cpu_ref.vit_param_shapes(cfg, 64, n)[name]
+        ok, msg = cpu_ref.compare_summary(name, g.reshape(shape), fx, rtol=1e-3, atol=1e-8)
+        assert ok, msg
+
+
+def test_vit_small_bf16_close_to_reference(golden):
+    fx = golden("vit_small.npz")
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n, dtype="bf16")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    out = m(px)
+    assert _maxrel(out.detach().cpu(), fx["log_rates"]) < 3e-2
+
+
+def test_vit_tiny_full_tokens_fp32(golden):
+    fx = golden("vit_tiny1l.npz")
+    cfg = cpu_ref.ViTCfg(hidden_size=192, num_attention_heads=3, intermediate_size=768, num_hidden_layers=1)
+    m = _vit_model(cfg, 64, 8, freeze=True)
+    with torch.no_grad():
+        out = m(torch.from_numpy(cpu_ref.make_pixels(cfg, 1)).to(DEV))
+    assert _maxrel(out.cpu(), fx["log_rates"]) < 1e-4
+
+
+@pytest.mark.parametrize("frozen", [True, False])
+def test_vit_small_loss_curve_matches_reference(golden, frozen):
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_small.npz")
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n, freeze=frozen)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=4, max_lr=1e-5, pct_start=0.15, div_factor=10)
+    losses = []
+    for s in range(4):
+        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=300 + s)).to(DEV)
+        y = torch.from_numpy(prng.spike_targets(350 + s, (B, 100, n))).to(DEV)
+        loss = poisson_nll_mean(m(px), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    ref = fx["curve_frozen" if frozen else "curve_train"]
+    np.testing.assert_allclose(losses, ref, rtol=1e-3)
+
+
+def test_linear_plugin_matches_reference(golden):
+    from vspike import Linear, poisson_nll_mean
+    fx = golden("linear_f.npz")
+    B, T, HW, n = 4, 8, 64, 16
+    conf = {"model_class": "Linear",
+            "encoder": {"input_dim": T * HW * HW, "hidden_dims": [256, 128], "output_dim": 64, "layer_num": 2},
+            "decoder": {"input_dim": 64, "hidden_dims": [128, 256], "output_dim": 100 * n, "layer_num": 2}}
+    m = Linear(conf)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_linear_params(shapes).items()})
+    m = m.to(DEV)
+    video = np.floor(prng.uniform(0, B * T * HW * HW, "video") * 256.0).astype(np.float32).reshape(B, T, 1, HW, HW)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    out = m(torch.from_numpy(video).to(DEV))
+    assert _maxrel(out.detach().cpu(), fx["log_rates"]) < 1e-4
+    loss = poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) < 1e-5
+    loss.backward()
+    for k, p in m.named_parameters():
+        ok, msg = cpu_ref.compare_summary(k, p.grad.cpu().numpy(), fx, rtol=1e-3, atol=1e-8)
+        assert ok, msg
+
+
+def test_linear_loss_curve_matches_reference(golden):
+    from vspike import FusedAdamW, Linear, poisson_nll_mean
+    fx = golden("linear_f.npz")
+    B, T, HW, n = 4, 8, 64, 16
+    conf = {"model_class": "Linear",
+            "encoder": {"input_dim": T * HW * HW, "hidden_dims": [256, 128], "output_dim": 64, "layer_num": 2},
+            "decoder": {"input_dim": 64, "hidden_dims": [128, 256], "output_dim": 100 * n, "layer_num": 2}}
+    m = Linear(conf)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_linear_params(shapes).items()})
+    m = m.to(DEV)
+    opt = FusedAdamW(m.parameters(), lr=1e-6, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=5, max_lr=1e-6, pct_start=0.15, div_factor=10)
+    losses = []
+    for s in range(5):
+        v = np.floor(prng.uniform(100 + s, B * T * HW * HW, "video") * 256.0).astype(np.float32)
+        y = torch.from_numpy(prng.spike_targets(200 + s, (B, 100, n))).to(DEV)
+        loss = poisson_nll_mean(m(torch.from_numpy(v.reshape(B, T, 1, HW, HW)).to(DEV)), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, fx["curve"], rtol=1e-3)
+
+
+def test_vit_bf16_trains_and_matches_fp32_gradients_direction():
+    """bf16 mode at a larger size: gradients agree with the fp32 mode's (cosine > 0.99)."""
+    from vspike import poisson_nll_mean
+    cfg = cpu_ref.ViTCfg(hidden_size=192, num_attention_heads=3, intermediate_size=768, num_hidden_layers=2)
+    B, n = 2, 8
+    m32 = _vit_model(cfg, 64, n, dtype="fp32")
+    m16 = _vit_model(cfg, 64, n, dtype="bf16")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    for m in (m32, m16):
+        poisson_nll_mean(m(px), y).backward()
+    for a, b in ((m32.enc_flat.grad, m16.enc_flat.grad), (m32.head_flat.grad, m16.head_flat.grad)):
+        cos = torch.nn.functional.cosine_similarity(a.double(), b.double(), dim=0).item()
+        assert cos > 0.99, cos
+
+
+def test_state_dict_roundtrip_and_pickle(tmp_path):
+    cfg = cpu_ref.VIT_SMALL_FIXTURE
+    m = _vit_model(cfg, 64, 16)
+    sd = m.reference_state_dict()
+    ref = cpu_ref.make_vit_params(cfg, 64, 16)
+    for k, v in ref.items():
+        assert np.array_equal(sd[k].cpu().numpy(), v), k
+    torch.save({"model": m, "epoch": 0}, tmp_path / "m.pt")      # src/trainer/base.py:285-291
+    m2 = torch.load(tmp_path / "m.pt", weights_only=False)["model"]    # our own file
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 1)).to(DEV)
+    with torch.no_grad():
+        assert torch.equal(m(px), m2(px))

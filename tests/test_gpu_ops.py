@@ -1,0 +1,276 @@
+"""Op-level parity of the HIP kernels (through the C-ABI) against torch-CPU references.
+
+f32 ops: within 1e-5 relative (exact-f32 MFMA / f32 VALU).  bf16 ops: inputs are rounded to bf16
+first and the CPU reference runs in f32/f64 on those same values; outputs are checked against a
+tolerance stated per test (f32 accumulation; bf16 rounding of outputs ~4e-3 relative).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vspike import _lib
+    _lib.lib()
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _rand(*shape, dtype=torch.float32, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+GEMM_SHAPES = [(64, 64, 64), (200, 136, 72), (25, 40, 16), (1568, 192, 192), (7, 576, 192), (256, 64, 2048)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("shape", GEMM_SHAPES)
+def test_gemm_layouts(dtype, akc, bkc, shape):
+    from vspike import ops
+    M, N, K = shape
+    vec = 8 if dtype == torch.bfloat16 else 4
+    if (not akc and M % vec) or (not bkc and N % vec) or (K % vec and (akc or bkc)):
+        pytest.skip("contiguous extent must be a multiple of 16 bytes")
+    A = _rand(M, K, seed=1).to(dtype).float()
+    B = _rand(K, N, seed=2).to(dtype).float()
+    ref = A.double() @ B.double()
+    a_dev = (A if akc else A.t().contiguous()).to(dtype).to(DEV)
+    b_dev = (B.t().contiguous() if bkc else B).to(dtype).to(DEV)
+    c = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.gemm(a_dev, b_dev, c, M=M, N=N, K=K, a_kcontig=akc, b_kcontig=bkc, lda=a_dev.stride(0),
+             ldb=b_dev.stride(0), ldc=N)
+    torch.cuda.synchronize()
+    # error bound of an f32-accumulated dot product over K terms
+    bound = 1e-5 * math.sqrt(K) / 8 + 1e-6
+    err = ((c.double().cpu() - ref).abs() / (A.abs().double() @ B.abs().double()).clamp_min(1e-30)).max().item()
+    assert err < bound, (err, bound)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    from vspike import ops, _lib as L
+    M, N, K = 300, 192, 128
+    x = _rand(M, K, seed=3).to(dtype)
+    w = _rand(N, K, seed=4, scale=0.1).to(dtype)
+    bias = _rand(N, seed=5)
+    res = _rand(M, N, seed=6)
+    pos = _rand(100, N, seed=7)
+    pre_ref = x.double() @ w.double().t() + bias.double()
+    dev = lambda t: t.to(DEV)  # noqa: E731
+    # bias + pos
+    c = torch.empty(M, N, device=DEV)
+    ops.linear(dev(x), dev(w), c, bias=dev(bias), epilogue=L.EPI_POS, pos=dev(pos), pos_rows=100)
+    ref = pre_ref + pos.double()[torch.arange(M) % 100]
+    assert rel(c, ref) < 1e-5
+    # bias + gelu (aux_out = pre-activation in operand dtype) + residual
+    a = torch.empty(M, N, dtype=dtype, device=DEV)
+    pre = torch.empty(M, N, dtype=dtype, device=DEV)
+    ops.linear(dev(x), dev(w), a, bias=dev(bias), epilogue=L.EPI_GELU, aux_out=pre, ld_aux_out=N)
+    tol = 1e-5 if dtype == torch.float32 else 8e-3
+    assert rel(pre.float(), pre_ref) < tol
+    assert rel(a.float(), torch.nn.functional.gelu(pre_ref)) < tol
+    r = torch.empty(M, N, device=DEV)
+    ops.linear(dev(x), dev(w), r, bias=dev(bias), epilogue=L.EPI_RESIDUAL, residual=dev(res), ld_residual=N)
+    assert rel(r, pre_ref + res.double()) < 1e-5
+    # relu and relu-bwd / gelu-bwd masks
+    rl = torch.empty(M, N, device=DEV)
+    ops.linear(dev(x), dev(w), rl, bias=dev(bias), epilogue=L.EPI_RELU)
+    assert rel(rl, pre_ref.clamp_min(0)) < 1e-5
+    g = torch.empty(M, N, device=DEV)
+    ops.linear(dev(x), dev(w), g, epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=N)
+    xp = pre.double().cpu().requires_grad_()
+    gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+    assert rel(g, (x.double() @ w.double().t()) * gg) < 1e-5
+    rb = torch.empty(M, N, device=DEV)
+    ops.linear(dev(x), dev(w), rb, epilogue=L.EPI_RELU_BWD, aux_in=res.to(dtype).to(DEV), ld_aux_in=N)
+    assert rel(rb, (x.double() @ w.double().t()) * (res.to(dtype).double() > 0)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_atomic_accumulates(dtype):
+    from vspike import ops, _lib as L
+    M, N, K = 64, 192, 25088           # the dW shape: reduction over B*N tokens
+    dy = _rand(K, M, seed=8).to(dtype)
+    x = _rand(K, N, seed=9).to(dtype)
+    c = torch.ones(M, N, device=DEV)   # accumulates on top of existing values
+    ops.linear_dw(dy.to(DEV), x.to(DEV), c)
+    ref = dy.double().t() @ x.double() + 1.0
+    assert rel(c, ref) < 2e-5
+
+
+# ----------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [128, 192, 768])
+def test_layernorm_fwd_bwd(dtype, cols):
+    from vspike import ops
+    rows = 333
+    x = _rand(rows, cols, seed=10) * 3 + 1
+    g = 1 + 0.1 * _rand(cols, seed=11)
+    b = 0.1 * _rand(cols, seed=12)
+    dy = _rand(rows, cols, seed=13)
+    dres = _rand(rows, cols, seed=14)
+    y = torch.empty(rows, cols, dtype=dtype, device=DEV)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV), 1e-12, y, mean, rstd)
+    xr = x.double().requires_grad_()
+    gr, br = g.double().requires_grad_(), b.double().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (cols,), gr, br, 1e-12)
+    assert rel(y.float(), yr.detach()) < (1e-5 if dtype == torch.float32 else 5e-3)
+    dx = torch.empty(rows, cols, device=DEV)
+    dg = torch.zeros(cols, device=DEV)
+    db = torch.zeros(cols, device=DEV)
+    ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx, dg, db, dres=dres.to(DEV))
+    gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy.double())
+    assert rel(dx, gx + dres.double()) < 1e-5
+    assert rel(dg, gg) < 1e-5 and rel(db, gb) < 1e-5
+
+
+# ----------------------------------------------------------------------------------- attention
+def _attn_ref(qkv, B, N, H, scale=0.125):
+    D = H * 64
+    q, k, v = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    p = torch.softmax((q @ k.transpose(-1, -2)) * scale, dim=-1)
+    o = (p @ v).permute(0, 2, 1, 3).reshape(B * N, D)
+    lse = torch.logsumexp((q @ k.transpose(-1, -2)) * scale, dim=-1)
+    return o, lse
+
+
+ATTN_SHAPES = [(1, 100, 1), (2, 196, 2), (1, 1568, 3), (2, 130, 1)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", ATTN_SHAPES)
+def test_attention_fwd_bwd(dtype, shape):
+    from vspike import ops
+    B, N, H = shape
+    D = H * 64
+    qkv = _rand(B * N, 3 * D, seed=20, scale=1.5).to(dtype)
+    do = _rand(B * N, D, seed=21).to(dtype)
+    qd = qkv.to(DEV)
+    o = torch.empty(B * N, D, dtype=dtype, device=DEV)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qd, o, lse, B, N, H)
+    ref_in = qkv.double().requires_grad_()
+    o_ref, lse_ref = _attn_ref(ref_in, B, N, H)
+    ftol = 1e-5 if dtype == torch.float32 else 1.5e-2
+    assert rel(o.float(), o_ref.detach()) < ftol
+    assert rel(lse, lse_ref.detach()) < (1e-5 if dtype == torch.float32 else 2e-3)
+    dqkv = torch.empty(B * N, 3 * D, dtype=dtype, device=DEV)
+    ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=DEV)
+    # the backward consumes the forward's own O (as in training)
+    ops.attn_bwd(qd, o, do.to(DEV), lse, dqkv, ws, B, N, H)
+    (g_ref,) = torch.autograd.grad(o_ref, ref_in, do.double())
+    btol = 2e-5 if dtype == torch.float32 else 3e-2
+    for part in range(3):
+        sl = slice(part * D, (part + 1) * D)
+        assert rel(dqkv[:, sl].float(), g_ref[:, sl]) < btol, ("qkv"[part], rel(dqkv[:, sl].float(), g_ref[:, sl]))
+
+
+def test_attention_bf16_matches_f32_kernel_on_same_inputs():
+    """bf16 MFMA path vs the exact f32 kernel on identical (bf16-representable) inputs."""
+    from vspike import ops
+    B, N, H = 2, 1568, 3
+    D = H * 64
+    qkv = _rand(B * N, 3 * D, seed=30, scale=2.0).to(torch.bfloat16)
+    o16 = torch.empty(B * N, D, dtype=torch.bfloat16, device=DEV)
+    o32 = torch.empty(B * N, D, device=DEV)
+    l16 = torch.empty(B, H, N, device=DEV)
+    l32 = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv.to(DEV), o16, l16, B, N, H)
+    ops.attn_fwd(qkv.float().to(DEV), o32, l32, B, N, H)
+    assert rel(o16.float(), o32) < 1e-2
+    assert rel(l16, l32) < 1e-3
+
+
+def test_attention_rescale_branch_forced():
+    """A huge score late in the sequence forces the online-softmax rescale (guide rule 26)."""
+    from vspike import ops
+    B, N, H = 1, 700, 1
+    qkv = _rand(N, 192, seed=40, scale=0.5)
+    qkv[600, 64:128] = qkv[5, 0:64] * 40.0            # key 600 dominates query 5
+    for dtype, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-2)):
+        x = qkv.to(dtype)
+        o = torch.empty(N, 64, dtype=dtype, device=DEV)
+        lse = torch.empty(1, 1, N, device=DEV)
+        ops.attn_fwd(x.to(DEV), o, lse, B, N, H)
+        o_ref, _ = _attn_ref(x.double(), B, N, H)
+        assert rel(o.float(), o_ref) < tol
+
+
+# ---------------------------------------------------------------------------- im2col / misc ops
+def test_im2col_matches_oracle():
+    from oracle import cpu_ref
+    from vspike import ops
+    cfg = cpu_ref.VIT_SMALL_FIXTURE
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 2))
+    ref = cpu_ref.im2col(px, cfg)
+    for dtype in (torch.float32, torch.bfloat16):
+        out = torch.empty(ref.shape, dtype=dtype, device=DEV)
+        ops.patch_im2col(px.to(DEV), out, cfg.tubelet_size, cfg.patch_size)
+        assert torch.equal(out.cpu(), ref.to(dtype))
+
+
+def test_sinusoid_table_matches_oracle():
+    from oracle import cpu_ref
+    from vspike import ops
+    t = ops.sinusoid_table(1568, 192, DEV)
+    assert (t.cpu() - cpu_ref.sinusoid_table(1568, 192)).abs().max().item() < 1e-6
+
+
+def test_colsum_and_cast():
+    from vspike import ops
+    x = _rand(1000, 300, seed=50)
+    out = torch.full((300,), 2.0, device=DEV)
+    ops.colsum(x.to(DEV), out)
+    assert rel(out, x.double().sum(0) + 2.0) < 1e-5
+    xb = torch.empty(1000, 300, dtype=torch.bfloat16, device=DEV)
+    ops.cast(x.to(DEV), xb)
+    assert torch.equal(xb.cpu(), x.to(torch.bfloat16))
+
+
+def test_poisson_nll_and_grad():
+    from oracle import prng
+    from vspike import ops
+    x = _rand(4, 100, 128, seed=60, scale=0.5)
+    y = torch.from_numpy(prng.spike_targets(1, (4, 100, 128)))
+    loss = torch.empty((), device=DEV)
+    dx = torch.empty_like(x, device=DEV)
+    ops.poisson_nll(x.to(DEV), y.to(DEV), loss, dx=dx)
+    xr = x.double().requires_grad_()
+    lr = torch.nn.PoissonNLLLoss(log_input=True, reduction="none")(xr, y.double()).mean()
+    (gr,) = torch.autograd.grad(lr, xr)
+    assert abs(loss.item() - lr.item()) < 1e-6 * abs(lr.item())
+    assert rel(dx, gr) < 1e-6
+
+
+def test_fused_adamw_matches_torch():
+    from vspike import FusedAdamW
+    p0 = _rand(5000, seed=70)
+    grads = [_rand(5000, seed=71 + i) for i in range(4)]
+    ref = p0.clone().requires_grad_()
+    opt_r = torch.optim.AdamW([ref], lr=3e-3, weight_decay=0.01, eps=1e-8)
+    mine = torch.nn.Parameter(p0.clone().to(DEV))
+    opt_m = FusedAdamW([mine], lr=3e-3, weight_decay=0.01, eps=1e-8)
+    for g in grads:
+        ref.grad = g.clone()
+        opt_r.step()
+        mine.grad = g.to(DEV)
+        opt_m.step()
+    assert rel(mine.detach(), ref.detach()) < 1e-6

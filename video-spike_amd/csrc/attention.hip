@@ -1,0 +1,695 @@
+// attention.hip — non-causal MHA over frame-patch tokens, head dim 64 (mv:230-266, 286-294).
+//
+// bf16 (performance) path — v_mfma_f32_32x32x16_bf16, f32 accumulation, online softmax:
+//   forward: workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32 queries.
+//     S^T = K Q^T is computed with the KEY on the accumulator row and the QUERY on the lane, so a
+//     lane owns one query's whole softmax state (max, sum) — no cross-lane reductions except one
+//     xor-32 swap per 64-key tile.  The exponentiated S^T accumulator is directly the B operand of
+//     O^T += V^T P^T (no LDS round trip); V^T fragments come from ds_read_tr16_b64 on the V tile.
+//     K/V tiles (64 keys) are register-staged into double-buffered, XOR-swizzled LDS images.
+//   backward: workgroup = 4 waves = 128 keys; each wave keeps its 32 keys' K, V as MFMA operands
+//     and dK^T, dV^T in accumulators while sweeping 32-query blocks (Q, dO staged in LDS).  S and
+//     dP are computed with the key on the lane (accumulators initialised with -LSE/scale and
+//     -delta), so P and dS feed dV^T/dK^T directly; only dS^T crosses LDS for dQ, which is summed
+//     across key blocks with f32 atomics and rounded once by a convert kernel.
+// f32 (parity) path — exact-f32 VALU kernels: 4 lanes per query/key row, K/V (or Q/dO) tiles in
+//   LDS, expf/logf in f32.  Used for the 1e-4-relative parity mode.
+#include <math.h>
+
+#include "common.h"
+
+namespace vs {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// ============================================================================================
+// f32 kernels
+// ============================================================================================
+__global__ __launch_bounds__(256) void attn_fwd_f32_kernel(const float* __restrict__ qkv, int64_t ldq,
+                                                           float* __restrict__ o, int64_t ldo, float* __restrict__ lse,
+                                                           int N, int H, float scale) {
+  __shared__ float sK[64][68];
+  __shared__ float sV[64][68];
+  const int tid = threadIdx.x, sub = tid & 3;
+  const int qi = blockIdx.x * 64 + (tid >> 2);
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const float* Qp = qkv + row0 * ldq + h * 64;
+  const float* Kp = Qp + D;
+  const float* Vp = Qp + 2 * D;
+  float q[16], acc[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    q[d] = qi < N ? Qp[(int64_t)qi * ldq + sub * 16 + d] : 0.f;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  const int nkt = (N + 63) / 64;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63, gk = kt * 64 + r;
+      sK[r][c] = gk < N ? Kp[(int64_t)gk * ldq + c] : 0.f;
+      sV[r][c] = gk < N ? Vp[(int64_t)gk * ldq + c] : 0.f;
+    }
+    __syncthreads();
+    float s[64];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kk = 0; kk < 64; ++kk) {
+      float part = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) part = fmaf(q[d], sK[kk][sub * 16 + d], part);
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      s[kk] = (kt * 64 + kk < N) ? part * scale : -INFINITY;
+      mt = fmaxf(mt, s[kk]);
+    }
+    const float mn = fmaxf(m, mt);
+    const float alpha = expf(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) acc[d] *= alpha;
+#pragma unroll
+    for (int kk = 0; kk < 64; ++kk) {
+      const float p = expf(s[kk] - mn);
+      l += p;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] = fmaf(p, sV[kk][sub * 16 + d], acc[d]);
+    }
+    m = mn;
+  }
+  if (qi < N) {
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) o[(row0 + qi) * ldo + h * 64 + sub * 16 + d] = acc[d] * inv;
+    if (sub == 0) lse[((int64_t)b * H + h) * N + qi] = m + logf(l);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_f32_kernel(const float* __restrict__ qkv, int64_t ldq,
+                                                                const float* __restrict__ dout, int64_t lddo,
+                                                                const float* __restrict__ lse,
+                                                                const float* __restrict__ delta,
+                                                                float* __restrict__ dqkv, int64_t ldd, int N, int H,
+                                                                float scale) {
+  __shared__ float sQ[64][68];
+  __shared__ float sD[64][68];
+  __shared__ float sL[64], sDel[64];
+  const int tid = threadIdx.x, sub = tid & 3;
+  const int ki = blockIdx.x * 64 + (tid >> 2);
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const float* Qp = qkv + row0 * ldq + h * 64;
+  const float* Kp = Qp + D;
+  const float* Vp = Qp + 2 * D;
+  const float* Dp = dout + row0 * lddo + h * 64;
+  const float* L = lse + ((int64_t)b * H + h) * N;
+  const float* Del = delta + ((int64_t)b * H + h) * N;
+  float k[16], v[16], dk[16], dv[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    k[d] = ki < N ? Kp[(int64_t)ki * ldq + sub * 16 + d] : 0.f;
+    v[d] = ki < N ? Vp[(int64_t)ki * ldq + sub * 16 + d] : 0.f;
+    dk[d] = dv[d] = 0.f;
+  }
+  const int nqt = (N + 63) / 64;
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63, gq = qt * 64 + r;
+      sQ[r][c] = gq < N ? Qp[(int64_t)gq * ldq + c] : 0.f;
+      sD[r][c] = gq < N ? Dp[(int64_t)gq * lddo + c] : 0.f;
+    }
+    if (tid < 64) {
+      const int gq = qt * 64 + tid;
+      sL[tid] = gq < N ? L[gq] : INFINITY;
+      sDel[tid] = gq < N ? Del[gq] : 0.f;
+    }
+    __syncthreads();
+    for (int qq = 0; qq < 64; ++qq) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        s = fmaf(sQ[qq][sub * 16 + d], k[d], s);
+        dp = fmaf(sD[qq][sub * 16 + d], v[d], dp);
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      dp += __shfl_xor(dp, 1, 64);
+      dp += __shfl_xor(dp, 2, 64);
+      const float p = expf(s * scale - sL[qq]);
+      const float ds = p * (dp - sDel[qq]);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        dv[d] = fmaf(p, sD[qq][sub * 16 + d], dv[d]);
+        dk[d] = fmaf(ds, sQ[qq][sub * 16 + d], dk[d]);
+      }
+    }
+  }
+  if (ki < N) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      dqkv[(row0 + ki) * ldd + D + h * 64 + sub * 16 + d] = dk[d] * scale;
+      dqkv[(row0 + ki) * ldd + 2 * D + h * 64 + sub * 16 + d] = dv[d];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_f32_kernel(const float* __restrict__ qkv, int64_t ldq,
+                                                              const float* __restrict__ dout, int64_t lddo,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ delta, float* __restrict__ dqkv,
+                                                              int64_t ldd, int N, int H, float scale) {
+  __shared__ float sK[64][68];
+  __shared__ float sV[64][68];
+  const int tid = threadIdx.x, sub = tid & 3;
+  const int qi = blockIdx.x * 64 + (tid >> 2);
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const float* Qp = qkv + row0 * ldq + h * 64;
+  const float* Kp = Qp + D;
+  const float* Vp = Qp + 2 * D;
+  const float* Dp = dout + row0 * lddo + h * 64;
+  float q[16], g[16], dq[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    q[d] = qi < N ? Qp[(int64_t)qi * ldq + sub * 16 + d] : 0.f;
+    g[d] = qi < N ? Dp[(int64_t)qi * lddo + sub * 16 + d] : 0.f;
+    dq[d] = 0.f;
+  }
+  const float li = qi < N ? lse[((int64_t)b * H + h) * N + qi] : INFINITY;
+  const float deli = qi < N ? delta[((int64_t)b * H + h) * N + qi] : 0.f;
+  const int nkt = (N + 63) / 64;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63, gk = kt * 64 + r;
+      sK[r][c] = gk < N ? Kp[(int64_t)gk * ldq + c] : 0.f;
+      sV[r][c] = gk < N ? Vp[(int64_t)gk * ldq + c] : 0.f;
+    }
+    __syncthreads();
+    const int lim = N - kt * 64 < 64 ? N - kt * 64 : 64;
+    for (int kk = 0; kk < lim; ++kk) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) {
+        s = fmaf(q[d], sK[kk][sub * 16 + d], s);
+        dp = fmaf(g[d], sV[kk][sub * 16 + d], dp);
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      dp += __shfl_xor(dp, 1, 64);
+      dp += __shfl_xor(dp, 2, 64);
+      const float p = expf(s * scale - li);
+      const float ds = p * (dp - deli);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) dq[d] = fmaf(ds, sK[kk][sub * 16 + d], dq[d]);
+    }
+  }
+  if (qi < N) {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) dqkv[(row0 + qi) * ldd + h * 64 + sub * 16 + d] = dq[d] * scale;
+  }
+}
+
+// delta[b,h,n] = sum_d dO[n, h*64+d] * O[n, h*64+d]   (one wave per (row, head))
+template <typename T>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o, int64_t ldo, const T* __restrict__ dout,
+                                                         int64_t lddo, float* __restrict__ delta, int64_t rows, int N,
+                                                         int H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= rows * H) return;
+  const int64_t row = w / H;
+  const int h = (int)(w % H);
+  float v = Elem<T>::load(o + row * ldo + h * 64 + lane) * Elem<T>::load(dout + row * lddo + h * 64 + lane);
+  v = wave_sum(v);
+  if (lane == 0) {
+    const int64_t b = row / N, n = row % N;
+    delta[(b * H + h) * N + n] = v;
+  }
+}
+
+// ============================================================================================
+// bf16 MFMA kernels
+// ============================================================================================
+__device__ __forceinline__ int swz_row(int r) { return (r >> 1) & 7; }           // 16-B chunk XOR
+__device__ __forceinline__ int swz_half(int r) { return ((r >> 1) & 1) << 2; }   // 64-B half XOR
+
+// byte offset of element (r, c) (c multiple of 4 for tr reads) in a 128-B-row image
+__device__ __forceinline__ int off_rowswz(int r, int c) { return r * 128 + (((c >> 3) ^ swz_row(r)) << 4) + (c & 7) * 2; }
+__device__ __forceinline__ int off_halfswz(int r, int c) { return r * 128 + (((c >> 3) ^ swz_half(r)) << 4) + (c & 7) * 2; }
+
+__device__ __forceinline__ bf16x8 tr_pair(const char* lds, int off0, int off1) {
+  short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(lds + off0));
+  short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(lds + off1));
+  typedef __attribute__((ext_vector_type(8))) short short8v;
+  short8v s = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return __builtin_bit_cast(bf16x8, s);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[base + j];
+  return r;
+}
+__device__ __forceinline__ bf16x8 pack8f(const float* a) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[j];
+  return r;
+}
+
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  u.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+  return u;
+}
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                               bf16_t* __restrict__ o, int64_t ldo,
+                                                               float* __restrict__ lse, int N, int H,
+                                                               float scale_log2) {
+  constexpr int TILE = 64 * 128;  // bytes of one 64-key x 64-dh bf16 tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Vp = Qp + 2 * D;
+  const int qi = blockIdx.x * 128 + wid * 32 + (lane & 31);
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (qi < N) qf[s] = *(const bf16x8*)(Qp + (int64_t)qi * ldq + 16 * s + 8 * hh);
+    else qf[s] = bf16x8{};
+  }
+  f32x16 oacc[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) oacc[0][r] = oacc[1][r] = 0.f;
+  float m_run = -INFINITY, l_half = 0.f;
+
+  uint4 rk[2], rv[2];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
+      const int gk = kt * 64 + key;
+      if (gk < N) {
+        rk[s] = *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8);
+        rv[s] = *(const uint4*)(Vp + (int64_t)gk * ldq + c * 8);
+      } else {
+        rk[s] = make_uint4(0, 0, 0, 0);  // (a chained vector assignment here crashes ROCm 7.2 MCP)
+        rv[s] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* sK = smem + buf * 2 * TILE;
+    char* sV = sK + TILE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
+      *(uint4*)(sK + key * 128 + ((c ^ swz_row(key)) << 4)) = rk[s];
+      *(uint4*)(sV + key * 128 + ((c ^ swz_half(key)) << 4)) = rv[s];
+    }
+  };
+
+  const int nkt = (N + 63) / 64;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* sK = smem + (kt & 1) * 2 * TILE;
+    const char* sV = sK + TILE;
+    const bool more = kt + 1 < nkt;
+    if (more) load_tile(kt + 1);
+
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+      const int key = kb * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *(const bf16x8*)(sK + key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4));
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+    if ((kt + 1) * 64 > N) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 64 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key >= N) sacc[kb][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * scale_log2);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    l_half *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      oacc[0][r] *= alpha;
+      oacc[1][r] *= alpha;
+    }
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(fmaf(sacc[kb][r], scale_log2, -m_new));
+        sacc[kb][r] = p;
+        psum += p;
+      }
+    l_half += psum;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(sacc[kb], 8 * s);
+        const int key0 = kb * 32 + 16 * s + 4 * hh + q4;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = dt * 32 + g16 + p4;
+          const bf16x8 va = tr_pair(sV, off_halfswz(key0, col), off_halfswz(key0 + 8, col));
+          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, oacc[dt], 0, 0, 0);
+        }
+      }
+    if (more) store_tile((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  const float l = l_half + __shfl_xor(l_half, 32, 64);
+  if (qi < N) {
+    const float inv = 1.f / l;
+    bf16_t* orow = o + (row0 + qi) * ldo + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(orow + d) = pack4(oacc[dt][4 * g] * inv, oacc[dt][4 * g + 1] * inv, oacc[dt][4 * g + 2] * inv,
+                                    oacc[dt][4 * g + 3] * inv);
+      }
+    if (hh == 0) lse[((int64_t)b * H + h) * N + qi] = (m_run + log2f(l)) * kLn2;
+  }
+}
+
+// ------------------------------------------------------------------ backward
+__global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                               const bf16_t* __restrict__ dout, int64_t lddo,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta,
+                                                               float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv,
+                                                               int64_t ldd, int N, int H, float scale) {
+  constexpr int QT = 32 * 128;             // 32 rows x 128 B
+  constexpr int OFF_Q = 0, OFF_DO = 2 * QT, OFF_L = 4 * QT, OFF_DEL = OFF_L + 256, OFF_K = OFF_DEL + 256,
+                OFF_DS = OFF_K + 128 * 128, TOTAL = OFF_DS + 128 * 64;
+  __shared__ __attribute__((aligned(16))) char smem[TOTAL];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Vp = Qp + 2 * D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const float* L = lse + ((int64_t)b * H + h) * N;
+  const float* Del = delta + ((int64_t)b * H + h) * N;
+  const int kb0 = blockIdx.x * 128;
+  const int kl = wid * 32 + (lane & 31);  // key within the workgroup
+  const int ki = kb0 + kl;
+  const float inv_scale = 1.f / scale;
+  const float c2 = scale * kLog2e;
+
+  // K, V of this wave's keys as B operands: lane holds row ki, dh = 16s + 8hh + 0..7
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (ki < N) {
+      kf[s] = *(const bf16x8*)(Kp + (int64_t)ki * ldq + 16 * s + 8 * hh);
+      vf[s] = *(const bf16x8*)(Vp + (int64_t)ki * ldq + 16 * s + 8 * hh);
+    } else {
+      kf[s] = bf16x8{};
+      vf[s] = bf16x8{};
+    }
+  }
+  // K tile of the workgroup for dQ (half-row swizzle, read transposed)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int id = tid + 256 * s, key = id >> 3, c = id & 7;
+    const int gk = kb0 + key;
+    const uint4 v = gk < N ? *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8) : make_uint4(0, 0, 0, 0);
+    *(uint4*)(smem + OFF_K + key * 128 + ((c ^ swz_half(key)) << 4)) = v;
+  }
+
+  f32x16 dkacc[2], dvacc[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dkacc[0][r] = dkacc[1][r] = dvacc[0][r] = dvacc[1][r] = 0.f;
+
+  uint4 rq, rd;
+  float rl = 0.f;
+  auto load_q = [&](int qb) {
+    const int row = tid >> 3, c = tid & 7, gq = qb * 32 + row;
+    if (gq < N) {
+      rq = *(const uint4*)(Qp + (int64_t)gq * ldq + c * 8);
+      rd = *(const uint4*)(Dp + (int64_t)gq * lddo + c * 8);
+    } else {
+      rq = make_uint4(0, 0, 0, 0);
+      rd = make_uint4(0, 0, 0, 0);
+    }
+    if (tid < 32) {
+      const int g = qb * 32 + tid;
+      rl = g < N ? L[g] * inv_scale : INFINITY;
+    } else if (tid < 64) {
+      const int g = qb * 32 + tid - 32;
+      rl = g < N ? Del[g] : 0.f;
+    }
+  };
+  auto store_q = [&](int buf) {
+    const int row = tid >> 3, c = tid & 7;
+    const int off = buf * QT + row * 128 + ((c ^ swz_row(row)) << 4);
+    *(uint4*)(smem + OFF_Q + off) = rq;
+    *(uint4*)(smem + OFF_DO + off) = rd;
+    if (tid < 32) ((float*)(smem + OFF_L))[buf * 32 + tid] = rl;
+    else if (tid < 64) ((float*)(smem + OFF_DEL))[buf * 32 + tid - 32] = rl;
+  };
+
+  const int nqb = (N + 31) / 32;
+  load_q(0);
+  store_q(0);
+  __syncthreads();
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
+  const int dtile = wid & 1, khalf = wid >> 1;
+  float* dq_base = dq_acc + row0 * D + h * 64 + dtile * 32 + (lane & 31);
+
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int buf = qb & 1;
+    const char* sQ = smem + OFF_Q + buf * QT;
+    const char* sD = smem + OFF_DO + buf * QT;
+    const float* sL = (const float*)(smem + OFF_L) + buf * 32;
+    const float* sDel = (const float*)(smem + OFF_DEL) + buf * 32;
+    const bool more = qb + 1 < nqb;
+    if (more) load_q(qb + 1);
+
+    // S - LSE/scale and dP - delta, key on the lane, query on the accumulator row
+    f32x16 sacc, dpacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = (r & 3) + 8 * (r >> 2) + 4 * hh;
+      sacc[r] = -sL[ql];
+      dpacc[r] = -sDel[ql];
+    }
+    const int qrow = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int coff = qrow * 128 + (((2 * s + hh) ^ swz_row(qrow)) << 4);
+      const bf16x8 qa = *(const bf16x8*)(sQ + coff);
+      const bf16x8 da = *(const bf16x8*)(sD + coff);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dpacc, 0, 0, 0);
+    }
+    float p[16], ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      p[r] = exp2f(sacc[r] * c2);
+      ds[r] = p[r] * dpacc[r];
+    }
+    // dV^T += dO^T P,  dK^T += Q^T dS   (k = query, permuted order of the accumulator rows)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack8f(p + 8 * s);
+      const bf16x8 db = pack8f(ds + 8 * s);
+      const int q0 = 16 * s + 4 * hh + q4;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int col = dt * 32 + g16 + p4;
+        const int o0 = off_rowswz(q0, col), o1 = off_rowswz(q0 + 8, col);
+        const bf16x8 doa = tr_pair(sD, o0, o1);
+        const bf16x8 qta = tr_pair(sQ, o0, o1);
+        dvacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dvacc[dt], 0, 0, 0);
+        dkacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qta, db, dkacc[dt], 0, 0, 0);
+      }
+    }
+    // dS^T -> LDS image [key][query] (8-B units XOR (key>>1)&7)
+    {
+      char* sDS = smem + OFF_DS;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int u = 2 * g + hh;
+        *(uint2*)(sDS + kl * 64 + ((u ^ swz_row(kl)) << 3)) = pack4(ds[4 * g], ds[4 * g + 1], ds[4 * g + 2], ds[4 * g + 3]);
+      }
+    }
+    __syncthreads();
+    // dQ tile (32 queries x 32 dh of dtile) over this wave's key half (64 keys)
+    {
+      const char* sDS = smem + OFF_DS;
+      const char* sK = smem + OFF_K;
+      f32x16 dq;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int key0 = khalf * 64 + ks * 16 + 8 * hh + q4;
+        const int qc = g16 + p4;
+        const int a0 = key0 * 64 + (((qc >> 2) ^ swz_row(key0)) << 3);
+        const int a1 = (key0 + 4) * 64 + (((qc >> 2) ^ swz_row(key0 + 4)) << 3);
+        const bf16x8 dsa = tr_pair(sDS, a0, a1);
+        const int kc = dtile * 32 + g16 + p4;
+        const bf16x8 kb = tr_pair(sK, off_halfswz(key0, kc), off_halfswz(key0 + 4, kc));
+        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsa, kb, dq, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gq = qb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (gq < N) unsafeAtomicAdd(dq_base + (int64_t)gq * D, dq[r]);
+      }
+    }
+    if (more) store_q(buf ^ 1);
+    __syncthreads();
+  }
+
+  if (ki < N) {
+    bf16_t* krow = dqkv + (row0 + ki) * ldd + D + h * 64;
+    bf16_t* vrow = krow + D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(krow + d) = pack4(dkacc[dt][4 * g] * scale, dkacc[dt][4 * g + 1] * scale,
+                                    dkacc[dt][4 * g + 2] * scale, dkacc[dt][4 * g + 3] * scale);
+        *(uint2*)(vrow + d) = pack4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
+      }
+  }
+}
+
+// dQ (f32, summed over key blocks) -> bf16 Q columns of dqkv, times the softmax scale
+__global__ void attn_dq_convert_kernel(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int64_t ldd,
+                                       int64_t rows, int D, float scale) {
+  const int64_t total4 = rows * D / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4, r = e / D, c = e % D;
+    const float4 v = *(const float4*)(dq_acc + e);
+    *(uint2*)(dqkv + r * ldd + c) = pack4(v.x * scale, v.y * scale, v.z * scale, v.w * scale);
+  }
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+static int attn_check(int64_t B, int64_t N, int64_t H, int64_t Dh) {
+  VS_REQUIRE(Dh == 64, "vs_attn: head dim must be 64");
+  VS_REQUIRE(B > 0 && N > 0 && H > 0, "vs_attn: empty problem");
+  VS_REQUIRE(B <= 65535 && H <= 65535 && N < (1 << 30), "vs_attn: extents out of range");
+  return VS_OK;
+}
+
+extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv, int64_t ld_qkv,
+                           void* o, int64_t ld_o, float* lse, float scale, void* stream) {
+  VS_CALL(attn_check(B, N, H, Dh));
+  VS_REQUIRE(qkv && o && lse, "vs_attn_fwd: null pointer");
+  VS_REQUIRE(ld_qkv >= 3 * H * 64 && ld_o >= H * 64, "vs_attn_fwd: leading dims too small");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_ATTN_FWD, s);
+  if (dtype == VS_BF16) {
+    VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
+               "vs_attn_fwd: bf16 rows must be 16-byte aligned");
+    dim3 grid((unsigned)cdiv(N, 128), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse,
+                       (int)N, (int)H, scale * kLog2e);
+  } else if (dtype == VS_F32) {
+    dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(attn_fwd_f32_kernel, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, (float*)o, ld_o, lse,
+                       (int)N, (int)H, scale);
+  } else {
+    VS_REQUIRE(false, "vs_attn_fwd: bad dtype");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" size_t vs_attn_bwd_workspace_bytes(int64_t B, int64_t N, int64_t H, int64_t Dh) {
+  // delta [B,H,N] f32 (padded to 256 B) + dQ accumulator [B*N, H*Dh] f32
+  const size_t delta = ((size_t)(B * H * N) * 4 + 255) / 256 * 256;
+  return delta + (size_t)(B * N * H * Dh) * 4;
+}
+
+extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv, int64_t ld_qkv,
+                           const void* o, int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv,
+                           int64_t ld_dqkv, void* workspace, float scale, void* stream) {
+  VS_CALL(attn_check(B, N, H, Dh));
+  VS_REQUIRE(qkv && o && dout && lse && dqkv && workspace, "vs_attn_bwd: null pointer");
+  VS_REQUIRE(ld_qkv >= 3 * H * 64 && ld_dqkv >= 3 * H * 64 && ld_o >= H * 64 && ld_do >= H * 64,
+             "vs_attn_bwd: leading dims too small");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_ATTN_BWD, s);
+  float* delta = (float*)workspace;
+  float* dq_acc = (float*)((char*)workspace + ((size_t)(B * H * N) * 4 + 255) / 256 * 256);
+  const int64_t rows = B * N;
+  const unsigned dgrid = (unsigned)cdiv(rows * H, 4);
+  if (dtype == VS_BF16) {
+    VS_REQUIRE(ld_qkv % 8 == 0 && ld_dqkv % 4 == 0 && ld_do % 8 == 0 && aligned16(qkv) && aligned16(dout) &&
+                   (((uintptr_t)dqkv) & 7) == 0,
+               "vs_attn_bwd: bf16 rows must be 16-byte aligned");
+    hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(dgrid), dim3(256), 0, s, (const bf16_t*)o, ld_o,
+                       (const bf16_t*)dout, ld_do, delta, rows, (int)N, (int)H);
+    hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)rows * H * 64 * 4, s);
+    if (e != hipSuccess) return (int)e;
+    dim3 grid((unsigned)cdiv(N, 128), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(attn_bwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout,
+                       ld_do, lse, delta, dq_acc, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+    const int64_t t4 = rows * H * 64 / 4;
+    hipLaunchKernelGGL(attn_dq_convert_kernel, dim3((unsigned)(cdiv(t4, 256) > 4096 ? 4096 : cdiv(t4, 256))), dim3(256),
+                       0, s, dq_acc, (bf16_t*)dqkv, ld_dqkv, rows, (int)(H * 64), scale);
+  } else if (dtype == VS_F32) {
+    hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,
+                       (const float*)dout, ld_do, delta, rows, (int)N, (int)H);
+    dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);
+    hipLaunchKernelGGL(attn_bwd_dkdv_f32_kernel, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, (const float*)dout,
+                       ld_do, lse, delta, (float*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_f32_kernel, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, (const float*)dout,
+                       ld_do, lse, delta, (float*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+  } else {
+    VS_REQUIRE(false, "vs_attn_bwd: bad dtype");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

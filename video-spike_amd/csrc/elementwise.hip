@@ -1,0 +1,281 @@
+// elementwise.hip — HBM-bound helpers of the hot path: tubelet im2col, sinusoid table, bias
+// column sums, casts, fused PoissonNLL(+grad) and the fused AdamW step.
+#include <math.h>
+
+#include "common.h"
+
+namespace vs {
+
+// ---------------------------------------------------------------------------------------------
+// im2col for the tubelet Conv3d (mv:176-181, 194-195).  One thread writes 8 consecutive columns
+// (8 consecutive j of one (c, t, i) row of a patch): 8 coalesced-ish f32 reads of one image row,
+// one 16-B (bf16) / 2x16-B (f32) store.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void im2col_kernel(const float* __restrict__ px, T* __restrict__ out, int64_t B, int F, int C, int H,
+                              int W, int t, int p) {
+  const int Fp = F / t, Hp = H / p, Wp = W / p;
+  const int64_t ncol = (int64_t)C * t * p * p;
+  const int64_t total8 = B * Fp * Hp * Wp * ncol / 8;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total8; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = g * 8;
+    const int64_t row = e0 / ncol;
+    const int64_t col = e0 % ncol;
+    // col = ((c*t + tt)*p + i)*p + j
+    const int j = (int)(col % p);
+    int64_t r = col / p;
+    const int i = (int)(r % p);
+    r /= p;
+    const int tt = (int)(r % t);
+    const int c = (int)(r / t);
+    // row = ((b*Fp + f')*Hp + hp)*Wp + wp
+    int64_t q = row;
+    const int wp = (int)(q % Wp);
+    q /= Wp;
+    const int hp = (int)(q % Hp);
+    q /= Hp;
+    const int fp = (int)(q % Fp);
+    const int64_t b = q / Fp;
+    const int f = fp * t + tt;
+    const float* src = px + ((((b * F + f) * C + c) * H + (hp * p + i)) * (int64_t)W + wp * p + j);
+    float v[8];
+    if ((j + 8 <= p)) {
+      const float4 a = *(const float4*)src;
+      const float4 bb = *(const float4*)(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = bb.x; v[5] = bb.y; v[6] = bb.z; v[7] = bb.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = src[k];
+    }
+    T* dst = out + e0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) Elem<T>::store(dst + k, v[k]);
+  }
+}
+
+__global__ void sinusoid_kernel(int64_t n_pos, int64_t dim, float* out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n_pos * dim) return;
+  const int64_t pos = i / dim, j = i % dim;
+  const double angle = (double)pos / pow(10000.0, (double)(2 * (j / 2)) / (double)dim);
+  out[i] = (float)((j % 2 == 0) ? sin(angle) : cos(angle));
+}
+
+// ---------------------------------------------------------------------------------------------
+// column sums (bias gradients).  Block = 256 threads = 4 row-lanes x 64 columns... each thread
+// owns one column inside a 64-column stripe and walks rows with stride; partials reduced in LDS,
+// one atomic per column per block.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ x, int64_t ldx, int64_t rows, int64_t cols, float* __restrict__ out,
+                              int64_t rows_per_block) {
+  __shared__ float part[4][64];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t c = blockIdx.x * 64 + cx;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > rows) r1 = rows;
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = r0 + ry; r < r1; r += 4) s += Elem<T>::load(x + r * ldx + c);
+  part[ry][cx] = s;
+  __syncthreads();
+  if (ry == 0 && c < cols) unsafeAtomicAdd(out + c, part[0][cx] + part[1][cx] + part[2][cx] + part[3][cx]);
+}
+
+__global__ void cast_f32_bf16(const float* __restrict__ in, bf16_t* __restrict__ out, int64_t n) {
+  for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
+    if (i + 4 <= n) {
+      const float4 v = *(const float4*)(in + i);
+      ushort4 o;
+      o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+      *(ushort4*)(out + i) = o;
+    } else {
+      for (int64_t k = i; k < n; ++k) out[k] = f2bf(in[k]);
+    }
+  }
+}
+__global__ void cast_bf16_f32(const bf16_t* __restrict__ in, float* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = bf2f(in[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// PoissonNLLLoss(log_input=True), mean reduction, fused with its gradient.
+// Stage 1: per-block partial sums (fixed order) + dx.  Stage 2: one block sums the partials in a
+// fixed order -> deterministic loss.
+// ---------------------------------------------------------------------------------------------
+constexpr int kPoissonBlocks = 256;
+
+__global__ void poisson_stage1(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ dx,
+                               float gscale, int64_t n, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float xi = x[i], yi = y[i];
+    const float ex = expf(xi);
+    s += ex - yi * xi;
+    if (dx) dx[i] = gscale * (ex - yi);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ void poisson_stage2(const float* __restrict__ partial, int nb, float inv_n, float* __restrict__ loss) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += partial[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) * inv_n;
+}
+__global__ void poisson_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                   const float* __restrict__ g, float* __restrict__ dx, int64_t n) {
+  const float s = g[0] / (float)n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = s * (expf(x[i]) - y[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// AdamW (torch.optim.AdamW, single-tensor semantics, foreach=False/True agree):
+//   p *= 1 - lr*wd;  m = m + (1-b1)*(g - m);  v = b2*v + (1-b2)*g*g
+//   p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+// ---------------------------------------------------------------------------------------------
+__global__ void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, bf16_t* __restrict__ plp, const float* __restrict__ hyper) {
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4], step = hyper[5],
+              gs = hyper[6];
+  const float bc1 = 1.f - powf(b1, step);
+  const float bc2s = sqrtf(1.f - powf(b2, step));
+  const float step_size = lr / bc1;
+  const float decay = 1.f - lr * wd;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gs;
+    float pi = p[i] * decay;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (plp) plp[i] = f2bf(pi);
+  }
+}
+
+static unsigned grid_for(int64_t n, int per_thread = 1) {
+  int64_t b = cdiv(cdiv(n, per_thread), 256);
+  if (b > 4096) b = 4096;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" int vs_patch_im2col(int32_t out_dtype, int64_t B, int64_t F, int64_t C, int64_t H, int64_t W,
+                               int64_t tubelet, int64_t patch, const float* pixels, void* cols, void* stream) {
+  VS_REQUIRE(pixels && cols, "vs_patch_im2col: null pointer");
+  VS_REQUIRE(tubelet > 0 && patch > 0 && F % tubelet == 0 && H % patch == 0 && W % patch == 0,
+             "vs_patch_im2col: frames/size must divide by tubelet/patch");
+  VS_REQUIRE(patch % 8 == 0 && W % 4 == 0 && aligned16(pixels), "vs_patch_im2col: patch must be a multiple of 8");
+  const int64_t total8 = B * (F / tubelet) * (H / patch) * (W / patch) * C * tubelet * patch * patch / 8;
+  if (total8 == 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = grid_for(total8);
+  if (out_dtype == VS_BF16)
+    hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(g), dim3(256), 0, s, pixels, (bf16_t*)cols, B, (int)F, (int)C,
+                       (int)H, (int)W, (int)tubelet, (int)patch);
+  else
+    hipLaunchKernelGGL(im2col_kernel<float>, dim3(g), dim3(256), 0, s, pixels, (float*)cols, B, (int)F, (int)C,
+                       (int)H, (int)W, (int)tubelet, (int)patch);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_sinusoid_table(int64_t n_pos, int64_t dim, float* out, void* stream) {
+  VS_REQUIRE(out && n_pos >= 0 && dim > 0, "vs_sinusoid_table: bad args");
+  if (n_pos == 0) return VS_OK;
+  hipLaunchKernelGGL(sinusoid_kernel, dim3((unsigned)cdiv(n_pos * dim, 256)), dim3(256), 0, (hipStream_t)stream,
+                     n_pos, dim, out);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_colsum(int32_t dtype, int64_t rows, int64_t cols, const void* x, int64_t ldx, float* out,
+                         void* stream) {
+  VS_REQUIRE(x && out && ldx >= cols, "vs_colsum: bad args");
+  if (rows == 0 || cols == 0) return VS_OK;
+  const int64_t cb = cdiv(cols, 64);
+  int64_t rb = cdiv(1024, cb);
+  if (rb > cdiv(rows, 64)) rb = cdiv(rows, 64);
+  if (rb < 1) rb = 1;
+  const int64_t rpb = cdiv(rows, rb);
+  dim3 grid((unsigned)cb, (unsigned)cdiv(rows, rpb));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VS_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, rows, cols, out, rpb);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, rows, cols, out, rpb);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_cast(int32_t in_dtype, int32_t out_dtype, int64_t n, const void* in, void* out, void* stream) {
+  VS_REQUIRE(in && out && n >= 0, "vs_cast: bad args");
+  if (n == 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (in_dtype == VS_F32 && out_dtype == VS_BF16) {
+    VS_REQUIRE(aligned16(in) && (((uintptr_t)out) & 7u) == 0, "vs_cast: misaligned");
+    hipLaunchKernelGGL(cast_f32_bf16, dim3(grid_for(n, 4)), dim3(256), 0, s, (const float*)in, (bf16_t*)out, n);
+  } else if (in_dtype == VS_BF16 && out_dtype == VS_F32) {
+    hipLaunchKernelGGL(cast_bf16_f32, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)in, (float*)out, n);
+  } else if (in_dtype == out_dtype) {
+    hipError_t e = hipMemcpyAsync(out, in, n * esize(in_dtype), hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return (int)e;
+    return VS_OK;
+  } else {
+    VS_REQUIRE(false, "vs_cast: bad dtype pair");
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" size_t vs_poisson_workspace_bytes(int64_t n) {
+  (void)n;
+  return kPoissonBlocks * sizeof(float);
+}
+
+extern "C" int vs_poisson_nll(int64_t n, const float* log_rate, const float* target, float* loss_out, float* dx,
+                              float grad_scale, void* workspace, void* stream) {
+  VS_REQUIRE(n > 0 && log_rate && target && loss_out && workspace, "vs_poisson_nll: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  int nb = (int)cdiv(n, 256);
+  if (nb > kPoissonBlocks) nb = kPoissonBlocks;
+  hipLaunchKernelGGL(poisson_stage1, dim3(nb), dim3(256), 0, s, log_rate, target, dx, grad_scale / (float)n, n,
+                     (float*)workspace);
+  hipLaunchKernelGGL(poisson_stage2, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, 1.0f / (float)n, loss_out);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_poisson_nll_bwd(int64_t n, const float* log_rate, const float* target, const float* grad_out,
+                                  float* dx, void* stream) {
+  VS_REQUIRE(n > 0 && log_rate && target && grad_out && dx, "vs_poisson_nll_bwd: bad args");
+  hipLaunchKernelGGL(poisson_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, log_rate, target,
+                     grad_out, dx, n);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_lp,
+                        const float* hyper, void* stream) {
+  VS_REQUIRE(param && grad && exp_avg && exp_avg_sq && hyper && n >= 0, "vs_adamw: bad args");
+  if (n == 0) return VS_OK;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, param, grad, exp_avg,
+                     exp_avg_sq, (bf16_t*)param_lp, hyper);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

@@ -1,0 +1,437 @@
+// gemm.hip — MFMA GEMM with fused epilogues (vs_gemm).
+//
+// Replaces the nn.Linear / F.linear / Conv3d(as im2col) kernels of the reference hot path and
+// their autograd backward (see include/vspike.h for the per-call-site citations).
+//
+// bf16 operands: v_mfma_f32_16x16x32_bf16, block tile BM x BN x 64, 4 waves in 2x2, each wave
+//   (BM/2) x (BN/2).  Operands are staged global -> registers -> LDS (double-buffered, loads for
+//   tile t+1 issued before the MFMAs of tile t).  LDS images:
+//     K-contiguous operand:  [rows][64 k] 128-B rows, 16-B chunk XOR (row>>1)&7  -> ds_read_b128
+//     M/N-contiguous operand: [64 k][rows] rows, chunk XOR f(k)                 -> ds_read_tr16_b64
+//   so the transposed products of the backward (dW = dY^T X, dX = dY W) need no transpose pass.
+// f32 operands: v_mfma_f32_16x16x4_f32 (exact f32 fma chain), tile 64x64x32, [k][rows] images.
+// Split-K (grid.z) writes through f32 atomics (VS_EPI_ATOMIC) for the skinny-output weight
+// gradients (K = B*N tokens) and the 1.2M-wide head.
+#include "common.h"
+
+namespace vs {
+
+struct EpiParams {
+  int64_t M, N;
+  void* c;
+  int64_t ldc;
+  int out_bf16;
+  int op_bf16;
+  uint32_t flags;
+  float alpha;
+  const float* bias;
+  const float* residual;
+  int64_t ldr;
+  const float* pos;
+  int64_t pos_rows;
+  const void* aux_in;
+  int64_t ld_aux_in;
+  void* aux_out;
+  int64_t ld_aux_out;
+};
+
+__device__ __forceinline__ float ld_any(const void* p, int64_t i, int bf) {
+  return bf ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, int64_t i, float v, int bf) {
+  if (bf) ((bf16_t*)p)[i] = f2bf(v);
+  else ((float*)p)[i] = v;
+}
+
+__device__ __forceinline__ void epilogue(const EpiParams& e, int64_t m, int64_t n, float v, bool first_split) {
+  if (m >= e.M || n >= e.N) return;
+  const uint32_t f = e.flags;
+  v *= e.alpha;
+  if (f & VS_EPI_ATOMIC) {
+    if ((f & VS_EPI_BIAS) && first_split) v += e.bias[n];
+    unsafeAtomicAdd((float*)e.c + m * e.ldc + n, v);
+    return;
+  }
+  if (f & VS_EPI_BIAS) v += e.bias[n];
+  if (f & VS_EPI_POS) v += e.pos[(m % e.pos_rows) * e.N + n];
+  if (f & VS_EPI_GELU_BWD) v *= gelu_erf_grad(ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16));
+  if (f & VS_EPI_RELU_BWD) v = ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16) > 0.f ? v : 0.f;
+  if (f & VS_EPI_GELU) {
+    st_any(e.aux_out, m * e.ld_aux_out + n, v, e.op_bf16);
+    // GELU of the value the backward will see (rounded pre-activation in bf16 mode)
+    v = gelu_erf(e.op_bf16 ? bf2f(f2bf(v)) : v);
+  }
+  if (f & VS_EPI_RELU) v = fmaxf(v, 0.f);
+  if (f & VS_EPI_RESIDUAL) v += e.residual[m * e.ldr + n];
+  if (f & VS_EPI_ACCUM) v += ((const float*)e.c)[m * e.ldc + n];
+  st_any(e.c, m * e.ldc + n, v, e.out_bf16);
+}
+
+// ----------------------------------------------------------------------------------------------
+// bf16 kernel
+// ----------------------------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ int swz_mc(int k) {  // chunk XOR for [k][R] images (R = 128 or 64)
+  if constexpr (R == 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+__device__ __forceinline__ int swz_kc(int r) { return (r >> 1) & 7; }
+
+template <int R, bool KC>
+struct OperandBf16 {
+  static constexpr int BK = 64;
+  static constexpr int BYTES = R * BK * 2;
+  static constexpr int CHUNKS = R * BK / 8 / 256;  // 16-B chunks per thread per tile
+
+  // global -> registers.  rows: extent of the R dimension; k_end: end of this split's K range.
+  __device__ __forceinline__ static void load(uint4 (&reg)[CHUNKS], const bf16_t* __restrict__ p, int64_t ld,
+                                              int64_t r0, int64_t rows, int64_t k0, int64_t k_end, int tid) {
+#pragma unroll
+    for (int s = 0; s < CHUNKS; ++s) {
+      const int i = tid + 256 * s;
+      int64_t gr, gk;
+      if constexpr (KC) {
+        gr = r0 + (i >> 3);
+        gk = k0 + (i & 7) * 8;
+      } else {
+        gk = k0 + i / (R / 8);
+        gr = r0 + (i % (R / 8)) * 8;
+      }
+      const bool ok = gr < rows && gk < k_end;
+      const bf16_t* src = KC ? p + gr * ld + gk : p + gk * ld + gr;
+      reg[s] = ok ? *(const uint4*)src : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ static void store(char* lds, const uint4 (&reg)[CHUNKS], int tid) {
+#pragma unroll
+    for (int s = 0; s < CHUNKS; ++s) {
+      const int i = tid + 256 * s;
+      int off;
+      if constexpr (KC) {
+        const int r = i >> 3, c = i & 7;
+        off = r * 128 + ((c ^ swz_kc(r)) << 4);
+      } else {
+        const int k = i / (R / 8), c = i % (R / 8);
+        off = k * (R * 2) + ((c ^ swz_mc<R>(k)) << 4);
+      }
+      *(uint4*)(lds + off) = reg[s];
+    }
+  }
+  // fragment of rows [rb, rb+16) for the 32-deep k step kk (0/1): lane holds rows rb+(lane&15),
+  // k = 32kk + 8(lane>>4) + 0..7.
+  __device__ __forceinline__ static bf16x8 frag(const char* lds, int rb, int kk, int lane) {
+    if constexpr (KC) {
+      const int r = rb + (lane & 15);
+      const int c = kk * 4 + (lane >> 4);
+      return *(const bf16x8*)(lds + r * 128 + ((c ^ swz_kc(r)) << 4));
+    } else {
+      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+      const int col = rb + p4;
+      const int k0 = kk * 32 + 8 * (lane >> 4) + q;
+      const int k1 = k0 + 4;
+      const int off0 = k0 * (R * 2) + (((col >> 3) ^ swz_mc<R>(k0)) << 4) + (col & 7) * 2;
+      const int off1 = k1 * (R * 2) + (((col >> 3) ^ swz_mc<R>(k1)) << 4) + (col & 7) * 2;
+      short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(lds + off0));
+      short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(lds + off1));
+      typedef __attribute__((ext_vector_type(8))) short short8v;
+      short8v s = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+      return __builtin_bit_cast(bf16x8, s);
+    }
+  }
+};
+
+template <int BM, int BN, bool AKC, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                           const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
+                                                           int64_t k_per_split, EpiParams e) {
+  using OA = OperandBf16<BM, AKC>;
+  using OB = OperandBf16<BN, BKC>;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const int64_t k_begin = (int64_t)blockIdx.z * k_per_split;
+  const int64_t k_end = k_begin + k_per_split < K ? k_begin + k_per_split : K;
+  const int nk = (int)((k_end - k_begin + 63) / 64);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[OA::CHUNKS], rb[OB::CHUNKS];
+  if (nk > 0) {
+    OA::load(ra, A, lda, m0, e.M, k_begin, k_end, tid);
+    OB::load(rb, B, ldb, n0, e.N, k_begin, k_end, tid);
+    OA::store(smem, ra, tid);
+    OB::store(smem + OA::BYTES, rb, tid);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* sa = smem + (t & 1) * STAGE;
+    const char* sb = sa + OA::BYTES;
+    const bool more = t + 1 < nk;
+    if (more) {
+      const int64_t kn = k_begin + (int64_t)(t + 1) * 64;
+      OA::load(ra, A, lda, m0, e.M, kn, k_end, tid);
+      OB::load(rb, B, ldb, n0, e.N, kn, k_end, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = OB::frag(sb, wc * WN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* dst = smem + ((t + 1) & 1) * STAGE;
+      OA::store(dst, ra, tid);
+      OB::store(dst + OA::BYTES, rb, tid);
+    }
+    __syncthreads();
+  }
+
+  const bool first = blockIdx.z == 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t n = n0 + wc * WN + j * 16 + (lane & 15);
+        epilogue(e, m, n, acc[i][j][r], first);
+      }
+}
+
+// ----------------------------------------------------------------------------------------------
+// f32 kernel (exact: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
+// ----------------------------------------------------------------------------------------------
+template <bool KC>
+struct OperandF32 {
+  static constexpr int R = 64, BK = 32, LD = 80;  // LD % 32 == 16 -> conflict-free ds_read_b32
+  static constexpr int BYTES = BK * LD * 4;
+  __device__ __forceinline__ static void load(float4 (&reg)[2], const float* __restrict__ p, int64_t ld, int64_t r0,
+                                              int64_t rows, int64_t k0, int64_t k_end, int tid) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = tid + 256 * s;
+      int64_t gr, gk;
+      if constexpr (KC) {
+        gr = r0 + (i >> 3);
+        gk = k0 + (i & 7) * 4;
+      } else {
+        gk = k0 + (i >> 4);
+        gr = r0 + (i & 15) * 4;
+      }
+      const bool ok = gr < rows && gk < k_end;
+      const float* src = KC ? p + gr * ld + gk : p + gk * ld + gr;
+      reg[s] = ok ? *(const float4*)src : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ static void store(float* lds, const float4 (&reg)[2], int tid) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = tid + 256 * s;
+      if constexpr (KC) {
+        const int r = i >> 3, k = (i & 7) * 4;
+        lds[(k + 0) * LD + r] = reg[s].x;
+        lds[(k + 1) * LD + r] = reg[s].y;
+        lds[(k + 2) * LD + r] = reg[s].z;
+        lds[(k + 3) * LD + r] = reg[s].w;
+      } else {
+        const int k = i >> 4, r = (i & 15) * 4;
+        *(float4*)(lds + k * LD + r) = reg[s];
+      }
+    }
+  }
+};
+
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ B, int64_t ldb, int64_t K,
+                                                          int64_t k_per_split, EpiParams e) {
+  using OA = OperandF32<AKC>;
+  using OB = OperandF32<BKC>;
+  constexpr int LD = OA::LD;
+  constexpr int STAGE = (OA::BYTES + OB::BYTES) / 4;  // floats
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
+  const int64_t k_begin = (int64_t)blockIdx.z * k_per_split;
+  const int64_t k_end = k_begin + k_per_split < K ? k_begin + k_per_split : K;
+  const int nk = (int)((k_end - k_begin + 31) / 32);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[2], rb[2];
+  if (nk > 0) {
+    OA::load(ra, A, lda, m0, e.M, k_begin, k_end, tid);
+    OB::load(rb, B, ldb, n0, e.N, k_begin, k_end, tid);
+    OA::store(smem, ra, tid);
+    OB::store(smem + OA::BYTES / 4, rb, tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const float* sa = smem + (t & 1) * STAGE;
+    const float* sb = sa + OA::BYTES / 4;
+    const bool more = t + 1 < nk;
+    if (more) {
+      const int64_t kn = k_begin + (int64_t)(t + 1) * 32;
+      OA::load(ra, A, lda, m0, e.M, kn, k_end, tid);
+      OB::load(rb, B, ldb, n0, e.N, kn, k_end, tid);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = 4 * s + (lane >> 4);
+      float af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = sa[k * LD + wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = sb[k * LD + wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      float* dst = smem + ((t + 1) & 1) * STAGE;
+      OA::store(dst, ra, tid);
+      OB::store(dst + OA::BYTES / 4, rb, tid);
+    }
+    __syncthreads();
+  }
+  const bool first = blockIdx.z == 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+        epilogue(e, m, n, acc[i][j][r], first);
+      }
+}
+
+// ----------------------------------------------------------------------------------------------
+// host dispatch
+// ----------------------------------------------------------------------------------------------
+template <int BM, int BN>
+static void launch_bf16(const vs_gemm_desc* d, dim3 grid, int64_t kps, const EpiParams& e, hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->a_kcontig && d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+  else if (d->a_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+  else if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+}
+
+static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
+  if (!atomic_ok) return 1;
+  if (want > 0) return (int)(want < nk ? want : nk);
+  if (tiles >= 512 || nk < 8) return 1;
+  int64_t s = (1024 + tiles - 1) / tiles;
+  const int64_t max_s = nk / 4;
+  if (s > max_s) s = max_s;
+  return s < 1 ? 1 : (int)s;
+}
+
+}  // namespace vs
+
+extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
+  using namespace vs;
+  VS_REQUIRE(d != nullptr, "vs_gemm: null descriptor");
+  VS_REQUIRE(d->dtype == VS_F32 || d->dtype == VS_BF16, "vs_gemm: dtype must be VS_F32 or VS_BF16");
+  VS_REQUIRE(d->out_dtype == VS_F32 || d->out_dtype == VS_BF16, "vs_gemm: bad out_dtype");
+  VS_REQUIRE(d->M >= 0 && d->N >= 0 && d->K >= 0, "vs_gemm: negative extent");
+  if (d->M == 0 || d->N == 0) return VS_OK;
+  VS_REQUIRE(d->a && d->b && d->c, "vs_gemm: null operand");
+  const uint32_t f = d->epilogue;
+  const int vec = d->dtype == VS_BF16 ? 8 : 4;
+  // contiguous extents and leading dims must allow 16-byte vector loads
+  VS_REQUIRE(aligned16(d->a) && aligned16(d->b), "vs_gemm: operands must be 16-byte aligned");
+  VS_REQUIRE(d->lda % vec == 0 && d->ldb % vec == 0, "vs_gemm: lda/ldb must be multiples of 16 bytes");
+  VS_REQUIRE(d->a_kcontig ? (d->K % vec == 0 && d->lda >= d->K) : (d->M % vec == 0 && d->lda >= d->M),
+             "vs_gemm: A contiguous extent must be a multiple of 16 bytes and <= lda");
+  VS_REQUIRE(d->b_kcontig ? (d->K % vec == 0 && d->ldb >= d->K) : (d->N % vec == 0 && d->ldb >= d->N),
+             "vs_gemm: B contiguous extent must be a multiple of 16 bytes and <= ldb");
+  VS_REQUIRE(d->ldc >= d->N, "vs_gemm: ldc < N");
+  VS_REQUIRE(!(f & VS_EPI_BIAS) || d->bias, "vs_gemm: BIAS needs bias");
+  VS_REQUIRE(!(f & VS_EPI_RESIDUAL) || d->residual, "vs_gemm: RESIDUAL needs residual");
+  VS_REQUIRE(!(f & VS_EPI_POS) || (d->pos && d->pos_rows > 0), "vs_gemm: POS needs pos/pos_rows");
+  VS_REQUIRE(!(f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) || d->aux_in, "vs_gemm: *_BWD needs aux_in");
+  VS_REQUIRE(!(f & VS_EPI_GELU) || d->aux_out, "vs_gemm: GELU needs aux_out");
+  VS_REQUIRE(!(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM)) || d->out_dtype == VS_F32, "vs_gemm: ATOMIC/ACCUM need f32 C");
+  VS_REQUIRE(!((f & VS_EPI_ATOMIC) && (f & ~(VS_EPI_ATOMIC | VS_EPI_BIAS))),
+             "vs_gemm: ATOMIC combines with BIAS only");
+  VS_REQUIRE(d->split_k <= 1 || (f & VS_EPI_ATOMIC), "vs_gemm: split_k > 1 needs VS_EPI_ATOMIC");
+
+  EpiParams e;
+  e.M = d->M; e.N = d->N; e.c = d->c; e.ldc = d->ldc;
+  e.out_bf16 = d->out_dtype == VS_BF16; e.op_bf16 = d->dtype == VS_BF16;
+  e.flags = f; e.alpha = d->alpha; e.bias = d->bias;
+  e.residual = d->residual; e.ldr = d->ld_residual;
+  e.pos = d->pos; e.pos_rows = d->pos_rows;
+  e.aux_in = d->aux_in; e.ld_aux_in = d->ld_aux_in;
+  e.aux_out = d->aux_out; e.ld_aux_out = d->ld_aux_out;
+
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_GEMM, s);
+  const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
+  if (d->dtype == VS_BF16) {
+    const int BM = d->M <= 64 ? 64 : 128;
+    const int BN = (d->N <= 64 || (d->N % 128 != 0 && d->N % 64 == 0 && d->N < 1024)) ? 64 : 128;
+    const int64_t tiles = cdiv(d->N, BN) * cdiv(d->M, BM);
+    const int64_t nk = cdiv(d->K, 64);
+    const int splits = pick_splits(tiles, nk, d->split_k, atomic_ok);
+    const int64_t kps = cdiv(nk, splits) * 64;
+    const int nz = (int)cdiv(d->K, kps > 0 ? kps : 64);
+    dim3 grid((unsigned)cdiv(d->N, BN), (unsigned)cdiv(d->M, BM), (unsigned)(nz > 0 ? nz : 1));
+    VS_REQUIRE(grid.y <= 65535, "vs_gemm: M too large");
+    if (BM == 128 && BN == 128) launch_bf16<128, 128>(d, grid, kps, e, s);
+    else if (BM == 128) launch_bf16<128, 64>(d, grid, kps, e, s);
+    else if (BN == 128) launch_bf16<64, 128>(d, grid, kps, e, s);
+    else launch_bf16<64, 64>(d, grid, kps, e, s);
+  } else {
+    const int64_t tiles = cdiv(d->N, 64) * cdiv(d->M, 64);
+    const int64_t nk = cdiv(d->K, 32);
+    const int splits = pick_splits(tiles, nk, d->split_k, atomic_ok);
+    const int64_t kps = cdiv(nk, splits) * 32;
+    const int nz = (int)cdiv(d->K, kps > 0 ? kps : 32);
+    dim3 grid((unsigned)cdiv(d->N, 64), (unsigned)cdiv(d->M, 64), (unsigned)(nz > 0 ? nz : 1));
+    VS_REQUIRE(grid.y <= 65535, "vs_gemm: M too large");
+    const float* a = (const float*)d->a;
+    const float* b = (const float*)d->b;
+    if (d->a_kcontig && d->b_kcontig)
+      hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    else if (d->a_kcontig)
+      hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    else if (d->b_kcontig)
+      hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+  }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

@@ -1,0 +1,143 @@
+// vit_exec.hip — native executor for one pre-LN ViT block (mv:419-445) and its backward.
+//
+// Sequencing lives in C++ so a whole block is one host call: 7 launches forward, ~16 backward,
+// all on the caller's stream (graph-capturable: no allocation, no synchronisation).
+// Forward (dtype T = f32 or bf16; residual stream f32):
+//   h1 = LN1(x) [T] -> qkv = h1 Wqkv^T + b [T] -> o = attn(qkv) [T] (+lse)
+//   y = x + o Wproj^T + b [f32] -> h2 = LN2(y) [T] -> a = gelu(h2 W1^T + b1) [T] (pre-act saved)
+//   x' = y + a W2^T + b2 [f32]
+// Backward mirrors it with the weight gradients accumulated in f32 (split-K atomics for the
+// token-reduction dW products, whose K is B*N = 25,088 rows at the bench shape).
+#include "common.h"
+
+namespace vs {
+
+static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t M, int64_t N, int64_t K, const void* a,
+                          int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, uint32_t epi) {
+  vs_gemm_desc d = {};
+  d.dtype = dtype;
+  d.out_dtype = out_dtype;
+  d.a_kcontig = akc;
+  d.b_kcontig = bkc;
+  d.M = M; d.N = N; d.K = K;
+  d.a = a; d.lda = lda;
+  d.b = b; d.ldb = ldb;
+  d.c = c; d.ldc = ldc;
+  d.epilogue = epi;
+  d.alpha = 1.0f;
+  return d;
+}
+
+static int check_layer(const vs_vit_layer* L) {
+  VS_REQUIRE(L, "vs_vit_layer: null");
+  VS_REQUIRE(L->dtype == VS_F32 || L->dtype == VS_BF16, "vs_vit_layer: bad dtype");
+  VS_REQUIRE(L->hidden == L->heads * 64, "vs_vit_layer: hidden must be heads*64");
+  VS_REQUIRE(L->batch > 0 && L->tokens > 0 && L->mlp > 0, "vs_vit_layer: empty");
+  return VS_OK;
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
+  VS_CALL(check_layer(L));
+  const int T = L->dtype;
+  const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
+  VS_CALL(vs_layernorm_fwd(T, M, D, L->x_in, D, L->ln1_g, L->ln1_b, L->ln_eps, L->h1, D, L->mean1, L->rstd1, stream));
+  {
+    vs_gemm_desc g = gdesc(T, T, true, true, M, 3 * D, D, L->h1, D, L->w_qkv, D, L->qkv, 3 * D, VS_EPI_BIAS);
+    g.bias = L->b_qkv;
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_attn_fwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, L->lse, L->attn_scale, stream));
+  {
+    vs_gemm_desc g = gdesc(T, VS_F32, true, true, M, D, D, L->attn_o, D, L->w_proj, D, L->y, D,
+                           VS_EPI_BIAS | VS_EPI_RESIDUAL);
+    g.bias = L->b_proj;
+    g.residual = L->x_in;
+    g.ld_residual = D;
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
+  {
+    vs_gemm_desc g = gdesc(T, T, true, true, M, F, D, L->h2, D, L->w_fc1, D, L->a_act, F, VS_EPI_BIAS | VS_EPI_GELU);
+    g.bias = L->b_fc1;
+    g.aux_out = L->a_pre;
+    g.ld_aux_out = F;
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  {
+    vs_gemm_desc g = gdesc(T, VS_F32, true, true, M, D, F, L->a_act, F, L->w_fc2, F, L->x_out, D,
+                           VS_EPI_BIAS | VS_EPI_RESIDUAL);
+    g.bias = L->b_fc2;
+    g.residual = L->y;
+    g.ld_residual = D;
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  return VS_OK;
+}
+
+extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream) {
+  VS_CALL(check_layer(L));
+  VS_REQUIRE(G && G->dx_out && G->dx_in && G->d_a && G->d_h && G->dy && G->d_o && G->d_qkv && G->attn_ws,
+             "vs_vit_layer_bwd: null gradient buffer");
+  const int T = L->dtype;
+  const bool lp = T == VS_BF16;
+  VS_REQUIRE(!lp || (G->dx_out_lp && G->dy_lp), "vs_vit_layer_bwd: bf16 mode needs dx_out_lp and dy_lp");
+  const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
+  const void* gx = lp ? G->dx_out_lp : (const void*)G->dx_out;  // dx' as a GEMM operand
+  const void* gy = lp ? G->dy_lp : (const void*)G->dy;
+
+  // ---- MLP: x' = y + a W2^T + b2
+  {  // dW2[D,F] += dx'^T a
+    vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_colsum(VS_F32, M, D, G->dx_out, D, G->b_fc2, stream));
+  {  // d(pre-act) = (dx' W2) * gelu'(pre)
+    vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
+    g.aux_in = L->a_pre;
+    g.ld_aux_in = F;
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  {  // dW1[F,D] += da^T h2
+    vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_colsum(T, M, F, G->d_a, F, G->b_fc1, stream));
+  {  // dh2 = da W1
+    vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  // dy = dx' + LN2'(dh2)
+  VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
+                           lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, stream));
+  // ---- attention: y = x + o Wp^T + bp
+  {  // dWp[D,D] += dy^T o
+    vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_colsum(VS_F32, M, D, G->dy, D, G->b_proj, stream));
+  {  // do = dy Wp
+    vs_gemm_desc g = gdesc(T, T, true, false, M, D, D, gy, D, L->w_proj, D, G->d_o, D, 0);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  VS_CALL(vs_attn_bwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, G->d_o, D, L->lse, G->d_qkv,
+                      3 * D, G->attn_ws, L->attn_scale, stream));
+  {  // dWqkv[3D,D] += dqkv^T h1
+    vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  // q and v biases only: the k bias is not a parameter (fixed 0 in the reference, mv:233)
+  VS_CALL(vs_colsum(T, M, D, G->d_qkv, 3 * D, G->b_qkv, stream));
+  VS_CALL(vs_colsum(T, M, D, (const char*)G->d_qkv + 2 * D * esize(T), 3 * D, G->b_qkv + 2 * D, stream));
+  {  // dh1 = dqkv Wqkv
+    vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
+    VS_CALL(vs_gemm(&g, stream));
+  }
+  // dx = dy + LN1'(dh1)
+  VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
+                           lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, stream));
+  return VS_OK;
+}

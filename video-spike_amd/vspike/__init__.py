@@ -1,0 +1,19 @@
+"""vspike — MI355X-native (gfx950) video->spike training hot path of PPWangyc/video-spike.
+
+Drop-in surface (src/utils/utils.py:28-34 of the reference): `NAME2MODEL[config.model.model_class]`
+builds the plugin from `config.model`; `forward(inputs) -> log-rates (B, 100, N)`.  All compute
+runs in libvspike.so (hand-written HIP, include/vspike.h) — there is no CPU fallback.
+"""
+from .config import DictConfig, config_from_kwargs, load_run_config, update_config
+from .linear import Linear
+from .loss import PoissonNLLMeanLoss, poisson_nll_mean
+from .optim import FusedAdamW
+from .vit import VideoMAE
+
+NAME2MODEL = {
+    "Linear": Linear,
+    "VideoMAE": VideoMAE,
+}
+
+__all__ = ["NAME2MODEL", "Linear", "VideoMAE", "FusedAdamW", "poisson_nll_mean", "PoissonNLLMeanLoss",
+           "DictConfig", "update_config", "config_from_kwargs", "load_run_config"]

@@ -1,0 +1,136 @@
+"""ctypes binding of libvspike.so — the C-ABI declared in include/vspike.h.
+
+The library is the ONLY compute path: there is no CPU or torch fallback.  If it is missing, or
+no GPU is visible, the ops raise.  Tensors cross the boundary as raw device pointers + sizes;
+kernels are enqueued on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from .build import LIB_PATH
+
+VS_F32, VS_BF16 = 0, 1
+EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
+EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
+TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM = 0, 1, 2
+
+c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
+                                         ctypes.c_void_p, ctypes.c_size_t)
+
+
+class VsError(RuntimeError):
+    pass
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_i32), ("out_dtype", c_i32), ("a_kcontig", c_i32), ("b_kcontig", c_i32),
+                ("M", c_i64), ("N", c_i64), ("K", c_i64),
+                ("a", c_p), ("lda", c_i64), ("b", c_p), ("ldb", c_i64), ("c", c_p), ("ldc", c_i64),
+                ("epilogue", c_u32), ("alpha", c_f32), ("bias", c_p),
+                ("residual", c_p), ("ld_residual", c_i64), ("pos", c_p), ("pos_rows", c_i64),
+                ("aux_in", c_p), ("ld_aux_in", c_i64), ("aux_out", c_p), ("ld_aux_out", c_i64),
+                ("split_k", c_i32), ("reserved", c_i32)]
+
+
+class VitLayer(ctypes.Structure):
+    _fields_ = [("dtype", c_i32), ("heads", c_i32), ("batch", c_i64), ("tokens", c_i64), ("hidden", c_i64),
+                ("mlp", c_i64), ("ln_eps", c_f32), ("attn_scale", c_f32),
+                ("ln1_g", c_p), ("ln1_b", c_p), ("ln2_g", c_p), ("ln2_b", c_p),
+                ("w_qkv", c_p), ("b_qkv", c_p), ("w_proj", c_p), ("b_proj", c_p),
+                ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
+                ("x_in", c_p), ("h1", c_p), ("mean1", c_p), ("rstd1", c_p), ("qkv", c_p), ("attn_o", c_p),
+                ("lse", c_p), ("y", c_p), ("h2", c_p), ("mean2", c_p), ("rstd2", c_p), ("a_pre", c_p),
+                ("a_act", c_p), ("x_out", c_p)]
+
+
+class VitLayerGrad(ctypes.Structure):
+    _fields_ = [("ln1_g", c_p), ("ln1_b", c_p), ("ln2_g", c_p), ("ln2_b", c_p),
+                ("w_qkv", c_p), ("b_qkv", c_p), ("w_proj", c_p), ("b_proj", c_p),
+                ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
+                ("dx_out", c_p), ("dx_out_lp", c_p), ("dx_in", c_p), ("dx_in_lp", c_p),
+                ("d_a", c_p), ("d_h", c_p), ("dy", c_p), ("dy_lp", c_p), ("d_o", c_p), ("d_qkv", c_p),
+                ("attn_ws", c_p)]
+
+
+# every entry point of include/vspike.h: name -> (restype, argtypes)
+PROTOTYPES = {
+    "vs_version": (ctypes.c_int, []),
+    "vs_last_error": (ctypes.c_char_p, []),
+    "vs_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "vs_struct_size": (ctypes.c_int, [ctypes.c_int]),
+    "vs_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p]),
+    "vs_layernorm_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p,
+                                        c_p]),
+    "vs_layernorm_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
+                                        c_i64, c_p, c_p, c_p, c_p]),
+    "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),
+    "vs_attn_bwd_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "vs_attn_bwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,
+                                   c_p, c_i64, c_p, c_f32, c_p]),
+    "vs_patch_im2col": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "vs_sinusoid_table": (ctypes.c_int, [c_i64, c_i64, c_p, c_p]),
+    "vs_colsum": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
+    "vs_cast": (ctypes.c_int, [c_i32, c_i32, c_i64, c_p, c_p, c_p]),
+    "vs_poisson_workspace_bytes": (c_sz, [c_i64]),
+    "vs_poisson_nll": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_f32, c_p, c_p]),
+    "vs_poisson_nll_bwd": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p]),
+    "vs_adamw": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "vs_vit_layer_fwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), c_p]),
+    "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
+    "vs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "vs_timing_collect": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
+}
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libvspike.so (built in-tree by vspike.build / __graft_entry__.build())."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise VsError(f"libvspike.so not found at {LIB_PATH}: build it with `python -m vspike.build` "
+                          "(or __graft_entry__.build()); there is no fallback path")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        for which, st in enumerate((GemmDesc, VitLayer, VitLayerGrad)):
+            got = handle.vs_struct_size(which)
+            if got != ctypes.sizeof(st):
+                raise VsError(f"ABI mismatch: {st.__name__} is {ctypes.sizeof(st)} B in Python, {got} B in C")
+        _LIB = handle
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().vs_last_error().decode() if rc == -1 else f"HIP error {rc}"
+        raise VsError(f"{what}: {msg}")
+
+
+def stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return VS_F32
+    if dt == torch.bfloat16:
+        return VS_BF16
+    raise VsError(f"unsupported dtype {dt} (float32 / bfloat16 only)")
+
+
+def require_device(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise VsError("vspike ops run on the GPU only (tensor on %s); there is no CPU fallback" % t.device)

@@ -1,0 +1,79 @@
+"""Build libvspike.so (hipcc, gfx950 only) in-tree: video-spike_amd/vspike/_build/libvspike.so.
+
+No torch extension machinery: the library is a plain C-ABI shared object (include/vspike.h)
+loaded with ctypes, so it builds in seconds and travels with the repo snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+SRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
+ROOT = os.path.dirname(os.path.dirname(PKG_DIR))
+INCLUDE = os.path.join(ROOT, "include")
+BUILD_DIR = os.path.join(PKG_DIR, "_build")
+LIB_PATH = os.path.join(BUILD_DIR, "libvspike.so")
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libvspike)")
+
+
+def _flags():
+    return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", SRC_DIR,
+            "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _needs(obj: str, deps) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(SRC_DIR, "*.h"))) + [os.path.join(INCLUDE, "vspike.h")]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(BUILD_DIR, os.path.basename(s)[:-4] + ".o")
+        objs.append(o)
+        if force or _needs(o, [s] + headers):
+            todo.append((s, o))
+
+    def compile_one(so):
+        s, o = so
+        cmd = [hipcc, *_flags(), "-c", s, "-o", o]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+        return s
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            for s in ex.map(compile_one, todo):
+                if verbose:
+                    print(f"[vspike.build] compiled {os.path.basename(s)}", file=sys.stderr)
+    if force or todo or _needs(LIB_PATH, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        if verbose:
+            print(f"[vspike.build] linked {LIB_PATH}", file=sys.stderr)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,184 @@
+"""Tensor-level wrappers over the libvspike C-ABI (one function per entry point).
+
+Each wrapper validates devices, passes raw pointers + sizes and enqueues on the current stream.
+Outputs are caller-allocated tensors (the PyTorch caching allocator owns all memory).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib as L
+from ._lib import check, lib, ptr, require_device, stream
+
+
+def gemm(a, b, c, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, ldc, epilogue=0, alpha=1.0, bias=None,
+         residual=None, ld_residual=0, pos=None, pos_rows=0, aux_in=None, ld_aux_in=0, aux_out=None,
+         ld_aux_out=0, split_k=0):
+    """C[M,N] = epilogue(alpha * A @ B); layouts as in include/vspike.h (vs_gemm)."""
+    require_device(a, b, c)
+    d = L.GemmDesc()
+    d.dtype = L.dtype_code(a.dtype)
+    if L.dtype_code(b.dtype) != d.dtype:
+        raise L.VsError("gemm: A and B must share a dtype")
+    d.out_dtype = L.dtype_code(c.dtype)
+    d.a_kcontig, d.b_kcontig = int(a_kcontig), int(b_kcontig)
+    d.M, d.N, d.K = M, N, K
+    d.a, d.lda, d.b, d.ldb, d.c, d.ldc = a.data_ptr(), lda, b.data_ptr(), ldb, c.data_ptr(), ldc
+    d.epilogue, d.alpha = epilogue, alpha
+    d.bias = ptr(bias)
+    d.residual, d.ld_residual = ptr(residual), ld_residual
+    d.pos, d.pos_rows = ptr(pos), pos_rows
+    d.aux_in, d.ld_aux_in = ptr(aux_in), ld_aux_in
+    d.aux_out, d.ld_aux_out = ptr(aux_out), ld_aux_out
+    d.split_k = split_k
+    check(lib().vs_gemm(ctypes.byref(d), stream()), "vs_gemm")
+    return c
+
+
+def linear(x, w, out, *, bias=None, epilogue=0, **kw):
+    """out[M,N] = x[M,K] @ w[N,K]^T (+ epilogue): the nn.Linear forward."""
+    M, K = x.shape
+    N = w.shape[0]
+    if bias is not None:
+        epilogue |= L.EPI_BIAS
+    return gemm(x, w, out, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=x.stride(0), ldb=w.stride(0),
+                ldc=out.stride(0), epilogue=epilogue, bias=bias, **kw)
+
+
+def linear_dx(dy, w, out, *, epilogue=0, **kw):
+    """out[M,K] = dy[M,N] @ w[N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    return gemm(dy, w, out, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=dy.stride(0), ldb=w.stride(0),
+                ldc=out.stride(0), epilogue=epilogue, **kw)
+
+
+def linear_dw(dy, x, dw, *, accumulate=True):
+    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw; split-K atomics over the M reduction)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    epi = L.EPI_ATOMIC if accumulate else 0
+    return gemm(dy, x, dw, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=dy.stride(0), ldb=x.stride(0),
+                ldc=dw.stride(0), epilogue=epi, split_k=0 if accumulate else 1)
+
+
+def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd):
+    require_device(x, y)
+    rows, cols = x.shape
+    check(lib().vs_layernorm_fwd(L.dtype_code(y.dtype), rows, cols, x.data_ptr(), x.stride(0), gamma.data_ptr(),
+                                 beta.data_ptr(), eps, y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr(),
+                                 stream()), "vs_layernorm_fwd")
+    return y
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=None):
+    require_device(dy, x, dx)
+    rows, cols = x.shape
+    check(lib().vs_layernorm_bwd(rows, cols, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
+                                 rstd.data_ptr(), gamma.data_ptr(), ptr(dres), dres.stride(0) if dres is not None else 0,
+                                 dx.data_ptr(), dx.stride(0), ptr(dx_lp), dgamma.data_ptr(), dbeta.data_ptr(),
+                                 stream()), "vs_layernorm_bwd")
+    return dx
+
+
+def attn_fwd(qkv, o, lse, B, N, H, scale=0.125):
+    require_device(qkv, o, lse)
+    check(lib().vs_attn_fwd(L.dtype_code(qkv.dtype), B, N, H, 64, qkv.data_ptr(), qkv.stride(0), o.data_ptr(),
+                            o.stride(0), lse.data_ptr(), scale, stream()), "vs_attn_fwd")
+    return o
+
+
+def attn_bwd_workspace_bytes(B, N, H):
+    return int(lib().vs_attn_bwd_workspace_bytes(B, N, H, 64))
+
+
+def attn_bwd(qkv, o, dout, lse, dqkv, workspace, B, N, H, scale=0.125):
+    require_device(qkv, o, dout, lse, dqkv, workspace)
+    check(lib().vs_attn_bwd(L.dtype_code(qkv.dtype), B, N, H, 64, qkv.data_ptr(), qkv.stride(0), o.data_ptr(),
+                            o.stride(0), dout.data_ptr(), dout.stride(0), lse.data_ptr(), dqkv.data_ptr(),
+                            dqkv.stride(0), workspace.data_ptr(), scale, stream()), "vs_attn_bwd")
+    return dqkv
+
+
+def patch_im2col(pixels, cols, tubelet, patch):
+    require_device(pixels, cols)
+    B, F, C, H, W = pixels.shape
+    check(lib().vs_patch_im2col(L.dtype_code(cols.dtype), B, F, C, H, W, tubelet, patch, pixels.data_ptr(),
+                                cols.data_ptr(), stream()), "vs_patch_im2col")
+    return cols
+
+
+def sinusoid_table(n_pos, dim, device):
+    out = torch.empty(n_pos, dim, dtype=torch.float32, device=device)
+    check(lib().vs_sinusoid_table(n_pos, dim, out.data_ptr(), stream()), "vs_sinusoid_table")
+    return out
+
+
+def colsum(x, out, rows=None, cols=None):
+    """out[c] += sum_r x[r, c] (out f32)."""
+    require_device(x, out)
+    rows = x.shape[0] if rows is None else rows
+    cols = x.shape[1] if cols is None else cols
+    check(lib().vs_colsum(L.dtype_code(x.dtype), rows, cols, x.data_ptr(), x.stride(0), out.data_ptr(), stream()),
+          "vs_colsum")
+    return out
+
+
+def cast(x, out):
+    require_device(x, out)
+    check(lib().vs_cast(L.dtype_code(x.dtype), L.dtype_code(out.dtype), x.numel(), x.data_ptr(), out.data_ptr(),
+                        stream()), "vs_cast")
+    return out
+
+
+def poisson_nll(log_rate, target, loss_out, dx=None, grad_scale=1.0, workspace=None):
+    require_device(log_rate, target, loss_out)
+    n = log_rate.numel()
+    if workspace is None:
+        workspace = torch.empty(int(lib().vs_poisson_workspace_bytes(n)) // 4, dtype=torch.float32,
+                                device=log_rate.device)
+    check(lib().vs_poisson_nll(n, log_rate.data_ptr(), target.data_ptr(), loss_out.data_ptr(), ptr(dx), grad_scale,
+                               workspace.data_ptr(), stream()), "vs_poisson_nll")
+    return loss_out
+
+
+def poisson_nll_bwd(log_rate, target, grad_out, dx):
+    require_device(log_rate, target, grad_out, dx)
+    check(lib().vs_poisson_nll_bwd(log_rate.numel(), log_rate.data_ptr(), target.data_ptr(), grad_out.data_ptr(),
+                                   dx.data_ptr(), stream()), "vs_poisson_nll_bwd")
+    return dx
+
+
+def adamw(param, grad, exp_avg, exp_avg_sq, hyper, param_lp=None):
+    require_device(param, grad, exp_avg, exp_avg_sq, hyper)
+    check(lib().vs_adamw(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                         ptr(param_lp), hyper.data_ptr(), stream()), "vs_adamw")
+
+
+def vit_layer_fwd(layer_struct):
+    check(lib().vs_vit_layer_fwd(ctypes.byref(layer_struct), stream()), "vs_vit_layer_fwd")
+
+
+def vit_layer_bwd(layer_struct, grad_struct):
+    check(lib().vs_vit_layer_bwd(ctypes.byref(layer_struct), ctypes.byref(grad_struct), stream()),
+          "vs_vit_layer_bwd")
+
+
+# ---- timing (bench instrumentation) -----------------------------------------------------------
+def timing_enable(mask: int):
+    """mask: OR of (1 << TIMER_*); 0 disables and discards recorded events."""
+    check(lib().vs_timing_enable(int(mask)), "vs_timing_enable")
+
+
+def timing_collect(timer: int):
+    n = ctypes.c_int64(0)
+    ms = ctypes.c_double(0.0)
+    check(lib().vs_timing_collect(timer, ctypes.byref(n), ctypes.byref(ms)), "vs_timing_collect")
+    return int(n.value), float(ms.value)
+
+
+def attn_scale(head_dim: int = 64) -> float:
+    return 1.0 / math.sqrt(head_dim)

@@ -1,0 +1,345 @@
+"""VideoMAE plugin — drop-in for the reference's `src/model/videomae.py:4-36` (NAME2MODEL['VideoMAE']).
+
+Reference behaviour kept:
+  * constructor `VideoMAE(config.model)` with `encoder.output_dim` / `decoder.output_dim`
+    (videomae.py:13-14; decoder.output_dim = 100 * neurons injected by src/train.py:41);
+  * `forward(x) -> log-rates (B, 100, N)` (videomae.py:31); consumed by
+    PoissonNLLLoss(log_input=True) (src/train.py:59);
+  * the encoder is frozen by default (videomae.py:12,17,34-36) — `freeze_encoder: false`
+    trains it (north-star mode); ViT geometry from an optional `backbone:` section, default
+    videomae-base (ViT-B/16, tubelet 2, 1568 tokens).
+MI355X design: parameters live in two flat f32 buffers (layout.py); every op runs in libvspike
+(im2col + patch GEMM with the sinusoid table fused in its epilogue, 12 native block executors,
+split-K head GEMM) and the whole backward is hand-sequenced here (no autograd graph inside).
+`compute_dtype: bf16` runs activations/weights in bf16 with f32 accumulation, f32 residual stream,
+f32 master weights and f32 weight gradients.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from . import ops
+from .layout import BackboneCfg, VitLayout
+from .memory import Arena
+
+_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
+           "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+def _cfg_get(config, key, default=None):
+    try:
+        return config[key] if key in config else default
+    except TypeError:
+        return getattr(config, key, default)
+
+
+class VideoMAE(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.backbone = BackboneCfg.from_config(_cfg_get(config, "backbone"))
+        self.freeze_encoder = bool(_cfg_get(config, "freeze_encoder", True))
+        self.compute_dtype = _DTYPES[str(_cfg_get(config, "compute_dtype", "fp32")).lower()]
+        enc_out = int(config["encoder"]["output_dim"])
+        out_dim = int(config["decoder"]["output_dim"])
+        if out_dim % 100:
+            raise ValueError("decoder.output_dim must be 100 * neurons (src/train.py:41)")
+        cfg = self.backbone
+        if cfg.hidden_size != 64 * cfg.num_attention_heads:
+            raise ValueError("this build supports head dim 64 (hidden_size = 64 * num_attention_heads)")
+        self.layout = VitLayout(cfg, enc_out, out_dim)
+        self.enc_flat = nn.Parameter(torch.zeros(self.layout.enc.numel), requires_grad=not self.freeze_encoder)
+        self.head_flat = nn.Parameter(torch.zeros(self.layout.head.numel))
+        # uniform 16-of-120 frame selection of the raw-video path (videomae.py:10-11)
+        self.register_buffer("frame_indices", (torch.linspace(0, 1, cfg.num_frames) * 119).long(), persistent=False)
+        self.grad_sink = None          # set by vspike.dp.GradExchange for overlapped all-reduce
+        self._pos_cache = {}
+        self.reset_parameters()
+
+    # ---------------------------------------------------------------------------------------
+    # parameters
+    # ---------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def reset_parameters(self, generator: Optional[torch.Generator] = None):
+        """HF VideoMAE `_init_weights` for the encoder (modeling_videomae.py:512-522): N(0, 0.02)
+        weights, zero biases, LayerNorm (1, 0); nn.Linear default init for the head."""
+        enc, head, lay = self.enc_flat, self.head_flat, self.layout
+        enc.zero_()
+        for name, slot in lay.enc.slots.items():
+            v = lay.enc.view(enc, name)
+            if name.endswith(("ln1_g", "ln2_g")):
+                v.fill_(1.0)
+            elif len(slot.shape) == 2:
+                v.normal_(0.0, 0.02, generator=generator)
+        head.zero_()
+        for wname, bname in (("enc_w", "enc_b"), ("dec_w", "dec_b")):
+            w = lay.head.view(head, wname)
+            bound = 1.0 / math.sqrt(w.shape[1])
+            w.uniform_(-bound, bound, generator=generator)
+            lay.head.view(head, bname).uniform_(-bound, bound, generator=generator)
+
+    def _flat(self, which):
+        return self.enc_flat if which == "enc" else self.head_flat
+
+    def _flat_layout(self, which):
+        return self.layout.enc if which == "enc" else self.layout.head
+
+    def reference_state_dict(self):
+        """Parameters under the reference plugin's names (HF VideoMAEModel + two Linears)."""
+        out = {}
+        for name, which, slot, rows in self.layout.hf_items():
+            t = self._flat_layout(which).view(self._flat(which).detach(), slot)
+            if slot == "patch_w":
+                t = t.view(self.backbone.hidden_size, self.backbone.num_channels, self.backbone.tubelet_size,
+                           self.backbone.patch_size, self.backbone.patch_size)
+            out[name] = (t if rows is None else t[rows]).clone()
+        return out
+
+    @torch.no_grad()
+    def load_reference_state_dict(self, sd, strict: bool = True):
+        """Load reference-named weights (e.g. a videomae-base checkpoint + head).  The k-bias of
+        newer HF versions must be zero (4.38 has none: modeling_videomae.py:233)."""
+        seen = set()
+        for name, which, slot, rows in self.layout.hf_items():
+            if name not in sd:
+                if strict:
+                    raise KeyError(f"missing {name}")
+                continue
+            dst = self._flat_layout(which).view(self._flat(which), slot)
+            src = torch.as_tensor(sd[name]).to(dst.device, torch.float32).reshape(
+                dst[rows].shape if rows is not None else dst.shape)
+            (dst[rows] if rows is not None else dst).copy_(src)
+            seen.add(name)
+        for k, v in sd.items():
+            if k.endswith("attention.attention.key.bias"):
+                if torch.as_tensor(v).abs().max() != 0:
+                    raise ValueError(f"{k} is non-zero; the reference encoder has no key bias")
+                seen.add(k)
+        if strict:
+            extra = set(sd) - seen
+            if extra:
+                raise KeyError(f"unexpected keys: {sorted(extra)[:5]}")
+
+    # ---------------------------------------------------------------------------------------
+    # forward
+    # ---------------------------------------------------------------------------------------
+    def forward(self, inputs: torch.Tensor) -> torch.Tensor:
+        cfg = self.backbone
+        if inputs.dim() != 5:
+            raise ValueError("VideoMAE expects a 5-D tensor")
+        if tuple(inputs.shape[1:]) != (cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size):
+            raise NotImplementedError(
+                f"expected pixel_values (B, {cfg.num_frames}, {cfg.num_channels}, {cfg.image_size}, {cfg.image_size}); "
+                "the reference's CPU preprocessing of raw (B, 120, 1, 128, 128) video (videomae.py:18-25) is not "
+                "on this device path yet")
+        L.require_device(inputs)
+        pixels = inputs.detach().to(torch.float32).contiguous()
+        return _VideoMAEFn.apply(pixels, self.enc_flat, self.head_flat, self)
+
+    def _pos_table(self, device):
+        key = str(device)
+        if key not in self._pos_cache:
+            self._pos_cache[key] = ops.sinusoid_table(self.backbone.num_tokens, self.backbone.hidden_size, device)
+        return self._pos_cache[key]
+
+    def __getstate__(self):
+        st = super().__getstate__() if hasattr(super(), "__getstate__") else self.__dict__.copy()
+        st = dict(st)
+        st["_pos_cache"] = {}
+        st["grad_sink"] = None
+        return st
+
+    # activation buffers of one block (names match VitLayer fields)
+    def _plan_layer(self, ar: Arena, pfx: str, B: int):
+        cfg, dt = self.backbone, self.compute_dtype
+        N, D, F, H = cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads
+        M = B * N
+        for name, shape, d in (("h1", (M, D), dt), ("mean1", (M,), torch.float32), ("rstd1", (M,), torch.float32),
+                               ("qkv", (M, 3 * D), dt), ("attn_o", (M, D), dt), ("lse", (B, H, N), torch.float32),
+                               ("y", (M, D), torch.float32), ("h2", (M, D), dt), ("mean2", (M,), torch.float32),
+                               ("rstd2", (M,), torch.float32), ("a_pre", (M, F), dt), ("a_act", (M, F), dt)):
+            ar.add(pfx + name, shape, d)
+
+    def _layer_struct(self, i, B, x_in, x_out, act, pfx, w_lp, w32):
+        cfg = self.backbone
+        lay = self.layout.enc
+        s = L.VitLayer()
+        s.dtype = L.dtype_code(self.compute_dtype)
+        s.heads = cfg.num_attention_heads
+        s.batch, s.tokens, s.hidden, s.mlp = B, cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size
+        s.ln_eps = cfg.layer_norm_eps
+        s.attn_scale = 1.0 / math.sqrt(64.0)
+        for k in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "b_qkv", "b_proj", "b_fc1", "b_fc2"):
+            setattr(s, k, lay.view(w32, f"{i}.{k}").data_ptr())
+        for k in ("w_qkv", "w_proj", "w_fc1", "w_fc2"):
+            setattr(s, k, lay.view(w_lp, f"{i}.{k}").data_ptr())
+        s.x_in, s.x_out = x_in.data_ptr(), x_out.data_ptr()
+        for k in ("h1", "mean1", "rstd1", "qkv", "attn_o", "lse", "y", "h2", "mean2", "rstd2", "a_pre", "a_act"):
+            setattr(s, k, act[pfx + k].data_ptr())
+        return s
+
+    def _lowp(self, flat):
+        if self.compute_dtype == torch.float32:
+            return flat
+        out = torch.empty(flat.shape, dtype=self.compute_dtype, device=flat.device)
+        ops.cast(flat, out)
+        return out
+
+    def _run_forward(self, pixels, save_encoder: bool):
+        cfg, dt = self.backbone, self.compute_dtype
+        B = pixels.shape[0]
+        N, D, Lyr = cfg.num_tokens, cfg.hidden_size, cfg.num_hidden_layers
+        M = B * N
+        dev = pixels.device
+        enc32, head32 = self.enc_flat.detach(), self.head_flat.detach()
+        enc_lp, head_lp = self._lowp(enc32), self._lowp(head32)
+        le, lh = self.layout.enc, self.layout.head
+
+        ar = Arena()
+        ar.add("cols", (M, cfg.patch_dim), dt)
+        ar.add("x0", (M, D), torch.float32)
+        n_sets = Lyr if save_encoder else 1
+        for j in range(n_sets):
+            self._plan_layer(ar, f"L{j}.", B)
+        for j in range(Lyr if save_encoder else 2):
+            ar.add(f"X{j}", (M, D), torch.float32)
+        if dt != torch.float32:
+            ar.add("x_lp", (B, N * D), dt)
+        ar.add("z", (B, self.layout.enc_out), torch.float32)
+        ar.add("r", (B, self.layout.out_dim), torch.float32)
+        act = ar.allocate(dev)
+
+        ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
+        ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
+                   epilogue=L.EPI_POS, pos=self._pos_table(dev), pos_rows=N)
+        x = act["x0"]
+        structs = []
+        for i in range(Lyr):
+            j = i if save_encoder else 0
+            x_out = act[f"X{i}"] if save_encoder else act[f"X{i % 2}"]
+            s = self._layer_struct(i, B, x, x_out, act, f"L{j}.", enc_lp, enc32)
+            ops.vit_layer_fwd(s)
+            structs.append(s)
+            x = x_out
+        x_flat = x.view(B, N * D)
+        if dt != torch.float32:
+            ops.cast(x_flat, act["x_lp"])
+            x_flat_lp = act["x_lp"]
+        else:
+            x_flat_lp = x_flat
+        z, r = act["z"], act["r"]
+        z.zero_()
+        ops.gemm(x_flat_lp, lh.view(head_lp, "enc_w"), z, M=B, N=self.layout.enc_out, K=N * D, a_kcontig=True,
+                 b_kcontig=True, lda=N * D, ldb=N * D, ldc=self.layout.enc_out, epilogue=L.EPI_ATOMIC | L.EPI_BIAS,
+                 bias=lh.view(head32, "enc_b"))
+        ops.linear(z, lh.view(head32, "dec_w"), r, bias=lh.view(head32, "dec_b"))
+        state = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_flat_lp": x_flat_lp,
+                 "x_final": x, "B": B}
+        return r.view(B, 100, -1), state
+
+    # ---------------------------------------------------------------------------------------
+    # backward
+    # ---------------------------------------------------------------------------------------
+    def _grad_buffer(self, p):
+        if self.grad_sink is not None:
+            return self.grad_sink.grad_buffer(p)
+        return torch.zeros_like(p)
+
+    def _ready(self, p, lo, hi):
+        if self.grad_sink is not None:
+            self.grad_sink.mark_ready(p, lo, hi)
+
+    def _run_backward(self, st, d_logrates, want_enc: bool, want_head: bool):
+        cfg, dt = self.backbone, self.compute_dtype
+        B = st["B"]
+        N, D, F, Lyr = cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
+        H = cfg.num_attention_heads
+        M = B * N
+        lay, le, lh = self.layout, self.layout.enc, self.layout.head
+        act = st["act"]
+        dev = d_logrates.device
+        head32 = self.head_flat.detach()
+        dr = d_logrates.reshape(B, lay.out_dim).to(torch.float32).contiguous()
+
+        g_head = self._grad_buffer(self.head_flat) if want_head else None
+        Gh = lambda n: lh.view(g_head, n)  # noqa: E731
+        z = act["z"]
+        dz = torch.empty(B, lay.enc_out, dtype=torch.float32, device=dev)
+        ops.linear_dx(dr, lh.view(head32, "dec_w"), dz)
+        if dt != torch.float32:
+            dz_lp = torch.empty(B, lay.enc_out, dtype=dt, device=dev)
+            ops.cast(dz, dz_lp)
+        else:
+            dz_lp = dz
+        if want_head:
+            ops.linear_dw(dr, z, Gh("dec_w"))
+            ops.colsum(dr, Gh("dec_b"))
+            ops.colsum(dz, Gh("enc_b"))
+            ops.linear_dw(dz_lp, st["x_flat_lp"], Gh("enc_w"))
+            self._ready(self.head_flat, 0, self.head_flat.numel())
+        if not want_enc:
+            return None, g_head
+
+        g_enc = self._grad_buffer(self.enc_flat)
+        Ge = lambda n: le.view(g_enc, n)  # noqa: E731
+        ar = Arena()
+        for k, shape, d in (("d_a", (M, F), dt), ("d_h", (M, D), torch.float32), ("dy", (M, D), torch.float32),
+                            ("d_o", (M, D), dt), ("d_qkv", (M, 3 * D), dt), ("dxA", (M, D), torch.float32),
+                            ("dxB", (M, D), torch.float32)):
+            ar.add(k, shape, d)
+        if dt != torch.float32:
+            for k in ("dy_lp", "dxA_lp", "dxB_lp"):
+                ar.add(k, (M, D), dt)
+        ar.add("attn_ws", (ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64,), torch.float32)
+        g = ar.allocate(dev)
+        lp = dt != torch.float32
+
+        dx, dx_lp = g["dxA"], (g["dxA_lp"] if lp else None)
+        ops.linear_dx(dz_lp, lh.view(st["head_lp"], "enc_w"), dx.view(B, N * D))
+        if lp:
+            ops.cast(dx, dx_lp)
+        for i in reversed(range(Lyr)):
+            s = st["structs"][i]
+            gs = L.VitLayerGrad()
+            for k in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "w_qkv", "b_qkv", "w_proj", "b_proj", "w_fc1", "b_fc1",
+                      "w_fc2", "b_fc2"):
+                setattr(gs, k, Ge(f"{i}.{k}").data_ptr())
+            nxt = "dxB" if dx is g["dxA"] else "dxA"
+            gs.dx_out, gs.dx_out_lp = dx.data_ptr(), L.ptr(dx_lp)
+            gs.dx_in, gs.dx_in_lp = g[nxt].data_ptr(), (g[nxt + "_lp"].data_ptr() if lp else None)
+            gs.d_a, gs.d_h, gs.dy = g["d_a"].data_ptr(), g["d_h"].data_ptr(), g["dy"].data_ptr()
+            gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
+            gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
+            ops.vit_layer_bwd(s, gs)
+            dx, dx_lp = g[nxt], (g[nxt + "_lp"] if lp else None)
+            lo, hi = lay.layer_ranges[i]
+            self._ready(self.enc_flat, lo, hi)
+        # patch embedding: dW = dx0^T cols, db = colsum(dx0); the position table is fixed
+        ops.linear_dw(dx_lp if lp else dx, act["cols"], Ge("patch_w"))
+        ops.colsum(dx, Ge("patch_b"))
+        self._ready(self.enc_flat, 0, lay.layer_ranges[0][0] if lay.layer_ranges else self.enc_flat.numel())
+        return g_enc, g_head
+
+
+class _VideoMAEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pixels, enc_flat, head_flat, mod):
+        want_enc = bool(ctx.needs_input_grad[1])
+        out, st = mod._run_forward(pixels, save_encoder=want_enc)
+        ctx.mod, ctx.st = mod, st
+        ctx.want = (want_enc, bool(ctx.needs_input_grad[2]))
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad):
+        mod = ctx.mod
+        g_enc, g_head = mod._run_backward(ctx.st, grad, *ctx.want)
+        ctx.st = None
+        if mod.grad_sink is not None:          # the sink owns .grad (all-reduced in place)
+            return None, None, None, None
+        return None, g_enc, g_head, None
