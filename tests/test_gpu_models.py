@@ -180,4 +180,6 @@ def test_state_dict_roundtrip_and_pickle(tmp_path):
     m2 = torch.load(tmp_path / "m.pt", weights_only=False)["model"]    # our own file
     px = torch.from_numpy(cpu_ref.make_pixels(cfg, 1)).to(DEV)
     with torch.no_grad():
-        assert torch.equal(m(px), m2(px))
+        a, b = m(px), m2(px)
+    # not bit-exact: the split-K head GEMM sums with f32 atomics in arrival order
+    assert (a - b).abs().max().item() <= 1e-5 * a.abs().max().item()
