@@ -82,6 +82,8 @@ typedef struct vs_gemm_desc {
   void* aux_out;         int64_t ld_aux_out;  /* operand dtype */
   int32_t split_k;      /* 0 = auto; >1 needs VS_EPI_ATOMIC */
   int32_t reserved;
+  float* a_rowsum;      /* optional [M] f32: += sum_k A(m,k) (the bias gradient of a dW = dY^T X
+                           product, fused: replaces a separate column-sum pass over dY) */
 } vs_gemm_desc;
 
 int vs_gemm(const vs_gemm_desc* d, void* stream);

@@ -109,9 +109,11 @@ def test_gemm_splitk_atomic_accumulates(dtype):
     dy = _rand(K, M, seed=8).to(dtype)
     x = _rand(K, N, seed=9).to(dtype)
     c = torch.ones(M, N, device=DEV)   # accumulates on top of existing values
-    ops.linear_dw(dy.to(DEV), x.to(DEV), c)
+    db = torch.full((M,), 3.0, device=DEV)
+    ops.linear_dw(dy.to(DEV), x.to(DEV), c, db=db)   # bias gradient fused (row sums of A = dy^T)
     ref = dy.double().t() @ x.double() + 1.0
     assert rel(c, ref) < 2e-5
+    assert rel(db, dy.double().sum(0) + 3.0) < 2e-5
 
 
 # ----------------------------------------------------------------------------------- LayerNorm
@@ -234,12 +236,19 @@ def test_sinusoid_table_matches_oracle():
     assert (t.cpu() - cpu_ref.sinusoid_table(1568, 192)).abs().max().item() < 1e-6
 
 
-def test_colsum_and_cast():
+@pytest.mark.parametrize("rows,cols,dtype", [(1000, 300, torch.float32), (25088, 192, torch.bfloat16),
+                                             (777, 576, torch.float32), (64, 8, torch.bfloat16)])
+def test_colsum(rows, cols, dtype):
     from vspike import ops
-    x = _rand(1000, 300, seed=50)
-    out = torch.full((300,), 2.0, device=DEV)
+    x = _rand(rows, cols, seed=50).to(dtype)
+    out = torch.full((cols,), 2.0, device=DEV)
     ops.colsum(x.to(DEV), out)
     assert rel(out, x.double().sum(0) + 2.0) < 1e-5
+
+
+def test_cast():
+    from vspike import ops
+    x = _rand(1000, 300, seed=50)
     xb = torch.empty(1000, 300, dtype=torch.bfloat16, device=DEV)
     ops.cast(x.to(DEV), xb)
     assert torch.equal(xb.cpu(), x.to(torch.bfloat16))

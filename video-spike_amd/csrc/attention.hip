@@ -7,11 +7,11 @@
 //     xor-32 swap per 64-key tile.  The exponentiated S^T accumulator is directly the B operand of
 //     O^T += V^T P^T (no LDS round trip); V^T fragments come from ds_read_tr16_b64 on the V tile.
 //     K/V tiles (64 keys) are register-staged into double-buffered, XOR-swizzled LDS images.
-//   backward: workgroup = 4 waves = 128 keys; each wave keeps its 32 keys' K, V as MFMA operands
-//     and dK^T, dV^T in accumulators while sweeping 32-query blocks (Q, dO staged in LDS).  S and
-//     dP are computed with the key on the lane (accumulators initialised with -LSE/scale and
-//     -delta), so P and dS feed dV^T/dK^T directly; only dS^T crosses LDS for dQ, which is summed
-//     across key blocks with f32 atomics and rounded once by a convert kernel.
+//   backward: two atomic-free kernels.  dK/dV is key-major (each wave keeps 32 keys' K, V as MFMA
+//     operands and dK^T, dV^T in accumulators while sweeping 32-query blocks); dQ is query-major
+//     like the forward (LSE and delta are per-lane constants).  Summing dQ across key blocks with
+//     f32 atomics instead was measured atomic-rate-bound (~489 MB of adds per ViT-Tiny launch at
+//     ~1.3 TB/s: 466 us/launch, profiles/r01_v0_kernel_stats.csv), so dQ recomputes S and dP.
 // f32 (parity) path — exact-f32 VALU kernels: 4 lanes per query/key row, K/V (or Q/dO) tiles in
 //   LDS, expf/logf in f32.  Used for the 1e-4-relative parity mode.
 #include <math.h>
@@ -412,16 +412,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16_t* __r
   }
 }
 
-// ------------------------------------------------------------------ backward
-__global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                               const bf16_t* __restrict__ dout, int64_t lddo,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ delta,
-                                                               float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv,
-                                                               int64_t ldd, int N, int H, float scale) {
-  constexpr int QT = 32 * 128;             // 32 rows x 128 B
-  constexpr int OFF_Q = 0, OFF_DO = 2 * QT, OFF_L = 4 * QT, OFF_DEL = OFF_L + 256, OFF_K = OFF_DEL + 256,
-                OFF_DS = OFF_K + 128 * 128, TOTAL = OFF_DS + 128 * 64;
+// ------------------------------------------------------------------ backward: dK, dV
+// Key-major.  Workgroup = 4 waves x 32 keys; each wave holds its keys' K, V as MFMA B operands and
+// dK^T, dV^T in accumulators while the workgroup sweeps 32-query blocks (Q, dO, LSE, delta staged
+// in double-buffered LDS; ONE barrier per block).  S and dP are produced with the key on the lane
+// and the query on the accumulator row, initialised with -LSE/scale and -delta, so P and dS are
+// directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands: ds_read_tr16_b64).
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                    const bf16_t* __restrict__ dout, int64_t lddo,
+                                                                    const float* __restrict__ lse,
+                                                                    const float* __restrict__ delta,
+                                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N,
+                                                                    int H, float scale) {
+  constexpr int QT = 32 * 128;  // 32 rows x 128 B
+  constexpr int OFF_Q = 0, OFF_DO = 2 * QT, OFF_L = 4 * QT, OFF_DEL = OFF_L + 256, TOTAL = OFF_DEL + 256;
   __shared__ __attribute__((aligned(16))) char smem[TOTAL];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
   const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
@@ -432,13 +436,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
   const bf16_t* Dp = dout + row0 * lddo + h * 64;
   const float* L = lse + ((int64_t)b * H + h) * N;
   const float* Del = delta + ((int64_t)b * H + h) * N;
-  const int kb0 = blockIdx.x * 128;
-  const int kl = wid * 32 + (lane & 31);  // key within the workgroup
-  const int ki = kb0 + kl;
+  const int ki = blockIdx.x * 128 + wid * 32 + (lane & 31);
   const float inv_scale = 1.f / scale;
   const float c2 = scale * kLog2e;
 
-  // K, V of this wave's keys as B operands: lane holds row ki, dh = 16s + 8hh + 0..7
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -450,18 +451,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
       vf[s] = bf16x8{};
     }
   }
-  // K tile of the workgroup for dQ (half-row swizzle, read transposed)
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int id = tid + 256 * s, key = id >> 3, c = id & 7;
-    const int gk = kb0 + key;
-    const uint4 v = gk < N ? *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8) : make_uint4(0, 0, 0, 0);
-    *(uint4*)(smem + OFF_K + key * 128 + ((c ^ swz_half(key)) << 4)) = v;
-  }
-
   f32x16 dkacc[2], dvacc[2];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) dkacc[0][r] = dkacc[1][r] = dvacc[0][r] = dvacc[1][r] = 0.f;
+  for (int r = 0; r < 16; ++r) {
+    dkacc[0][r] = 0.f;
+    dkacc[1][r] = 0.f;
+    dvacc[0][r] = 0.f;
+    dvacc[1][r] = 0.f;
+  }
 
   uint4 rq, rd;
   float rl = 0.f;
@@ -496,9 +493,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
   store_q(0);
   __syncthreads();
   const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
-  const int dtile = wid & 1, khalf = wid >> 1;
-  float* dq_base = dq_acc + row0 * D + h * 64 + dtile * 32 + (lane & 31);
-
+  const int qrow = lane & 31;
   for (int qb = 0; qb < nqb; ++qb) {
     const int buf = qb & 1;
     const char* sQ = smem + OFF_Q + buf * QT;
@@ -508,7 +503,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
     const bool more = qb + 1 < nqb;
     if (more) load_q(qb + 1);
 
-    // S - LSE/scale and dP - delta, key on the lane, query on the accumulator row
     f32x16 sacc, dpacc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -516,7 +510,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
       sacc[r] = -sL[ql];
       dpacc[r] = -sDel[ql];
     }
-    const int qrow = lane & 31;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int coff = qrow * 128 + (((2 * s + hh) ^ swz_row(qrow)) << 4);
@@ -528,10 +521,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
     float p[16], ds[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      p[r] = exp2f(sacc[r] * c2);
+      p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2);
       ds[r] = p[r] * dpacc[r];
     }
-    // dV^T += dO^T P,  dK^T += Q^T dS   (k = query, permuted order of the accumulator rows)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8 pb = pack8f(p + 8 * s);
@@ -545,40 +537,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
         const bf16x8 qta = tr_pair(sQ, o0, o1);
         dvacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dvacc[dt], 0, 0, 0);
         dkacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qta, db, dkacc[dt], 0, 0, 0);
-      }
-    }
-    // dS^T -> LDS image [key][query] (8-B units XOR (key>>1)&7)
-    {
-      char* sDS = smem + OFF_DS;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int u = 2 * g + hh;
-        *(uint2*)(sDS + kl * 64 + ((u ^ swz_row(kl)) << 3)) = pack4(ds[4 * g], ds[4 * g + 1], ds[4 * g + 2], ds[4 * g + 3]);
-      }
-    }
-    __syncthreads();
-    // dQ tile (32 queries x 32 dh of dtile) over this wave's key half (64 keys)
-    {
-      const char* sDS = smem + OFF_DS;
-      const char* sK = smem + OFF_K;
-      f32x16 dq;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dq[r] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int key0 = khalf * 64 + ks * 16 + 8 * hh + q4;
-        const int qc = g16 + p4;
-        const int a0 = key0 * 64 + (((qc >> 2) ^ swz_row(key0)) << 3);
-        const int a1 = (key0 + 4) * 64 + (((qc >> 2) ^ swz_row(key0 + 4)) << 3);
-        const bf16x8 dsa = tr_pair(sDS, a0, a1);
-        const int kc = dtile * 32 + g16 + p4;
-        const bf16x8 kb = tr_pair(sK, off_halfswz(key0, kc), off_halfswz(key0 + 4, kc));
-        dq = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsa, kb, dq, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int gq = qb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (gq < N) unsafeAtomicAdd(dq_base + (int64_t)gq * D, dq[r]);
       }
     }
     if (more) store_q(buf ^ 1);
@@ -600,14 +558,133 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_bf16_kernel(const bf16_t* __r
   }
 }
 
-// dQ (f32, summed over key blocks) -> bf16 Q columns of dqkv, times the softmax scale
-__global__ void attn_dq_convert_kernel(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int64_t ldd,
-                                       int64_t rows, int D, float scale) {
-  const int64_t total4 = rows * D / 4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 4, r = e / D, c = e % D;
-    const float4 v = *(const float4*)(dq_acc + e);
-    *(uint2*)(dqkv + r * ldd + c) = pack4(v.x * scale, v.y * scale, v.z * scale, v.w * scale);
+// ------------------------------------------------------------------ backward: dQ
+// Query-major, the forward's structure: workgroup = 4 waves x 32 queries, K/V tiles of 64 keys in
+// double-buffered LDS.  S^T = K Q^T and dP^T = V dO^T put the QUERY on the lane, so LSE and delta
+// are per-lane constants; dS^T = P^T (dP^T - delta) is directly the B operand of
+// dQ^T += K^T dS^T (K^T via ds_read_tr16_b64).  No atomics: each query block owns its dQ rows.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                  const bf16_t* __restrict__ dout, int64_t lddo,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
+                                                                  float scale) {
+  constexpr int TILE = 64 * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Vp = Qp + 2 * D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const int qi = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const float c2 = scale * kLog2e;
+
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (qi < N) {
+      qf[s] = *(const bf16x8*)(Qp + (int64_t)qi * ldq + 16 * s + 8 * hh);
+      df[s] = *(const bf16x8*)(Dp + (int64_t)qi * lddo + 16 * s + 8 * hh);
+    } else {
+      qf[s] = bf16x8{};
+      df[s] = bf16x8{};
+    }
+  }
+  const float lse2 = qi < N ? lse[((int64_t)b * H + h) * N + qi] * kLog2e : INFINITY;
+  const float dl = qi < N ? delta[((int64_t)b * H + h) * N + qi] : 0.f;
+  f32x16 dqacc[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dqacc[0][r] = 0.f;
+    dqacc[1][r] = 0.f;
+  }
+
+  uint4 rk[2], rv[2];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
+      const int gk = kt * 64 + key;
+      if (gk < N) {
+        rk[s] = *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8);
+        rv[s] = *(const uint4*)(Vp + (int64_t)gk * ldq + c * 8);
+      } else {
+        rk[s] = make_uint4(0, 0, 0, 0);
+        rv[s] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* sK = smem + buf * 2 * TILE;
+    char* sV = sK + TILE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
+      *(uint4*)(sK + key * 128 + ((c ^ swz_row(key)) << 4)) = rk[s];
+      *(uint4*)(sV + key * 128 + ((c ^ swz_row(key)) << 4)) = rv[s];
+    }
+  };
+
+  const int nkt = (N + 63) / 64;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* sK = smem + (kt & 1) * 2 * TILE;
+    const char* sV = sK + TILE;
+    const bool more = kt + 1 < nkt;
+    if (more) load_tile(kt + 1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        dpacc[r] = 0.f;
+      }
+      const int key = kb * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int off = key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4);
+        const bf16x8 ka = *(const bf16x8*)(sK + off);
+        const bf16x8 va = *(const bf16x8*)(sV + off);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpacc, 0, 0, 0);
+      }
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pr = __builtin_amdgcn_exp2f(fmaf(sacc[r], c2, -lse2));
+        ds[r] = pr * (dpacc[r] - dl);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 db = pack8f(ds + 8 * s);
+        const int key0 = kb * 32 + 16 * s + 4 * hh + q4;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int col = dt * 32 + g16 + p4;
+          const bf16x8 ka = tr_pair(sK, off_rowswz(key0, col), off_rowswz(key0 + 8, col));
+          dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db, dqacc[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_tile((kt + 1) & 1);
+    __syncthreads();
+  }
+  if (qi < N) {
+    bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(qrow + d) = pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
+                                    dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale);
+      }
   }
 }
 
@@ -647,9 +724,9 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
 }
 
 extern "C" size_t vs_attn_bwd_workspace_bytes(int64_t B, int64_t N, int64_t H, int64_t Dh) {
-  // delta [B,H,N] f32 (padded to 256 B) + dQ accumulator [B*N, H*Dh] f32
-  const size_t delta = ((size_t)(B * H * N) * 4 + 255) / 256 * 256;
-  return delta + (size_t)(B * N * H * Dh) * 4;
+  (void)Dh;
+  // delta [B,H,N] f32, padded to 256 B
+  return ((size_t)(B * H * N) * 4 + 255) / 256 * 256;
 }
 
 extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv, int64_t ld_qkv,
@@ -662,7 +739,6 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_ATTN_BWD, s);
   float* delta = (float*)workspace;
-  float* dq_acc = (float*)((char*)workspace + ((size_t)(B * H * N) * 4 + 255) / 256 * 256);
   const int64_t rows = B * N;
   const unsigned dgrid = (unsigned)cdiv(rows * H, 4);
   if (dtype == VS_BF16) {
@@ -671,14 +747,11 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
                "vs_attn_bwd: bf16 rows must be 16-byte aligned");
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(dgrid), dim3(256), 0, s, (const bf16_t*)o, ld_o,
                        (const bf16_t*)dout, ld_do, delta, rows, (int)N, (int)H);
-    hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)rows * H * 64 * 4, s);
-    if (e != hipSuccess) return (int)e;
     dim3 grid((unsigned)cdiv(N, 128), (unsigned)H, (unsigned)B);
-    hipLaunchKernelGGL(attn_bwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout,
-                       ld_do, lse, delta, dq_acc, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
-    const int64_t t4 = rows * H * 64 / 4;
-    hipLaunchKernelGGL(attn_dq_convert_kernel, dim3((unsigned)(cdiv(t4, 256) > 4096 ? 4096 : cdiv(t4, 256))), dim3(256),
-                       0, s, dq_acc, (bf16_t*)dqkv, ld_dqkv, rows, (int)(H * 64), scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+                       (const bf16_t*)dout, ld_do, lse, delta, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+                       (const bf16_t*)dout, ld_do, lse, delta, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
   } else if (dtype == VS_F32) {
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,
                        (const float*)dout, ld_do, delta, rows, (int)N, (int)H);

@@ -62,10 +62,64 @@ __global__ void sinusoid_kernel(int64_t n_pos, int64_t dim, float* out) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// column sums (bias gradients).  Block = 256 threads = 4 row-lanes x 64 columns... each thread
-// owns one column inside a 64-column stripe and walks rows with stride; partials reduced in LDS,
-// one atomic per column per block.
+// column sums (bias gradients).  Vector kernel: block = 8 row-lanes x 32 column groups of 8
+// columns (16-B bf16 / 2x16-B f32 loads), rows strided by 8 within the block's row range, 4 rows
+// in flight per thread; partials reduced across row-lanes in LDS, one atomic per column per block.
+// Scalar kernel: fallback for unaligned / cols % 8 != 0.
 // ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void colsum8_kernel(const T* __restrict__ x, int64_t ldx, int64_t rows, int64_t cols,
+                                                      float* __restrict__ out, int64_t rows_per_block) {
+  __shared__ float part[8][257];
+  const int cgi = threadIdx.x & 31, ry = threadIdx.x >> 5;
+  const int64_t c = (blockIdx.x * 32 + cgi) * 8;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > rows) r1 = rows;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + ry;
+    for (; r + 24 < r1; r += 32) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const T* p = x + (r + 8 * u) * ldx + c;
+        if constexpr (sizeof(T) == 2) {
+          const uint4 w = *(const uint4*)p;
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[u][2 * k] = __uint_as_float(ww[k] << 16);
+            v[u][2 * k + 1] = __uint_as_float(ww[k] & 0xffff0000u);
+          }
+        } else {
+          const float4 a = *(const float4*)p, b = *(const float4*)((const float*)p + 4);
+          v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
+          v[u][4] = b.x; v[u][5] = b.y; v[u][6] = b.z; v[u][7] = b.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[u][k];
+    }
+    for (; r < r1; r += 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += Elem<T>::load(x + r * ldx + c + k);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) part[ry][cgi * 8 + k] = acc[k];
+  __syncthreads();
+  const int cc = threadIdx.x;  // one column per thread
+  const int64_t col = blockIdx.x * 256 + cc;
+  if (col < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += part[k][cc];
+    unsafeAtomicAdd(out + col, s);
+  }
+}
+
 template <typename T>
 __global__ void colsum_kernel(const T* __restrict__ x, int64_t ldx, int64_t rows, int64_t cols, float* __restrict__ out,
                               int64_t rows_per_block) {
@@ -208,17 +262,31 @@ extern "C" int vs_colsum(int32_t dtype, int64_t rows, int64_t cols, const void* 
                          void* stream) {
   VS_REQUIRE(x && out && ldx >= cols, "vs_colsum: bad args");
   if (rows == 0 || cols == 0) return VS_OK;
-  const int64_t cb = cdiv(cols, 64);
-  int64_t rb = cdiv(1024, cb);
-  if (rb > cdiv(rows, 64)) rb = cdiv(rows, 64);
-  if (rb < 1) rb = 1;
-  const int64_t rpb = cdiv(rows, rb);
-  dim3 grid((unsigned)cb, (unsigned)cdiv(rows, rpb));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VS_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, rows, cols, out, rpb);
-  else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, rows, cols, out, rpb);
+  const int vec = dtype == VS_BF16 ? 8 : 4;
+  if (cols % 8 == 0 && ldx % vec == 0 && aligned16(x)) {
+    const int64_t cb = cdiv(cols, 256);
+    int64_t rb = cdiv(512, cb);
+    if (rb > cdiv(rows, 64)) rb = cdiv(rows, 64);
+    if (rb < 1) rb = 1;
+    const int64_t rpb = cdiv(rows, rb);
+    dim3 grid((unsigned)cb, (unsigned)cdiv(rows, rpb));
+    if (dtype == VS_BF16)
+      hipLaunchKernelGGL(colsum8_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, rows, cols, out, rpb);
+    else
+      hipLaunchKernelGGL(colsum8_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, rows, cols, out, rpb);
+  } else {
+    const int64_t cb = cdiv(cols, 64);
+    int64_t rb = cdiv(1024, cb);
+    if (rb > cdiv(rows, 64)) rb = cdiv(rows, 64);
+    if (rb < 1) rb = 1;
+    const int64_t rpb = cdiv(rows, rb);
+    dim3 grid((unsigned)cb, (unsigned)cdiv(rows, rpb));
+    if (dtype == VS_BF16)
+      hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, rows, cols, out, rpb);
+    else
+      hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, rows, cols, out, rpb);
+  }
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

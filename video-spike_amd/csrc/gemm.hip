@@ -10,8 +10,13 @@
 //     M/N-contiguous operand: [64 k][rows] rows, chunk XOR f(k)                 -> ds_read_tr16_b64
 //   so the transposed products of the backward (dW = dY^T X, dX = dY W) need no transpose pass.
 // f32 operands: v_mfma_f32_16x16x4_f32 (exact f32 fma chain), tile 64x64x32, [k][rows] images.
-// Split-K (grid.z) writes through f32 atomics (VS_EPI_ATOMIC) for the skinny-output weight
-// gradients (K = B*N tokens) and the 1.2M-wide head.
+// Epilogue: the accumulator tile is staged through LDS (f32, padded rows) and written back in
+//   row order, 8 consecutive columns per thread: every bias/pos/residual/aux read and every output
+//   store is a 16-B vector access (the shapes here — M = 25,088 tokens, K = 192..768 — are
+//   HBM-bound on their outputs; the first version's 2-4 B scattered stores were 5-9x off that
+//   bound, profiles/r01_v0_kernel_stats.csv).  Split-K (VS_EPI_ATOMIC) adds whole 256-B rows.
+// Grid: 1-D, tiles remapped so that consecutive tiles of one XCD (blockIdx % 8 group) share the
+//   A row-panel / the same K slice (bijective remap, cdna_hip_programming.md §5 T1).
 #include "common.h"
 
 namespace vs {
@@ -33,7 +38,42 @@ struct EpiParams {
   int64_t ld_aux_in;
   void* aux_out;
   int64_t ld_aux_out;
+  int vec_ok;  // all leading dims / pointers allow 16-B vectors on 8-column groups
+  float* a_rowsum;  // optional: += sum_k A(m, k) (fused bias gradient of dW = dY^T X)
 };
+
+// Row sums of the A fragments a wave consumed (lane holds row (lane & 15) of 16-row fragment i):
+// reduce the 4 lane groups and add once per row.
+template <int TM>
+__device__ __forceinline__ void flush_rowsum(float* out, float (&rs)[TM], int64_t row_base, int64_t M, int lane) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float v = rs[i];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const int64_t m = row_base + i * 16 + lane;
+    if (lane < 16 && m < M) unsafeAtomicAdd(out + m, v);
+  }
+}
+
+struct GridMap {
+  int tiles_n, tiles_m, splits;
+  int64_t k_per_split;
+};
+
+__device__ __forceinline__ void map_block(const GridMap& g, int& nt, int& mt, int& split) {
+  // bijective XCD-aware remap: blocks b, b+8, b+16 ... (one XCD under round-robin dispatch) get
+  // consecutive tile indices
+  const int nwg = g.tiles_n * g.tiles_m * g.splits;
+  const int b = blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, x = b % 8;
+  const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+  const int tiles = g.tiles_n * g.tiles_m;
+  split = t / tiles;
+  const int rem = t % tiles;
+  mt = rem / g.tiles_n;
+  nt = rem % g.tiles_n;
+}
 
 __device__ __forceinline__ float ld_any(const void* p, int64_t i, int bf) {
   return bf ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
@@ -43,28 +83,147 @@ __device__ __forceinline__ void st_any(void* p, int64_t i, float v, int bf) {
   else ((float*)p)[i] = v;
 }
 
-__device__ __forceinline__ void epilogue(const EpiParams& e, int64_t m, int64_t n, float v, bool first_split) {
-  if (m >= e.M || n >= e.N) return;
-  const uint32_t f = e.flags;
-  v *= e.alpha;
-  if (f & VS_EPI_ATOMIC) {
-    if ((f & VS_EPI_BIAS) && first_split) v += e.bias[n];
-    unsafeAtomicAdd((float*)e.c + m * e.ldc + n, v);
-    return;
+__device__ __forceinline__ void ld8(const void* p, int64_t i, int bf, float (&v)[8]) {
+  if (bf) {
+    const uint4 u = *(const uint4*)((const bf16_t*)p + i);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *(const float4*)((const float*)p + i);
+    const float4 b = *(const float4*)((const float*)p + i + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   }
+}
+__device__ __forceinline__ void st8(void* p, int64_t i, int bf, const float (&v)[8]) {
+  if (bf) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *(uint4*)((bf16_t*)p + i) = u;
+  } else {
+    *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// elementwise part of the epilogue for one value (scalar path)
+__device__ __forceinline__ void epi_one(const EpiParams& e, int64_t m, int64_t n, float v) {
+  const uint32_t f = e.flags;
   if (f & VS_EPI_BIAS) v += e.bias[n];
   if (f & VS_EPI_POS) v += e.pos[(m % e.pos_rows) * e.N + n];
   if (f & VS_EPI_GELU_BWD) v *= gelu_erf_grad(ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16));
   if (f & VS_EPI_RELU_BWD) v = ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16) > 0.f ? v : 0.f;
   if (f & VS_EPI_GELU) {
     st_any(e.aux_out, m * e.ld_aux_out + n, v, e.op_bf16);
-    // GELU of the value the backward will see (rounded pre-activation in bf16 mode)
-    v = gelu_erf(e.op_bf16 ? bf2f(f2bf(v)) : v);
+    v = gelu_erf(e.op_bf16 ? bf2f(f2bf(v)) : v);  // GELU of the value the backward will see
   }
   if (f & VS_EPI_RELU) v = fmaxf(v, 0.f);
   if (f & VS_EPI_RESIDUAL) v += e.residual[m * e.ldr + n];
   if (f & VS_EPI_ACCUM) v += ((const float*)e.c)[m * e.ldc + n];
   st_any(e.c, m * e.ldc + n, v, e.out_bf16);
+}
+
+// the same for 8 consecutive columns with 16-B vector accesses
+__device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t n, float (&v)[8]) {
+  const uint32_t f = e.flags;
+  float t[8];
+  if (f & VS_EPI_BIAS) {
+    ld8(e.bias, n, 0, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+  if (f & VS_EPI_POS) {
+    ld8(e.pos, (m % e.pos_rows) * e.N + n, 0, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) {
+    ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, t);
+    if (f & VS_EPI_GELU_BWD) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= gelu_erf_grad(t[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = t[k] > 0.f ? v[k] : 0.f;
+    }
+  }
+  if (f & VS_EPI_GELU) {
+    st8(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gelu_erf(e.op_bf16 ? bf2f(f2bf(v[k])) : v[k]);
+  }
+  if (f & VS_EPI_RELU) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (f & VS_EPI_RESIDUAL) {
+    ld8(e.residual, m * e.ldr + n, 0, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+  if (f & VS_EPI_ACCUM) {
+    ld8(e.c, m * e.ldc + n, 0, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+  st8(e.c, m * e.ldc + n, e.out_bf16, v);
+}
+
+// Stage a BM x BN f32 tile (16x16-MFMA C layout in `acc`) through LDS and apply the epilogue in
+// row order.  `lds` must hold BM*(BN+4) floats; callers sync before (LDS reuse) — done here.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const f32x4 (&acc)[TM][TN], int64_t m0,
+                                           int64_t n0, bool first_split) {
+  constexpr int LDT = BN + 4;  // +4 floats: 16-B aligned rows, conflict-free scalar writes
+  constexpr int WM = BM / 2, WN = BN / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        lds[(wr * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
+  __syncthreads();
+  if (e.flags & VS_EPI_ATOMIC) {
+    // one column per lane: a wave adds 64 consecutive floats (256 B) of a row per instruction
+    for (int idx = tid; idx < BM * BN; idx += 256) {
+      const int rr = idx / BN, cc = idx % BN;
+      const int64_t m = m0 + rr, n = n0 + cc;
+      if (m < e.M && n < e.N) {
+        float v = lds[rr * LDT + cc];
+        if ((e.flags & VS_EPI_BIAS) && first_split) v += e.bias[n];
+        unsafeAtomicAdd((float*)e.c + m * e.ldc + n, v);
+      }
+    }
+    return;
+  }
+  constexpr int CPR = BN / 8;        // 8-column groups per row
+  constexpr int RPP = 256 / CPR;     // rows per pass
+  const int cg = tid % CPR;
+  for (int rr = tid / CPR; rr < BM; rr += RPP) {
+    const int64_t m = m0 + rr;
+    if (m >= e.M) break;
+    const int64_t n = n0 + cg * 8;
+    if (n >= e.N) continue;
+    const float* src = lds + rr * LDT + cg * 8;
+    if (e.vec_ok && n + 8 <= e.N) {
+      float v[8];
+      const float4 a = *(const float4*)src;
+      const float4 b = *(const float4*)(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      epi_eight(e, m, n, v);
+    } else {
+      for (int k = 0; k < 8 && n + k < e.N; ++k) epi_one(e, m, n + k, src[k]);
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -83,7 +242,6 @@ struct OperandBf16 {
   static constexpr int BYTES = R * BK * 2;
   static constexpr int CHUNKS = R * BK / 8 / 256;  // 16-B chunks per thread per tile
 
-  // global -> registers.  rows: extent of the R dimension; k_end: end of this split's K range.
   __device__ __forceinline__ static void load(uint4 (&reg)[CHUNKS], const bf16_t* __restrict__ p, int64_t ld,
                                               int64_t r0, int64_t rows, int64_t k0, int64_t k_end, int tid) {
 #pragma unroll
@@ -140,21 +298,29 @@ struct OperandBf16 {
   }
 };
 
+template <int A, int B>
+struct CMax {
+  static constexpr int v = A > B ? A : B;
+};
+
 template <int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
-                                                           int64_t k_per_split, EpiParams e) {
+                                                           GridMap g, EpiParams e) {
   using OA = OperandBf16<BM, AKC>;
   using OB = OperandBf16<BN, BKC>;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int SMEM = CMax<2 * STAGE, BM*(BN + 4) * 4>::v;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
+  int nt, mt, split;
+  map_block(g, nt, mt, split);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
-  const int64_t k_begin = (int64_t)blockIdx.z * k_per_split;
-  const int64_t k_end = k_begin + k_per_split < K ? k_begin + k_per_split : K;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
+  const int64_t k_begin = (int64_t)split * g.k_per_split;
+  const int64_t k_end = k_begin + g.k_per_split < K ? k_begin + g.k_per_split : K;
   const int nk = (int)((k_end - k_begin + 63) / 64);
 
   f32x4 acc[TM][TN];
@@ -162,6 +328,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restr
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fused bias gradient: only the first column tile's wc == 0 waves (wave-uniform condition)
+  const bool rowsum_on = e.a_rowsum != nullptr && nt == 0 && wc == 0;
+  float rs[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) rs[i] = 0.f;
 
   uint4 ra[OA::CHUNKS], rb[OB::CHUNKS];
   if (nk > 0) {
@@ -188,6 +360,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restr
       for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * WM + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = OB::frag(sb, wc * WN + j * 16, kk, lane);
+      if (rowsum_on) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rs[i] += (float)af[i][q];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -200,18 +378,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restr
     }
     __syncthreads();
   }
-
-  const bool first = blockIdx.z == 0;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int64_t n = n0 + wc * WN + j * 16 + (lane & 15);
-        epilogue(e, m, n, acc[i][j][r], first);
-      }
+  if (rowsum_on) flush_rowsum<TM>(e.a_rowsum, rs, m0 + wr * WM, e.M, lane);
+  store_tile<BM, BN, TM, TN>(e, (float*)smem, acc, m0, n0, split == 0);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -260,18 +428,21 @@ struct OperandF32 {
 template <bool AKC, bool BKC>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restrict__ A, int64_t lda,
                                                           const float* __restrict__ B, int64_t ldb, int64_t K,
-                                                          int64_t k_per_split, EpiParams e) {
+                                                          GridMap g, EpiParams e) {
   using OA = OperandF32<AKC>;
   using OB = OperandF32<BKC>;
   constexpr int LD = OA::LD;
   constexpr int STAGE = (OA::BYTES + OB::BYTES) / 4;  // floats
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  constexpr int SMEM = CMax<2 * STAGE, 64 * 68>::v;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
 
+  int nt, mt, split;
+  map_block(g, nt, mt, split);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * 64, n0 = (int64_t)blockIdx.x * 64;
-  const int64_t k_begin = (int64_t)blockIdx.z * k_per_split;
-  const int64_t k_end = k_begin + k_per_split < K ? k_begin + k_per_split : K;
+  const int64_t m0 = (int64_t)mt * 64, n0 = (int64_t)nt * 64;
+  const int64_t k_begin = (int64_t)split * g.k_per_split;
+  const int64_t k_end = k_begin + g.k_per_split < K ? k_begin + g.k_per_split : K;
   const int nk = (int)((k_end - k_begin + 31) / 32);
 
   f32x4 acc[2][2];
@@ -279,6 +450,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restric
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool rowsum_on = e.a_rowsum != nullptr && nt == 0 && wc == 0;
+  float rs[2] = {0.f, 0.f};
 
   float4 ra[2], rb[2];
   if (nk > 0) {
@@ -305,6 +479,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restric
       for (int i = 0; i < 2; ++i) af[i] = sa[k * LD + wr * 32 + i * 16 + (lane & 15)];
 #pragma unroll
       for (int j = 0; j < 2; ++j) bfr[j] = sb[k * LD + wc * 32 + j * 16 + (lane & 15)];
+      if (rowsum_on) {
+        rs[0] += af[0];
+        rs[1] += af[1];
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -317,44 +495,50 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restric
     }
     __syncthreads();
   }
-  const bool first = blockIdx.z == 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
-        const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
-        epilogue(e, m, n, acc[i][j][r], first);
-      }
+  if (rowsum_on) flush_rowsum<2>(e.a_rowsum, rs, m0 + wr * 32, e.M, lane);
+  store_tile<64, 64, 2, 2>(e, smem, acc, m0, n0, split == 0);
 }
 
 // ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
 template <int BM, int BN>
-static void launch_bf16(const vs_gemm_desc* d, dim3 grid, int64_t kps, const EpiParams& e, hipStream_t s) {
+static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
   if (d->a_kcontig && d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, true>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else if (d->a_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, false>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
 }
 
+// Split-K for the token reductions (dW): aim at ~2 blocks per CU, at least 8 k-tiles per split
+// (the f32 atomics of every split's tile cost ~1.3 TB/s chip-wide: fewer, longer splits).
 static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
   if (!atomic_ok) return 1;
   if (want > 0) return (int)(want < nk ? want : nk);
-  if (tiles >= 512 || nk < 8) return 1;
-  int64_t s = (1024 + tiles - 1) / tiles;
-  const int64_t max_s = nk / 4;
+  if (tiles >= 384 || nk < 16) return 1;
+  int64_t s = (512 + tiles - 1) / tiles;
+  const int64_t max_s = nk / 8;
   if (s > max_s) s = max_s;
   return s < 1 ? 1 : (int)s;
+}
+
+static bool vec_ok(const vs_gemm_desc* d) {
+  const uint32_t f = d->epilogue;
+  const int ovec = d->out_dtype == VS_BF16 ? 8 : 4;
+  const int avec = d->dtype == VS_BF16 ? 8 : 4;
+  bool ok = d->ldc % ovec == 0 && aligned16(d->c);
+  if (f & VS_EPI_BIAS) ok = ok && aligned16(d->bias);
+  if (f & VS_EPI_POS) ok = ok && aligned16(d->pos) && d->N % 4 == 0;
+  if (f & VS_EPI_RESIDUAL) ok = ok && aligned16(d->residual) && d->ld_residual % 4 == 0;
+  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) ok = ok && aligned16(d->aux_in) && d->ld_aux_in % avec == 0;
+  if (f & VS_EPI_GELU) ok = ok && aligned16(d->aux_out) && d->ld_aux_out % avec == 0;
+  return ok;
 }
 
 }  // namespace vs
@@ -395,42 +579,48 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   e.pos = d->pos; e.pos_rows = d->pos_rows;
   e.aux_in = d->aux_in; e.ld_aux_in = d->ld_aux_in;
   e.aux_out = d->aux_out; e.ld_aux_out = d->ld_aux_out;
+  e.vec_ok = vec_ok(d);
+  e.a_rowsum = d->a_rowsum;
 
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_GEMM, s);
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
+  GridMap g;
   if (d->dtype == VS_BF16) {
     const int BM = d->M <= 64 ? 64 : 128;
     const int BN = (d->N <= 64 || (d->N % 128 != 0 && d->N % 64 == 0 && d->N < 1024)) ? 64 : 128;
-    const int64_t tiles = cdiv(d->N, BN) * cdiv(d->M, BM);
+    g.tiles_n = (int)cdiv(d->N, BN);
+    g.tiles_m = (int)cdiv(d->M, BM);
     const int64_t nk = cdiv(d->K, 64);
-    const int splits = pick_splits(tiles, nk, d->split_k, atomic_ok);
-    const int64_t kps = cdiv(nk, splits) * 64;
-    const int nz = (int)cdiv(d->K, kps > 0 ? kps : 64);
-    dim3 grid((unsigned)cdiv(d->N, BN), (unsigned)cdiv(d->M, BM), (unsigned)(nz > 0 ? nz : 1));
-    VS_REQUIRE(grid.y <= 65535, "vs_gemm: M too large");
-    if (BM == 128 && BN == 128) launch_bf16<128, 128>(d, grid, kps, e, s);
-    else if (BM == 128) launch_bf16<128, 64>(d, grid, kps, e, s);
-    else if (BN == 128) launch_bf16<64, 128>(d, grid, kps, e, s);
-    else launch_bf16<64, 64>(d, grid, kps, e, s);
+    const int splits = pick_splits((int64_t)g.tiles_n * g.tiles_m, nk, d->split_k, atomic_ok);
+    g.k_per_split = cdiv(nk, splits) * 64;
+    g.splits = (int)(d->K > 0 ? cdiv(d->K, g.k_per_split) : 1);
+    const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
+    VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
+    if (BM == 128 && BN == 128) launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
+    else if (BM == 128) launch_bf16<128, 64>(d, (unsigned)nblk, g, e, s);
+    else if (BN == 128) launch_bf16<64, 128>(d, (unsigned)nblk, g, e, s);
+    else launch_bf16<64, 64>(d, (unsigned)nblk, g, e, s);
   } else {
-    const int64_t tiles = cdiv(d->N, 64) * cdiv(d->M, 64);
+    g.tiles_n = (int)cdiv(d->N, 64);
+    g.tiles_m = (int)cdiv(d->M, 64);
     const int64_t nk = cdiv(d->K, 32);
-    const int splits = pick_splits(tiles, nk, d->split_k, atomic_ok);
-    const int64_t kps = cdiv(nk, splits) * 32;
-    const int nz = (int)cdiv(d->K, kps > 0 ? kps : 32);
-    dim3 grid((unsigned)cdiv(d->N, 64), (unsigned)cdiv(d->M, 64), (unsigned)(nz > 0 ? nz : 1));
-    VS_REQUIRE(grid.y <= 65535, "vs_gemm: M too large");
+    const int splits = pick_splits((int64_t)g.tiles_n * g.tiles_m, nk, d->split_k, atomic_ok);
+    g.k_per_split = cdiv(nk, splits) * 32;
+    g.splits = (int)(d->K > 0 ? cdiv(d->K, g.k_per_split) : 1);
+    const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
+    VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
     const float* a = (const float*)d->a;
     const float* b = (const float*)d->b;
+    dim3 grid((unsigned)nblk);
     if (d->a_kcontig && d->b_kcontig)
-      hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+      hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
     else if (d->a_kcontig)
-      hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+      hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
     else if (d->b_kcontig)
-      hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+      hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
     else
-      hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, kps, e);
+      hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   }
   VS_LAUNCH_CHECK();
   return VS_OK;

@@ -90,22 +90,22 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   const void* gy = lp ? G->dy_lp : (const void*)G->dy;
 
   // ---- MLP: x' = y + a W2^T + b2
-  {  // dW2[D,F] += dx'^T a
+  {  // dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
+    g.a_rowsum = G->b_fc2;
     VS_CALL(vs_gemm(&g, stream));
   }
-  VS_CALL(vs_colsum(VS_F32, M, D, G->dx_out, D, G->b_fc2, stream));
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
     vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
     g.aux_in = L->a_pre;
     g.ld_aux_in = F;
     VS_CALL(vs_gemm(&g, stream));
   }
-  {  // dW1[F,D] += da^T h2
+  {  // dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
+    g.a_rowsum = G->b_fc1;
     VS_CALL(vs_gemm(&g, stream));
   }
-  VS_CALL(vs_colsum(T, M, F, G->d_a, F, G->b_fc1, stream));
   {  // dh2 = da W1
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
     VS_CALL(vs_gemm(&g, stream));
@@ -114,24 +114,25 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
                            lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, stream));
   // ---- attention: y = x + o Wp^T + bp
-  {  // dWp[D,D] += dy^T o
+  {  // dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
+    g.a_rowsum = G->b_proj;
     VS_CALL(vs_gemm(&g, stream));
   }
-  VS_CALL(vs_colsum(VS_F32, M, D, G->dy, D, G->b_proj, stream));
   {  // do = dy Wp
     vs_gemm_desc g = gdesc(T, T, true, false, M, D, D, gy, D, L->w_proj, D, G->d_o, D, 0);
     VS_CALL(vs_gemm(&g, stream));
   }
   VS_CALL(vs_attn_bwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, G->d_o, D, L->lse, G->d_qkv,
                       3 * D, G->attn_ws, L->attn_scale, stream));
-  {  // dWqkv[3D,D] += dqkv^T h1
+  {  // dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
+    g.a_rowsum = G->b_qkv;
     VS_CALL(vs_gemm(&g, stream));
+    // the k bias is not a parameter (fixed 0 in the reference, mv:233): its slot stays exactly 0
+    hipError_t e = hipMemsetAsync(G->b_qkv + D, 0, D * sizeof(float), (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
   }
-  // q and v biases only: the k bias is not a parameter (fixed 0 in the reference, mv:233)
-  VS_CALL(vs_colsum(T, M, D, G->d_qkv, 3 * D, G->b_qkv, stream));
-  VS_CALL(vs_colsum(T, M, D, (const char*)G->d_qkv + 2 * D * esize(T), 3 * D, G->b_qkv + 2 * D, stream));
   {  // dh1 = dqkv Wqkv
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
     VS_CALL(vs_gemm(&g, stream));

@@ -33,7 +33,7 @@ class GemmDesc(ctypes.Structure):
                 ("epilogue", c_u32), ("alpha", c_f32), ("bias", c_p),
                 ("residual", c_p), ("ld_residual", c_i64), ("pos", c_p), ("pos_rows", c_i64),
                 ("aux_in", c_p), ("ld_aux_in", c_i64), ("aux_out", c_p), ("ld_aux_out", c_i64),
-                ("split_k", c_i32), ("reserved", c_i32)]
+                ("split_k", c_i32), ("reserved", c_i32), ("a_rowsum", c_p)]
 
 
 class VitLayer(ctypes.Structure):

@@ -118,8 +118,7 @@ class _MLPFn(torch.autograd.Function):
             inp = x if i == 0 else outs[i - 1]
             dw = torch.zeros_like(ws[i])
             db = torch.zeros(ws[i].shape[0], dtype=torch.float32, device=dy.device)
-            ops.linear_dw(dy, inp, dw)
-            ops.colsum(dy, db)
+            ops.linear_dw(dy, inp, dw, db=db)
             grads[2 * i], grads[2 * i + 1] = dw, db
             if i > 0 or ctx.need_x:
                 dx = torch.empty(dy.shape[0], ws[i].shape[1], dtype=torch.float32, device=dy.device)

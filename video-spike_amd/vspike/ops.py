@@ -16,7 +16,7 @@ from ._lib import check, lib, ptr, require_device, stream
 
 def gemm(a, b, c, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, ldc, epilogue=0, alpha=1.0, bias=None,
          residual=None, ld_residual=0, pos=None, pos_rows=0, aux_in=None, ld_aux_in=0, aux_out=None,
-         ld_aux_out=0, split_k=0):
+         ld_aux_out=0, split_k=0, a_rowsum=None):
     """C[M,N] = epilogue(alpha * A @ B); layouts as in include/vspike.h (vs_gemm)."""
     require_device(a, b, c)
     d = L.GemmDesc()
@@ -34,6 +34,7 @@ def gemm(a, b, c, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, ldc, epilogue=0, a
     d.aux_in, d.ld_aux_in = ptr(aux_in), ld_aux_in
     d.aux_out, d.ld_aux_out = ptr(aux_out), ld_aux_out
     d.split_k = split_k
+    d.a_rowsum = ptr(a_rowsum)
     check(lib().vs_gemm(ctypes.byref(d), stream()), "vs_gemm")
     return c
 
@@ -48,21 +49,25 @@ def linear(x, w, out, *, bias=None, epilogue=0, **kw):
                 ldc=out.stride(0), epilogue=epilogue, bias=bias, **kw)
 
 
-def linear_dx(dy, w, out, *, epilogue=0, **kw):
-    """out[M,K] = dy[M,N] @ w[N,K]."""
+def linear_dx(dy, w, out, *, epilogue=0, accumulate=False, **kw):
+    """out[M,K] = dy[M,N] @ w[N,K]; accumulate=True adds into an f32 `out` with split-K atomics
+    (for skinny products whose reduction N is long, e.g. the head's dZ over 100*neurons)."""
     M, N = dy.shape
     K = w.shape[1]
+    if accumulate:
+        epilogue |= L.EPI_ATOMIC
     return gemm(dy, w, out, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=dy.stride(0), ldb=w.stride(0),
                 ldc=out.stride(0), epilogue=epilogue, **kw)
 
 
-def linear_dw(dy, x, dw, *, accumulate=True):
-    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw; split-K atomics over the M reduction)."""
+def linear_dw(dy, x, dw, *, accumulate=True, db=None):
+    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw; split-K atomics over the M reduction).
+    db (optional, f32 [N]) += column sums of dy, fused into the same pass."""
     M, N = dy.shape
     K = x.shape[1]
     epi = L.EPI_ATOMIC if accumulate else 0
     return gemm(dy, x, dw, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=dy.stride(0), ldb=x.stride(0),
-                ldc=dw.stride(0), epilogue=epi, split_k=0 if accumulate else 1)
+                ldc=dw.stride(0), epilogue=epi, split_k=0 if accumulate else 1, a_rowsum=db)
 
 
 def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd):

@@ -268,17 +268,16 @@ class VideoMAE(nn.Module):
         g_head = self._grad_buffer(self.head_flat) if want_head else None
         Gh = lambda n: lh.view(g_head, n)  # noqa: E731
         z = act["z"]
-        dz = torch.empty(B, lay.enc_out, dtype=torch.float32, device=dev)
-        ops.linear_dx(dr, lh.view(head32, "dec_w"), dz)
+        dz = torch.zeros(B, lay.enc_out, dtype=torch.float32, device=dev)
+        ops.linear_dx(dr, lh.view(head32, "dec_w"), dz, accumulate=True)     # K = 100*neurons: split-K
         if dt != torch.float32:
             dz_lp = torch.empty(B, lay.enc_out, dtype=dt, device=dev)
             ops.cast(dz, dz_lp)
         else:
             dz_lp = dz
         if want_head:
-            ops.linear_dw(dr, z, Gh("dec_w"))
-            ops.colsum(dr, Gh("dec_b"))
-            ops.colsum(dz, Gh("enc_b"))
+            ops.linear_dw(dr, z, Gh("dec_w"), db=Gh("dec_b"))
+            ops.colsum(dz, Gh("enc_b"))                      # dz is B x 64: the lp copy may be rounded
             ops.linear_dw(dz_lp, st["x_flat_lp"], Gh("enc_w"))
             self._ready(self.head_flat, 0, self.head_flat.numel())
         if not want_enc:
@@ -319,8 +318,11 @@ class VideoMAE(nn.Module):
             lo, hi = lay.layer_ranges[i]
             self._ready(self.enc_flat, lo, hi)
         # patch embedding: dW = dx0^T cols, db = colsum(dx0); the position table is fixed
-        ops.linear_dw(dx_lp if lp else dx, act["cols"], Ge("patch_w"))
-        ops.colsum(dx, Ge("patch_b"))
+        if lp:
+            ops.linear_dw(dx_lp, act["cols"], Ge("patch_w"))
+            ops.colsum(dx, Ge("patch_b"))                    # from the f32 gradient, not its bf16 copy
+        else:
+            ops.linear_dw(dx, act["cols"], Ge("patch_w"), db=Ge("patch_b"))
         self._ready(self.enc_flat, 0, lay.layer_ranges[0][0] if lay.layer_ranges else self.enc_flat.numel())
         return g_enc, g_head
 
