@@ -1,0 +1,115 @@
+"""Per-op timing of the ViT training-step shapes (C2: ViT-Tiny, B=16) with hipEvents.
+
+Prints, per op: average microseconds over `--reps` launches, algorithmic HBM bytes and FLOPs,
+achieved GB/s and TFLOP/s, and the fraction of the op's bound (HBM 6.3 TB/s measured-achievable
+or 2.5 PF bf16 MFMA).  Usage:  python scripts/microbench.py [--only gemm|attn|ln] [--reps 50]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "video-spike_amd"))
+
+import torch  # noqa: E402
+
+from vspike import _lib as L, ops  # noqa: E402
+
+HBM = 6.3e12
+MFMA = 2.5e15
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def report(name, us, nbytes, flops):
+    gbs = nbytes / (us * 1e-6) / 1e9
+    tfs = flops / (us * 1e-6) / 1e12
+    bound = max(nbytes / HBM, flops / MFMA) * 1e6
+    print(f"{name:34s} {us:9.1f} us  {gbs:8.0f} GB/s  {tfs:7.1f} TF/s  bound {bound:7.1f} us  ({bound / us * 100:5.1f}% of roof)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=16)
+    a = ap.parse_args()
+    dev = "cuda"
+    B, N, D, F, H = a.batch, 1568, 192, 768, 3
+    M = B * N
+    bf = torch.bfloat16
+    r = lambda *s, dt=bf: (torch.randn(*s, device=dev) * 0.5).to(dt)  # noqa: E731
+    if a.only in ("", "gemm"):
+        x, w3, wd, w1, w2 = r(M, D), r(3 * D, D), r(D, D), r(F, D), r(D, F)
+        b3, bd, b1 = r(3 * D, dt=torch.float32), r(D, dt=torch.float32), r(F, dt=torch.float32)
+        qkv, o, a_, pre = r(M, 3 * D), r(M, D), r(M, F), r(M, F)
+        y32, res32 = torch.empty(M, D, device=dev), r(M, D, dt=torch.float32)
+        g_lp, ga = r(M, D), r(M, F)
+        dW = {k: torch.zeros(*s, device=dev) for k, s in (("qkv", (3 * D, D)), ("p", (D, D)), ("1", (F, D)), ("2", (D, F)))}
+        db = {k: torch.zeros(s, device=dev) for k, s in (("qkv", 3 * D), ("p", D), ("1", F), ("2", D))}
+        e2 = 2
+        report("fwd qkv [M,192]x[192,576]", timeit(lambda: ops.linear(x, w3, qkv, bias=b3), a.reps),
+               M * D * e2 + M * 3 * D * e2, 2 * M * D * 3 * D)
+        report("fwd proj +res (f32 out)", timeit(lambda: ops.linear(o, wd, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
+                                                                   residual=res32, ld_residual=D), a.reps),
+               M * D * e2 + 2 * M * D * 4, 2 * M * D * D)
+        report("fwd fc1 +GELU (act+pre)", timeit(lambda: ops.linear(x, w1, a_, bias=b1, epilogue=L.EPI_GELU, aux_out=pre,
+                                                                    ld_aux_out=F), a.reps),
+               M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
+        report("fwd fc2 +res (K=768)", timeit(lambda: ops.linear(a_, w2, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
+                                                                 residual=res32, ld_residual=D), a.reps),
+               M * F * e2 + 2 * M * D * 4, 2 * M * D * F)
+        report("bwd da = dx W2 * gelu'", timeit(lambda: ops.linear_dx(g_lp, w2, ga, epilogue=L.EPI_GELU_BWD, aux_in=pre,
+                                                                      ld_aux_in=F), a.reps),
+               M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
+        report("bwd dh2 = da W1 (f32)", timeit(lambda: ops.linear_dx(ga, w1, y32), a.reps),
+               M * F * e2 + M * D * 4, 2 * M * D * F)
+        report("bwd do = dy Wp", timeit(lambda: ops.linear_dx(g_lp, wd, o), a.reps), 2 * M * D * e2, 2 * M * D * D)
+        report("bwd dh1 = dqkv Wqkv (f32)", timeit(lambda: ops.linear_dx(qkv, w3, y32), a.reps),
+               M * 3 * D * e2 + M * D * 4, 2 * M * D * 3 * D)
+        report("dW2 [192,768] (+db)", timeit(lambda: ops.linear_dw(g_lp, a_, dW["2"], db=db["2"]), a.reps),
+               M * (D + F) * e2, 2 * M * D * F)
+        report("dW1 [768,192] (+db)", timeit(lambda: ops.linear_dw(ga, x, dW["1"], db=db["1"]), a.reps),
+               M * (D + F) * e2, 2 * M * D * F)
+        report("dWp [192,192] (+db)", timeit(lambda: ops.linear_dw(g_lp, o, dW["p"], db=db["p"]), a.reps),
+               M * 2 * D * e2, 2 * M * D * D)
+        report("dWqkv [576,192] (+db)", timeit(lambda: ops.linear_dw(qkv, x, dW["qkv"], db=db["qkv"]), a.reps),
+               M * 4 * D * e2, 2 * M * D * 3 * D)
+    if a.only in ("", "attn"):
+        qkv = r(M, 3 * D, dt=bf) * 3
+        o = torch.empty(M, D, dtype=bf, device=dev)
+        lse = torch.empty(B, H, N, device=dev)
+        do = r(M, D)
+        dq = torch.empty(M, 3 * D, dtype=bf, device=dev)
+        ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=dev)
+        f = 4.0 * B * H * N * N * 64
+        report("attn fwd", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps), M * 4 * D * 2, f)
+        report("attn bwd (delta+dkdv+dq)", timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps),
+               M * 8 * D * 2, 2.5 * f)
+    if a.only in ("", "ln"):
+        x = r(M, D, dt=torch.float32)
+        g, b = r(D, dt=torch.float32) + 1, r(D, dt=torch.float32)
+        y = torch.empty(M, D, dtype=bf, device=dev)
+        mu, rs = torch.empty(M, device=dev), torch.empty(M, device=dev)
+        dx, dxl = torch.empty(M, D, device=dev), torch.empty(M, D, dtype=bf, device=dev)
+        dg, dbb = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        report("ln fwd (f32 in, bf16 out)", timeit(lambda: ops.layernorm_fwd(x, g, b, 1e-12, y, mu, rs), a.reps),
+               M * D * 6, 0)
+        ops.layernorm_fwd(x, g, b, 1e-12, y, mu, rs)
+        report("ln bwd (+dres, + bf16 copy)", timeit(lambda: ops.layernorm_bwd(x, x, mu, rs, g, dx, dg, dbb, dres=x,
+                                                                               dx_lp=dxl), a.reps), M * D * 18, 0)
+
+
+if __name__ == "__main__":
+    main()
