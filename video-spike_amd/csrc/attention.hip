@@ -16,6 +16,8 @@
 //   LDS, expf/logf in f32.  Used for the 1e-4-relative parity mode.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace vs {
@@ -250,17 +252,15 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* lds, int off0, int off1) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+// 8 f32 -> 8 bf16 as four v_cvt_pk_bf16_f32 (element-wise casts cost one cvt per value)
 __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[base + j];
-  return r;
+  const f32x8 v = {a[base], a[base + 1], a[base + 2], a[base + 3], a[base + 4], a[base + 5], a[base + 6], a[base + 7]};
+  return __builtin_convertvector(v, bf16x8);
 }
 __device__ __forceinline__ bf16x8 pack8f(const float* a) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[j];
-  return r;
+  const f32x8 v = {a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]};
+  return __builtin_convertvector(v, bf16x8);
 }
 
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
@@ -271,145 +271,294 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+// Per 64-key tile and wave (32 queries): 8 MFMAs for S^T = K (c Q)^T and 8 for O^T += V^T P^T.
+// VALU per score is minimised:
+//   * Q is pre-scaled by c = log2(e)/sqrt(64) when loaded, and the running max enters the QK^T
+//     chain as the MFMA's C operand (a splat of -m that is only rewritten when m moves), so the
+//     accumulator IS log2(p): p = v_exp_f32(acc) with no per-score FMA;
+//   * the max is lazily raised (only when a lane's scores exceed m by 2^kRescaleThr, guide T13);
+//     the O/l rescale is a wave-uniform branch that is skipped in steady state, P <= 2^kRescaleThr;
+//   * max via v_max3 (asm: hipcc canonicalises fmaxf operands), xor-32 exchange via
+//     v_permlane32_swap (no LDS), staging loads unconditional (clamped row + select);
+//   * the tile loop is unrolled over the two LDS buffers so every LDS address is a per-lane base
+//     plus an immediate offset.
+// Softmax VALU of sub-block j overlaps the MFMAs of sub-block j+1 (issue order QK1, SM0, PV0,
+// SM1, PV1).
+constexpr float kRescaleThr = 8.0f;
+
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float max16(const f32x16& x) {
+  const float a = max3f(x[0], x[1], x[2]), b = max3f(x[3], x[4], x[5]), c = max3f(x[6], x[7], x[8]);
+  const float d = max3f(x[9], x[10], x[11]), e = max3f(x[12], x[13], x[14]);
+  return max3f(max3f(a, b, c), max3f(d, e, x[15]), -INFINITY);
+}
+// v_permlane32_swap(v, v) returns {v[lane & 31], v[32 + (lane & 31)]}: both halves' values in
+// every lane, so a pair reduction over lanes l and l^32 needs no LDS round trip.
+__device__ __forceinline__ float pair_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return max3f(__uint_as_float(r[0]), __uint_as_float(r[1]), -INFINITY);
+}
+__device__ __forceinline__ float pair_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int I>
+using IC = std::integral_constant<int, I>;
+
+#ifdef VS_STAMP
+// Diagnostic build only (-DVS_STAMP): per wave {start, end} realtime ticks (100 MHz), HW ids, and
+// shader-clock cycles accumulated in the forward's barrier and vmcnt waits; read back with
+// vs_dbg_stamps().  Not part of the product library.
+__device__ unsigned long long g_stamp[8 * 8192];
+__device__ __forceinline__ void stamp(int slot, bool end) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w < 8192) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (!end) {
+      g_stamp[8 * w] = t;
+      g_stamp[8 * w + 2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      g_stamp[8 * w + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    } else {
+      g_stamp[8 * w + 1] = t;
+    }
+  }
+  (void)slot;
+}
+__device__ __forceinline__ void stamp_acc(int slot, unsigned long long v) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && w < 8192) g_stamp[8 * w + slot] = v;
+}
+#define VS_CLK() __builtin_amdgcn_s_memtime()
+#define VS_STAMP_AT(end) stamp(0, end)
+#else
+#define VS_STAMP_AT(end)
+#define VS_CLK() 0ull
+#endif
+
+__global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                bf16_t* __restrict__ o, int64_t ldo,
                                                                float* __restrict__ lse, int N, int H,
                                                                float scale_log2) {
   constexpr int TILE = 64 * 128;  // bytes of one 64-key x 64-dh bf16 tile
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  VS_STAMP_AT(false);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
   const bf16_t* Kp = Qp + D;
-  const bf16_t* Vp = Qp + 2 * D;
-  const int qi = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int q0w = qb * 128 + wid * 32;  // this wave's first query
+  const int qi = q0w + (lane & 31);
+  const float c = scale_log2;
 
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    if (qi < N) qf[s] = *(const bf16x8*)(Qp + (int64_t)qi * ldq + 16 * s + 8 * hh);
-    else qf[s] = bf16x8{};
-  }
-  f32x16 oacc[2];
+    const int qr = qi < N ? qi : N - 1;
+    const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+    f32x8 v;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) oacc[0][r] = oacc[1][r] = 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c;
+    qf[s] = __builtin_convertvector(v, bf16x8);
+  }
+  f32x16 oacc[2], cinit;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    oacc[0][r] = 0.f;
+    oacc[1][r] = 0.f;
+    cinit[r] = 0.f;
+  }
   float m_run = -INFINITY, l_half = 0.f;
 
-  uint4 rk[2], rv[2];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
-      const int gk = kt * 64 + key;
-      if (gk < N) {
-        rk[s] = *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8);
-        rv[s] = *(const uint4*)(Vp + (int64_t)gk * ldq + c * 8);
-      } else {
-        rk[s] = make_uint4(0, 0, 0, 0);  // (a chained vector assignment here crashes ROCm 7.2 MCP)
-        rv[s] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* sK = smem + buf * 2 * TILE;
-    char* sV = sK + TILE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
-      *(uint4*)(sK + key * 128 + ((c ^ swz_row(key)) << 4)) = rk[s];
-      *(uint4*)(sV + key * 128 + ((c ^ swz_half(key)) << 4)) = rv[s];
-    }
-  };
-
-  const int nkt = (N + 63) / 64;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+  // Per-lane LDS byte offsets, tile-invariant.  Every read is a lane base plus an immediate:
+  //  K rows key = kb*32 + (lane&31): swz_row(key + 32) == swz_row(key), so kb adds 32*128 B;
+  //  the 4 k-chunks XOR (2s+hh) into the swizzled chunk index -> one base per s.
+  //  V^T reads rows k0 = kb*32 + 16s + 4hh + q4 (+8): swz_half(k0) depends on q4 bit 1 only, so
+  //  kb/s/+8 are immediates and dt (64-B half) just selects one of two bases.
   const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const char* sK = smem + (kt & 1) * 2 * TILE;
-    const char* sV = sK + TILE;
-    const bool more = kt + 1 < nkt;
-    if (more) load_tile(kt + 1);
-
-    f32x16 sacc[2];
+  int kbase[4];
+  {
+    const int key = lane & 31;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int s = 0; s < 4; ++s) kbase[s] = key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4);
+  }
+  int vbase[2];
+  {
+    const int k0 = 4 * hh + q4;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
-      const int key = kb * 32 + (lane & 31);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *(const bf16x8*)(sK + key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4));
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
-      }
+    for (int dt = 0; dt < 2; ++dt) vbase[dt] = TILE + off_halfswz(k0, dt * 32 + g16 + p4);
+  }
+  // K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4): one wave-instruction fills a 1-KiB
+  // piece = 8 rows x 128 B, lane L writing position L*16.  The LDS images keep their XOR swizzles
+  // because each lane loads the SOURCE chunk that belongs at its position: (L&7) ^ swz(row).  Wave
+  // w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1.  No staging registers, no ds_write.
+  const int prow0 = wid * 16 + (lane >> 3), ppos = lane & 7;  // rows prow0 and prow0 + 8
+  const uint32_t gk0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_row(prow0)) << 4));
+  const uint32_t gk1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_row(prow0 + 8)) << 4));
+  const uint32_t gv0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_half(prow0)) << 4));
+  const uint32_t gv1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_half(prow0 + 8)) << 4));
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  auto glds = [](const char* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 16, 0,
+                                     0);
+  };
+  auto load_tile = [&](int kt, char* buf) {
+    const char* kb = (const char*)Kp + kt * tile_bytes;
+    const char* vb = kb + vdelta;
+    char* dk = buf + wid * 2048;
+    char* dv = buf + TILE + wid * 2048;
+    if ((kt + 1) * 64 <= N) {
+      glds(kb + gk0, dk);
+      glds(kb + gk1, dk + 1024);
+      glds(vb + gv0, dv);
+      glds(vb + gv1, dv + 1024);
+    } else {  // partial last tile: rows past N re-read row N-1 (finite data; its scores are masked)
+      const int r0 = kt * 64 + prow0, r1 = r0 + 8;
+      const int c0 = (r0 < N ? r0 : N - 1) - kt * 64, c1 = (r1 < N ? r1 : N - 1) - kt * 64;
+      glds(kb + (int64_t)c0 * 2 * ldq + ((ppos ^ swz_row(prow0)) << 4), dk);
+      glds(kb + (int64_t)c1 * 2 * ldq + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
+      glds(vb + (int64_t)c0 * 2 * ldq + ((ppos ^ swz_half(prow0)) << 4), dv);
+      glds(vb + (int64_t)c1 * 2 * ldq + ((ppos ^ swz_half(prow0 + 8)) << 4), dv + 1024);
     }
-    if ((kt + 1) * 64 > N) {
+  };
+  auto qk = [&](const char* base, int kb) {
+    f32x16 acc = cinit;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(base + kb * 4096 + kbase[s]), qf[s], acc, 0, 0,
+                                                    0);
+    return acc;
+  };
+  // acc = log2-domain scores relative to the reference max the QK chain was seeded with (cinit =
+  // -m_run, or 0 before the first tile).  Raises the reference when some lane's scores exceed it
+  // by more than 2^kRescaleThr (always on the first call): shifts acc by d, rescales O and l, and
+  // reports d so that an S accumulator already computed with the old reference can be shifted too.
+  auto softmax = [&](f32x16& acc, int key0, bf16x8& pa, bf16x8& pb, float& d_out) {
+    if (key0 + 32 > N) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * 64 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          if (key >= N) sacc[kb][r] = -INFINITY;
-        }
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
     }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[kb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx * scale_log2);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    l_half *= alpha;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      oacc[0][r] *= alpha;
-      oacc[1][r] *= alpha;
-    }
-    float psum = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    // fast path: this lane's 16 scores only (the xor-32 partner holds the query's other keys);
+    // the pair maximum is formed only on the rare wave-uniform rescale path
+    const float mx = max16(acc);
+    const bool first = m_run == -INFINITY;
+    d_out = 0.f;
+    if (__any(first || mx > kRescaleThr)) {
+      const float mxp = pair_max(mx);
+      const bool grow = first || mxp > kRescaleThr;  // identical in both lanes of a query
+      const float d = grow ? mxp : 0.f;
+      const float alpha = (grow && !first) ? __builtin_amdgcn_exp2f(-d) : 1.f;
+      m_run = grow ? (first ? d : m_run + d) : m_run;
+      l_half *= alpha;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(fmaf(sacc[kb][r], scale_log2, -m_new));
-        sacc[kb][r] = p;
-        psum += p;
+        acc[r] -= d;
+        oacc[0][r] *= alpha;
+        oacc[1][r] *= alpha;
+        cinit[r] -= d;  // in place: the QK seed stays -m_run in one register set
       }
-    l_half += psum;
+      d_out = d;
+    }
+    float p[16];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r]);
+    l_half += ((((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) +
+               (((p[8] + p[9]) + (p[10] + p[11])) + ((p[12] + p[13]) + (p[14] + p[15]))));
+    pa = pack8f(p);
+    pb = pack8f(p + 8);
+  };
+  auto pv = [&](const char* base, int kb, const bf16x8& pa, const bf16x8& pb) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pb = pack8(sacc[kb], 8 * s);
-        const int key0 = kb * 32 + 16 * s + 4 * hh + q4;
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int col = dt * 32 + g16 + p4;
-          const bf16x8 va = tr_pair(sV, off_halfswz(key0, col), off_halfswz(key0 + 8, col));
-          oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, oacc[dt], 0, 0, 0);
-        }
+      for (int dt = 0; dt < 2; ++dt) {
+        const char* vb = base + kb * 4096 + s * 2048;
+        const bf16x8 va = tr_pair(vb, vbase[dt], vbase[dt] + 1024);
+        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, s == 0 ? pa : pb, oacc[dt], 0, 0, 0);
       }
-    if (more) store_tile((kt + 1) & 1);
+  };
+
+  // One barrier per 64-key tile, at its top: it publishes tile kt (DMA issued at the top of kt-1)
+  // and retires every wave's reads of the buffer that the DMA for tile kt+1, issued right after it,
+  // overwrites.  The two 32-key halves run serially (QK, softmax, PV): issuing both QK^T halves
+  // first costs 16 more VGPRs and drops the kernel below 3 waves/SIMD; the 2-3 co-resident waves
+  // per SIMD supply the MFMA/VALU overlap instead.
+  const int nkt = (N + 63) / 64;
+  load_tile(0, smem);
+  unsigned long long t_vm = 0, t_bar = 0;
+  const unsigned long long t_begin = VS_CLK();
+  auto iter = [&](int kt, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const char* cur = smem + BUF * 2 * TILE;
+    char* nxt = smem + (BUF ^ 1) * 2 * TILE;
+#ifdef VS_STAMP
+    const unsigned long long c0 = VS_CLK();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long c1 = VS_CLK();
     __syncthreads();
+    t_vm += c1 - c0;
+    t_bar += VS_CLK() - c1;
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt landed
+    __syncthreads();                                  // ... and every other wave's
+#endif
+    const bool more = kt + 1 < nkt;
+    if (more) load_tile(kt + 1, nxt);
+    f32x16 sa = qk(cur, 0);
+    bf16x8 a0, a1, b0, b1;
+    float d0, d1;
+    softmax(sa, kt * 64, a0, a1, d0);
+    pv(cur, 0, a0, a1);
+    f32x16 sb = qk(cur, 1);
+    softmax(sb, kt * 64 + 32, b0, b1, d1);
+    pv(cur, 1, b0, b1);
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    iter(kt, IC<0>{});
+    if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
   }
 
-  const float l = l_half + __shfl_xor(l_half, 32, 64);
-  if (qi < N) {
-    const float inv = 1.f / l;
-    bf16_t* orow = o + (row0 + qi) * ldo + h * 64;
+  // Epilogue: O^T accumulators -> normalised bf16 rows staged through LDS (wave-private 4 KB,
+  // XOR-swizzled 16-B chunks), then written as whole 128-B rows (8 lanes per row).
+  const float l = pair_sum(l_half);
+  const float inv = 1.f / l;
+  __syncthreads();  // every wave is done with the last K/V tile
+  char* so = smem + wid * 4096;
+  const int oq = lane & 31;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+  for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
-        *(uint2*)(orow + d) = pack4(oacc[dt][4 * g] * inv, oacc[dt][4 * g + 1] * inv, oacc[dt][4 * g + 2] * inv,
-                                    oacc[dt][4 * g + 3] * inv);
-      }
-    if (hh == 0) lse[((int64_t)b * H + h) * N + qi] = (m_run + log2f(l)) * kLn2;
+    for (int g = 0; g < 4; ++g) {
+      const int chunk = dt * 4 + g;  // 8 dims per 16-B chunk; this lane holds its 4hh half
+      *(uint2*)(so + oq * 128 + ((chunk ^ (oq & 7)) << 4) + 8 * hh) =
+          pack4(oacc[dt][4 * g] * inv, oacc[dt][4 * g + 1] * inv, oacc[dt][4 * g + 2] * inv,
+                oacc[dt][4 * g + 3] * inv);
+    }
+  if (hh == 0 && qi < N) lse[((int64_t)b * H + h) * N + qi] = (m_run + __log2f(l)) * kLn2;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed (wave-private)
+#pragma unroll
+  for (int pss = 0; pss < 4; ++pss) {
+    const int r = pss * 8 + (lane >> 3), ch = lane & 7;
+    const uint4 v = *(const uint4*)(so + r * 128 + ((ch ^ (r & 7)) << 4));
+    if (q0w + r < N) *(uint4*)(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8) = v;
   }
+  VS_STAMP_AT(true);
+#ifdef VS_STAMP
+  stamp_acc(4, t_vm);
+  stamp_acc(5, t_bar);
+  stamp_acc(6, VS_CLK() - t_begin);
+#else
+  (void)t_vm;
+  (void)t_bar;
+  (void)t_begin;
+#endif
 }
 
 // ------------------------------------------------------------------ backward: dK, dV
@@ -418,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16_t* __r
 // in double-buffered LDS; ONE barrier per block).  S and dP are produced with the key on the lane
 // and the query on the accumulator row, initialised with -LSE/scale and -delta, so P and dS are
 // directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands: ds_read_tr16_b64).
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                     const bf16_t* __restrict__ dout, int64_t lddo,
                                                                     const float* __restrict__ lse,
                                                                     const float* __restrict__ delta,
@@ -428,7 +577,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16_kernel(const bf16_t
   constexpr int OFF_Q = 0, OFF_DO = 2 * QT, OFF_L = 4 * QT, OFF_DEL = OFF_L + 256, TOTAL = OFF_DEL + 256;
   __shared__ __attribute__((aligned(16))) char smem[TOTAL];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
   const bf16_t* Kp = Qp + D;
@@ -436,7 +586,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16_kernel(const bf16_t
   const bf16_t* Dp = dout + row0 * lddo + h * 64;
   const float* L = lse + ((int64_t)b * H + h) * N;
   const float* Del = delta + ((int64_t)b * H + h) * N;
-  const int ki = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int ki = qb * 128 + wid * 32 + (lane & 31);
   const float inv_scale = 1.f / scale;
   const float c2 = scale * kLog2e;
 
@@ -572,13 +722,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16_t* 
   constexpr int TILE = 64 * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z, D = H * 64;
+  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
   const bf16_t* Kp = Qp + D;
   const bf16_t* Vp = Qp + 2 * D;
   const bf16_t* Dp = dout + row0 * lddo + h * 64;
-  const int qi = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int qi = qb * 128 + wid * 32 + (lane & 31);
   const float c2 = scale * kLog2e;
 
   bf16x8 qf[4], df[4];
@@ -709,7 +860,7 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   if (dtype == VS_BF16) {
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
-    dim3 grid((unsigned)cdiv(N, 128), (unsigned)H, (unsigned)B);
+    dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse,
                        (int)N, (int)H, scale * kLog2e);
   } else if (dtype == VS_F32) {
@@ -747,7 +898,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
                "vs_attn_bwd: bf16 rows must be 16-byte aligned");
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(dgrid), dim3(256), 0, s, (const bf16_t*)o, ld_o,
                        (const bf16_t*)dout, ld_do, delta, rows, (int)N, (int)H);
-    dim3 grid((unsigned)cdiv(N, 128), (unsigned)H, (unsigned)B);
+    dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     hipLaunchKernelGGL(attn_bwd_dkdv_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                        (const bf16_t*)dout, ld_do, lse, delta, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
     hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
@@ -766,3 +917,10 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
+
+#ifdef VS_STAMP
+extern "C" int vs_dbg_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vs::g_stamp), (size_t)n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

@@ -85,4 +85,13 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Bijective XCD-aware block remap for a 1D grid of nwg workgroups.  The dispatcher deals workgroup
+// ids round-robin over the 8 XCDs (id % 8); this returns a logical index such that the workgroups
+// of one XCD get CONSECUTIVE logical indices, so blocks that share operands (e.g. the query blocks
+// of one (batch, head)) share that XCD's L2 instead of being fetched into eight of them.
+__device__ __forceinline__ int xcd_remap(int id, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = id % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+}
+
 }  // namespace vs

@@ -92,10 +92,11 @@ def lib() -> ctypes.CDLL:
     """Load libvspike.so (built in-tree by vspike.build / __graft_entry__.build())."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise VsError(f"libvspike.so not found at {LIB_PATH}: build it with `python -m vspike.build` "
+        path = os.environ.get("VSPIKE_LIB") or LIB_PATH   # override: A/B timing of two builds
+        if not os.path.exists(path):
+            raise VsError(f"libvspike.so not found at {path}: build it with `python -m vspike.build` "
                           "(or __graft_entry__.build()); there is no fallback path")
-        handle = ctypes.CDLL(LIB_PATH)
+        handle = ctypes.CDLL(path)
         for name, (res, args) in PROTOTYPES.items():
             fn = getattr(handle, name)
             fn.restype = res
