@@ -84,9 +84,14 @@ typedef struct vs_gemm_desc {
   int32_t reserved;
   float* a_rowsum;      /* optional [M] f32: += sum_k A(m,k) (the bias gradient of a dW = dY^T X
                            product, fused: replaces a separate column-sum pass over dY) */
+  void* workspace;      /* optional, VS_EPI_ATOMIC split-K only: each split stores its f32 tile   */
+  int64_t workspace_bytes; /* here and a second launch adds the splits into C (instead of f32
+                              atomics); splits are capped to what fits; NULL/0 keeps atomics */
 } vs_gemm_desc;
 
 int vs_gemm(const vs_gemm_desc* d, void* stream);
+/* bytes of split-K workspace the automatic split of an ATOMIC GEMM of this shape would use */
+size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64_t N, int64_t K);
 
 /* ------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, eps = 1e-12 in the reference (mv:416-417, nn.LayerNorm).
@@ -97,10 +102,13 @@ int vs_gemm(const vs_gemm_desc* d, void* stream);
 int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, const float* x, int64_t ldx,
                      const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
                      float* mean, float* rstd, void* stream);
+/* workspace (optional, >= vs_layernorm_bwd_workspace_bytes): dgamma/dbeta partial rows per
+ * block, summed by a second launch; NULL falls back to one f32 atomic per column per block. */
+size_t vs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t cols);
 int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, const float* x,
                      int64_t ldx, const float* mean, const float* rstd, const float* gamma,
                      const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
-                     float* dgamma, float* dbeta, void* stream);
+                     float* dgamma, float* dbeta, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Non-causal multi-head attention, head dim 64 (mv:243-258; SDPA variant mv:286-294):
@@ -200,6 +208,9 @@ typedef struct vs_vit_layer_grad {
   void* d_o;            /* [M, D] dtype */
   void* d_qkv;          /* [M, 3D] dtype */
   void* attn_ws;        /* vs_attn_bwd_workspace_bytes */
+  void* ln_ws;          /* vs_layernorm_bwd_workspace_bytes(M, D) */
+  void* gemm_ws;        /* split-K partials of the weight-gradient GEMMs (optional) */
+  int64_t gemm_ws_bytes;
 } vs_vit_layer_grad;
 
 int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);

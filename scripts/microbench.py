@@ -20,6 +20,8 @@ MFMA = 2.5e15
 
 
 def timeit(fn, reps):
+    if fn is None:
+        return float("nan")
     for _ in range(3):
         fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -32,6 +34,9 @@ def timeit(fn, reps):
     return s.elapsed_time(e) / reps * 1e3  # us
 
 
+SELECT = ""
+
+
 def report(name, us, nbytes, flops):
     gbs = nbytes / (us * 1e-6) / 1e9
     tfs = flops / (us * 1e-6) / 1e12
@@ -41,10 +46,13 @@ def report(name, us, nbytes, flops):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="")
+    ap.add_argument("--only", default="", help="gemm|attn|ln, or gemm:<name substring> for one GEMM")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
     a = ap.parse_args()
+    global SELECT
+    if a.only.startswith("gemm:"):
+        a.only, SELECT = "gemm", a.only[5:]
     dev = "cuda"
     B, N, D, F, H = a.batch, 1568, 192, 768, 3
     M = B * N
@@ -59,32 +67,36 @@ def main():
         dW = {k: torch.zeros(*s, device=dev) for k, s in (("qkv", (3 * D, D)), ("p", (D, D)), ("1", (F, D)), ("2", (D, F)))}
         db = {k: torch.zeros(s, device=dev) for k, s in (("qkv", 3 * D), ("p", D), ("1", F), ("2", D))}
         e2 = 2
-        report("fwd qkv [M,192]x[192,576]", timeit(lambda: ops.linear(x, w3, qkv, bias=b3), a.reps),
+
+        def rep(name, t, nbytes, flops):
+            if SELECT in name:
+                report(name, t(), nbytes, flops)
+        rep("fwd qkv [M,192]x[192,576]", lambda: timeit(lambda: ops.linear(x, w3, qkv, bias=b3), a.reps),
                M * D * e2 + M * 3 * D * e2, 2 * M * D * 3 * D)
-        report("fwd proj +res (f32 out)", timeit(lambda: ops.linear(o, wd, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
+        rep("fwd proj +res (f32 out)", lambda: timeit(lambda: ops.linear(o, wd, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
                                                                    residual=res32, ld_residual=D), a.reps),
                M * D * e2 + 2 * M * D * 4, 2 * M * D * D)
-        report("fwd fc1 +GELU (act+pre)", timeit(lambda: ops.linear(x, w1, a_, bias=b1, epilogue=L.EPI_GELU, aux_out=pre,
+        rep("fwd fc1 +GELU (act+pre)", lambda: timeit(lambda: ops.linear(x, w1, a_, bias=b1, epilogue=L.EPI_GELU, aux_out=pre,
                                                                     ld_aux_out=F), a.reps),
                M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
-        report("fwd fc2 +res (K=768)", timeit(lambda: ops.linear(a_, w2, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
+        rep("fwd fc2 +res (K=768)", lambda: timeit(lambda: ops.linear(a_, w2, y32, bias=bd, epilogue=L.EPI_RESIDUAL,
                                                                  residual=res32, ld_residual=D), a.reps),
                M * F * e2 + 2 * M * D * 4, 2 * M * D * F)
-        report("bwd da = dx W2 * gelu'", timeit(lambda: ops.linear_dx(g_lp, w2, ga, epilogue=L.EPI_GELU_BWD, aux_in=pre,
+        rep("bwd da = dx W2 * gelu'", lambda: timeit(lambda: ops.linear_dx(g_lp, w2, ga, epilogue=L.EPI_GELU_BWD, aux_in=pre,
                                                                       ld_aux_in=F), a.reps),
                M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
-        report("bwd dh2 = da W1 (f32)", timeit(lambda: ops.linear_dx(ga, w1, y32), a.reps),
+        rep("bwd dh2 = da W1 (f32)", lambda: timeit(lambda: ops.linear_dx(ga, w1, y32), a.reps),
                M * F * e2 + M * D * 4, 2 * M * D * F)
-        report("bwd do = dy Wp", timeit(lambda: ops.linear_dx(g_lp, wd, o), a.reps), 2 * M * D * e2, 2 * M * D * D)
-        report("bwd dh1 = dqkv Wqkv (f32)", timeit(lambda: ops.linear_dx(qkv, w3, y32), a.reps),
+        rep("bwd do = dy Wp", lambda: timeit(lambda: ops.linear_dx(g_lp, wd, o), a.reps), 2 * M * D * e2, 2 * M * D * D)
+        rep("bwd dh1 = dqkv Wqkv (f32)", lambda: timeit(lambda: ops.linear_dx(qkv, w3, y32), a.reps),
                M * 3 * D * e2 + M * D * 4, 2 * M * D * 3 * D)
-        report("dW2 [192,768] (+db)", timeit(lambda: ops.linear_dw(g_lp, a_, dW["2"], db=db["2"]), a.reps),
+        rep("dW2 [192,768] (+db)", lambda: timeit(lambda: ops.linear_dw(g_lp, a_, dW["2"], db=db["2"]), a.reps),
                M * (D + F) * e2, 2 * M * D * F)
-        report("dW1 [768,192] (+db)", timeit(lambda: ops.linear_dw(ga, x, dW["1"], db=db["1"]), a.reps),
+        rep("dW1 [768,192] (+db)", lambda: timeit(lambda: ops.linear_dw(ga, x, dW["1"], db=db["1"]), a.reps),
                M * (D + F) * e2, 2 * M * D * F)
-        report("dWp [192,192] (+db)", timeit(lambda: ops.linear_dw(g_lp, o, dW["p"], db=db["p"]), a.reps),
+        rep("dWp [192,192] (+db)", lambda: timeit(lambda: ops.linear_dw(g_lp, o, dW["p"], db=db["p"]), a.reps),
                M * 2 * D * e2, 2 * M * D * D)
-        report("dWqkv [576,192] (+db)", timeit(lambda: ops.linear_dw(qkv, x, dW["qkv"], db=db["qkv"]), a.reps),
+        rep("dWqkv [576,192] (+db)", lambda: timeit(lambda: ops.linear_dw(qkv, x, dW["qkv"], db=db["qkv"]), a.reps),
                M * 4 * D * e2, 2 * M * D * 3 * D)
     if a.only in ("", "attn"):
         qkv = r(M, 3 * D, dt=bf) * 3

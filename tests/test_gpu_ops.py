@@ -103,23 +103,46 @@ def test_gemm_epilogues(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_splitk_atomic_accumulates(dtype):
-    from vspike import ops, _lib as L
-    M, N, K = 64, 192, 25088           # the dW shape: reduction over B*N tokens
+@pytest.mark.parametrize("ws", [None, False])       # split-K partials + reduce launch, or f32 atomics
+@pytest.mark.parametrize("shape", [(64, 192, 25088), (192, 768, 25088), (104, 40, 5000)])
+def test_gemm_splitk_atomic_accumulates(dtype, ws, shape):
+    from vspike import ops
+    M, N, K = shape                    # the dW shapes: reduction over B*N tokens (+ a ragged one)
     dy = _rand(K, M, seed=8).to(dtype)
     x = _rand(K, N, seed=9).to(dtype)
     c = torch.ones(M, N, device=DEV)   # accumulates on top of existing values
     db = torch.full((M,), 3.0, device=DEV)
-    ops.linear_dw(dy.to(DEV), x.to(DEV), c, db=db)   # bias gradient fused (row sums of A = dy^T)
+    ops.linear_dw(dy.to(DEV), x.to(DEV), c, db=db, workspace=ws)   # bias gradient fused (row sums of A)
     ref = dy.double().t() @ x.double() + 1.0
     assert rel(c, ref) < 2e-5
     assert rel(db, dy.double().sum(0) + 3.0) < 2e-5
+    if ws is None:                     # the partial-sum path is deterministic: bit-identical reruns
+        c2 = torch.ones(M, N, device=DEV)
+        ops.linear_dw(dy.to(DEV), x.to(DEV), c2, workspace=ws)
+        assert torch.equal(c, c2)
+
+
+def test_gemm_splitk_workspace_bias_once():
+    from vspike import ops, _lib as L
+    M, N, K = 96, 128, 20000
+    a = _rand(K, M, seed=21).to(torch.bfloat16).to(DEV)
+    b = _rand(K, N, seed=22).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=23).to(DEV)
+    c = torch.zeros(M, N, device=DEV)
+    nb = ops.splitk_workspace_bytes(torch.bfloat16, M, N, K)
+    assert nb > 0
+    ws = torch.empty(nb // 4, device=DEV)
+    ops.gemm(a, b, c, M=M, N=N, K=K, a_kcontig=False, b_kcontig=False, lda=M, ldb=N, ldc=N,
+             epilogue=L.EPI_ATOMIC | L.EPI_BIAS, bias=bias, workspace=ws)
+    ref = a.double().t() @ b.double() + bias.double()
+    assert rel(c, ref) < 2e-5
 
 
 # ----------------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols", [128, 192, 768])
-def test_layernorm_fwd_bwd(dtype, cols):
+@pytest.mark.parametrize("ws", [None, False])       # two-stage dgamma/dbeta reduction, or per-block atomics
+def test_layernorm_fwd_bwd(dtype, cols, ws):
     from vspike import ops
     rows = 333
     x = _rand(rows, cols, seed=10) * 3 + 1
@@ -136,12 +159,22 @@ def test_layernorm_fwd_bwd(dtype, cols):
     yr = torch.nn.functional.layer_norm(xr, (cols,), gr, br, 1e-12)
     assert rel(y.float(), yr.detach()) < (1e-5 if dtype == torch.float32 else 5e-3)
     dx = torch.empty(rows, cols, device=DEV)
+    dx_lp = torch.empty(rows, cols, dtype=torch.bfloat16, device=DEV)
     dg = torch.zeros(cols, device=DEV)
     db = torch.zeros(cols, device=DEV)
-    ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx, dg, db, dres=dres.to(DEV))
+    ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx, dg, db, dres=dres.to(DEV), dx_lp=dx_lp,
+                      workspace=ws)
     gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy.double())
     assert rel(dx, gx + dres.double()) < 1e-5
+    assert torch.equal(dx_lp, dx.to(torch.bfloat16))          # the bf16 copy is the rounded f32 result
     assert rel(dg, gg) < 1e-5 and rel(db, gb) < 1e-5
+    # no residual gradient
+    dx2 = torch.empty(rows, cols, device=DEV)
+    dg.zero_()
+    db.zero_()
+    ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx2, dg, db, workspace=ws)
+    assert rel(dg, gg) < 1e-5 and rel(db, gb) < 1e-5
+    assert rel(dx2, gx) < 1e-5
 
 
 # ----------------------------------------------------------------------------------- attention

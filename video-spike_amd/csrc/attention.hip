@@ -284,6 +284,13 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 //     plus an immediate offset.
 // Softmax VALU of sub-block j overlaps the MFMAs of sub-block j+1 (issue order QK1, SM0, PV0,
 // SM1, PV1).
+// An opaque copy of a lane value: stops loop strength reduction from turning "uniform tile base +
+// lane offset" into one loop-carried 64-bit pointer per DMA stream (30 VGPRs in the dK/dV kernel);
+// the DMA then uses the SGPR-base + 32-bit VGPR-offset form.
+__device__ __forceinline__ uint32_t vopaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ float max3f(float a, float b, float c) {
@@ -414,10 +421,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
     char* dk = buf + wid * 2048;
     char* dv = buf + TILE + wid * 2048;
     if ((kt + 1) * 64 <= N) {
-      glds(kb + gk0, dk);
-      glds(kb + gk1, dk + 1024);
-      glds(vb + gv0, dv);
-      glds(vb + gv1, dv + 1024);
+      glds(kb + vopaque(gk0), dk);
+      glds(kb + vopaque(gk1), dk + 1024);
+      glds(vb + vopaque(gv0), dv);
+      glds(vb + vopaque(gv1), dv + 1024);
     } else {  // partial last tile: rows past N re-read row N-1 (finite data; its scores are masked)
       const int r0 = kt * 64 + prow0, r1 = r0 + 8;
       const int c0 = (r0 < N ? r0 : N - 1) - kt * 64, c1 = (r1 < N ? r1 : N - 1) - kt * 64;
@@ -561,44 +568,101 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 #endif
 }
 
+// ------------------------------------------------------------------ backward: row constants
+// Per (batch, head, query): nlse2 = -LSE * log2(e) and ndel = -delta (delta = rowsum(dO * O)),
+// stored [B*H][Npad] with Npad = N rounded up to 64 and the padding set to (-inf, 0): the dK/dV
+// kernel DMAs 64-query slices of them straight into LDS and seeds its S / dP accumulators with
+// them, and a padded query then contributes exactly P = 0, dS = 0.  One thread per (row, head),
+// eight 16-B loads of O and of dO.
+__global__ __launch_bounds__(256) void attn_rowprep_kernel(const bf16_t* __restrict__ o, int64_t ldo,
+                                                           const bf16_t* __restrict__ dout, int64_t lddo,
+                                                           const float* __restrict__ lse, float* __restrict__ nlse2,
+                                                           float* __restrict__ ndel, int64_t B, int N, int H,
+                                                           int Npad) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * 256;
+  if (t < B * N * H) {
+    const int64_t row = t / H;
+    const int h = (int)(t % H);
+    const int64_t b = row / N, n = row % N;
+    const bf16x8* op = (const bf16x8*)(o + row * ldo + h * 64);
+    const bf16x8* dp = (const bf16x8*)(dout + row * lddo + h * 64);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8 a = op[j], g = dp[j];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf((float)a[k], (float)g[k], acc);
+    }
+    const int64_t w = (b * H + h) * Npad + n;
+    ndel[w] = -acc;
+    nlse2[w] = -lse[(b * H + h) * N + n] * kLog2e;
+  }
+  const int pad = Npad - N;
+  for (int64_t i = t; i < B * H * pad; i += nthreads) {
+    const int64_t w = (i / pad) * Npad + N + i % pad;
+    nlse2[w] = -INFINITY;
+    ndel[w] = 0.f;
+  }
+}
+
 // ------------------------------------------------------------------ backward: dK, dV
-// Key-major.  Workgroup = 4 waves x 32 keys; each wave holds its keys' K, V as MFMA B operands and
-// dK^T, dV^T in accumulators while the workgroup sweeps 32-query blocks (Q, dO, LSE, delta staged
-// in double-buffered LDS; ONE barrier per block).  S and dP are produced with the key on the lane
-// and the query on the accumulator row, initialised with -LSE/scale and -delta, so P and dS are
+// Key-major.  Workgroup = 4 waves x 32 keys; each wave holds its keys' K (pre-scaled by
+// c = scale * log2 e, one bf16 rounding as the forward's Q) and V as MFMA B operands and dK^T,
+// dV^T in accumulators while the workgroup sweeps 64-query slices: Q, dO, nlse2 and ndel arrive
+// by LDS-DMA into a double-buffered stage, one barrier per slice.  S and dP are produced with the
+// key on the lane and the query on the accumulator row; their chains start from nlse2 / ndel
+// (4 ds_read_b128 each), so p = exp2(acc) and dS = p * acc with no other VALU, and P, dS are
 // directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands: ds_read_tr16_b64).
+// The Q/dO images use swz_rt, an XOR swizzle that is conflict-free for BOTH the row reads
+// (ds_read_b128) and the transposed reads (rows r..r+3 land in distinct bank quarters); the
+// previous (r >> 1) & 7 swizzle put rows r and r+2 of every tr read on the same banks.
+__device__ __forceinline__ int swz_rt(int r) {
+  const int u = (r >> 1) & 7;
+  return ((u & 1) << 2) | (u >> 1);
+}
+__device__ __forceinline__ int off_rtswz(int r, int c) { return r * 128 + (((c >> 3) ^ swz_rt(r)) << 4) + (c & 7) * 2; }
+
+__device__ __forceinline__ void glds16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 4, 0, 0);
+}
+
 __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                     const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                    const float* __restrict__ lse,
-                                                                    const float* __restrict__ delta,
+                                                                    const float* __restrict__ nlse2,
+                                                                    const float* __restrict__ ndel,
                                                                     bf16_t* __restrict__ dqkv, int64_t ldd, int N,
-                                                                    int H, float scale) {
-  constexpr int QT = 32 * 128;  // 32 rows x 128 B
-  constexpr int OFF_Q = 0, OFF_DO = 2 * QT, OFF_L = 4 * QT, OFF_DEL = OFF_L + 256, TOTAL = OFF_DEL + 256;
-  __shared__ __attribute__((aligned(16))) char smem[TOTAL];
+                                                                    int H, int Npad, float scale) {
+  constexpr int QT = 64 * 128;            // one 64-query x 64-dh bf16 image
+  constexpr int STG = 2 * QT + 512;       // Q, dO, nlse2[64], ndel[64]
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), kb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
   const bf16_t* Kp = Qp + D;
   const bf16_t* Vp = Qp + 2 * D;
   const bf16_t* Dp = dout + row0 * lddo + h * 64;
-  const float* L = lse + ((int64_t)b * H + h) * N;
-  const float* Del = delta + ((int64_t)b * H + h) * N;
-  const int ki = qb * 128 + wid * 32 + (lane & 31);
-  const float inv_scale = 1.f / scale;
+  const float* NL = nlse2 + ((int64_t)b * H + h) * Npad;
+  const float* ND = ndel + ((int64_t)b * H + h) * Npad;
+  const int ki = kb * 128 + wid * 32 + (lane & 31);
   const float c2 = scale * kLog2e;
 
   bf16x8 kf[4], vf[4];
+  {
+    const int kr = ki < N ? ki : N - 1;  // rows past N: finite data, their dK/dV are not stored
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (ki < N) {
-      kf[s] = *(const bf16x8*)(Kp + (int64_t)ki * ldq + 16 * s + 8 * hh);
-      vf[s] = *(const bf16x8*)(Vp + (int64_t)ki * ldq + 16 * s + 8 * hh);
-    } else {
-      kf[s] = bf16x8{};
-      vf[s] = bf16x8{};
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 k = *(const bf16x8*)(Kp + (int64_t)kr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)k[j] * c2;
+      kf[s] = __builtin_convertvector(v, bf16x8);
+      vf[s] = *(const bf16x8*)(Vp + (int64_t)kr * ldq + 16 * s + 8 * hh);
     }
   }
   f32x16 dkacc[2], dvacc[2];
@@ -610,87 +674,124 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t
     dvacc[1][r] = 0.f;
   }
 
-  uint4 rq, rd;
-  float rl = 0.f;
-  auto load_q = [&](int qb) {
-    const int row = tid >> 3, c = tid & 7, gq = qb * 32 + row;
-    if (gq < N) {
-      rq = *(const uint4*)(Qp + (int64_t)gq * ldq + c * 8);
-      rd = *(const uint4*)(Dp + (int64_t)gq * lddo + c * 8);
-    } else {
-      rq = make_uint4(0, 0, 0, 0);
-      rd = make_uint4(0, 0, 0, 0);
+  // LDS-DMA: wave w fills Q pieces 2w, 2w+1 and dO pieces 2w, 2w+1 (8 rows x 128 B each); lane L
+  // loads the source chunk that belongs at position L & 7 of its row; waves 0 / 1 fill nlse2 / ndel.
+  auto load_stage = [&](int it, char* dst) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;  // recomputed per stage: no live VGPRs
+    const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+    const uint32_t gq0 = (uint32_t)(prow * 2 * ldq) + cq0, gq1 = (uint32_t)((prow + 8) * 2 * ldq) + cq1;
+    const uint32_t gd0 = (uint32_t)(prow * 2 * lddo) + cq0, gd1 = (uint32_t)((prow + 8) * 2 * lddo) + cq1;
+    const int q0 = it * 64;
+    const char* qs = (const char*)(Qp + (int64_t)q0 * ldq);
+    const char* ds = (const char*)(Dp + (int64_t)q0 * lddo);
+    char* dq_ = dst + wid * 2048;
+    char* dd_ = dst + QT + wid * 2048;
+    if (q0 + 64 <= N) {
+      glds16(qs + vopaque(gq0), dq_);
+      glds16(qs + vopaque(gq1), dq_ + 1024);
+      glds16(ds + vopaque(gd0), dd_);
+      glds16(ds + vopaque(gd1), dd_ + 1024);
+    } else {  // partial last slice: rows past N re-read row N-1 (their nlse2 = -inf zeroes them)
+      const int r0 = q0 + prow < N ? prow : N - 1 - q0, r1 = q0 + prow + 8 < N ? prow + 8 : N - 1 - q0;
+      glds16(qs + (int64_t)r0 * 2 * ldq + cq0, dq_);
+      glds16(qs + (int64_t)r1 * 2 * ldq + cq1, dq_ + 1024);
+      glds16(ds + (int64_t)r0 * 2 * lddo + cq0, dd_);
+      glds16(ds + (int64_t)r1 * 2 * lddo + cq1, dd_ + 1024);
     }
-    if (tid < 32) {
-      const int g = qb * 32 + tid;
-      rl = g < N ? L[g] * inv_scale : INFINITY;
-    } else if (tid < 64) {
-      const int g = qb * 32 + tid - 32;
-      rl = g < N ? Del[g] : 0.f;
-    }
-  };
-  auto store_q = [&](int buf) {
-    const int row = tid >> 3, c = tid & 7;
-    const int off = buf * QT + row * 128 + ((c ^ swz_row(row)) << 4);
-    *(uint4*)(smem + OFF_Q + off) = rq;
-    *(uint4*)(smem + OFF_DO + off) = rd;
-    if (tid < 32) ((float*)(smem + OFF_L))[buf * 32 + tid] = rl;
-    else if (tid < 64) ((float*)(smem + OFF_DEL))[buf * 32 + tid - 32] = rl;
+    if (wid == 0) glds4((const char*)(NL + q0) + vopaque(4 * lane), dst + 2 * QT);
+    else if (wid == 1) glds4((const char*)(ND + q0) + vopaque(4 * lane), dst + 2 * QT + 256);
   };
 
-  const int nqb = (N + 31) / 32;
-  load_q(0);
-  store_q(0);
-  __syncthreads();
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
+  // per-lane LDS offsets: row reads of query qrow (+32 per sub-slice), chunk 2s+hh; transposed
+  // reads of rows qt and qt+8 (qt = 4hh + q4, +16 per s2, +32 per sub-slice: immediates)
   const int qrow = lane & 31;
-  for (int qb = 0; qb < nqb; ++qb) {
-    const int buf = qb & 1;
-    const char* sQ = smem + OFF_Q + buf * QT;
-    const char* sD = smem + OFF_DO + buf * QT;
-    const float* sL = (const float*)(smem + OFF_L) + buf * 32;
-    const float* sDel = (const float*)(smem + OFF_DEL) + buf * 32;
-    const bool more = qb + 1 < nqb;
-    if (more) load_q(qb + 1);
+  int roff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) roff[s] = qrow * 128 + (((2 * s + hh) ^ swz_rt(qrow)) << 4);
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, qt = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(qt, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(qt + 8, dt * 32 + g16 + p4);
+  }
 
-    f32x16 sacc, dpacc;
+  // Phased so that S and dP are never live together (fits 3 waves/SIMD): S -> P -> dV += dO^T P,
+  // then dP -> dS = P * dP -> dK += Q^T dS.  sched_barriers keep the scheduler from merging the
+  // phases back (it hoists the second chain's LDS reads and MFMAs otherwise: 212 VGPRs).
+  auto slice = [&](const char* st, int sub) {
+    const char* sQ = st;
+    const char* sD = st + QT;
+    const float* sL = (const float*)(st + 2 * QT) + sub * 32 + 4 * hh;
+    const float* sE = (const float*)(st + 2 * QT + 256) + sub * 32 + 4 * hh;
+    f32x16 acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ql = (r & 3) + 8 * (r >> 2) + 4 * hh;
-      sacc[r] = -sL[ql];
-      dpacc[r] = -sDel[ql];
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *(const float4*)(sL + 8 * g);
+      acc[4 * g] = l4.x; acc[4 * g + 1] = l4.y; acc[4 * g + 2] = l4.z; acc[4 * g + 3] = l4.w;
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int coff = qrow * 128 + (((2 * s + hh) ^ swz_row(qrow)) << 4);
-      const bf16x8 qa = *(const bf16x8*)(sQ + coff);
-      const bf16x8 da = *(const bf16x8*)(sD + coff);
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
-      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dpacc, 0, 0, 0);
-    }
-    float p[16], ds[16];
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(sQ + sub * 4096 + roff[s]), kf[s], acc, 0, 0, 0);
+    bf16x8 pbs[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2);
-      ds[r] = p[r] * dpacc[r];
-    }
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float p[8];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pb = pack8f(p + 8 * s);
-      const bf16x8 db = pack8f(ds + 8 * s);
-      const int q0 = 16 * s + 4 * hh + q4;
+      for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(acc[8 * s2 + r]);
+      const bf16x8 pb = pack8f(p);
+      pbs[s2] = pb;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const int col = dt * 32 + g16 + p4;
-        const int o0 = off_rowswz(q0, col), o1 = off_rowswz(q0 + 8, col);
-        const bf16x8 doa = tr_pair(sD, o0, o1);
-        const bf16x8 qta = tr_pair(sQ, o0, o1);
-        dvacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doa, pb, dvacc[dt], 0, 0, 0);
-        dkacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qta, db, dkacc[dt], 0, 0, 0);
+        const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];
+        dvacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sD, o0, o1), pb, dvacc[dt], 0, 0, 0);
       }
     }
-    if (more) store_q(buf ^ 1);
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 e4 = *(const float4*)(sE + 8 * g);
+      acc[4 * g] = e4.x; acc[4 * g + 1] = e4.y; acc[4 * g + 2] = e4.z; acc[4 * g + 3] = e4.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(sD + sub * 4096 + roff[s]), vf[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float ds[8];  // dS = P * (dP - delta) from the bf16 P of the dV product (carried packed: 8 VGPRs)
+      const uint4 u = __builtin_bit_cast(uint4, pbs[s2]);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float pr = __uint_as_float((r & 1) ? (w[r >> 1] & 0xffff0000u) : (w[r >> 1] << 16));
+        ds[r] = pr * acc[8 * s2 + r];
+      }
+      const bf16x8 db = pack8f(ds);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];
+        dkacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sQ, o0, o1), db, dkacc[dt], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nit = (N + 63) / 64;
+  load_stage(0, smem);
+  auto iter = [&](int it, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of slice it landed
+    __syncthreads();                                  // ... and every wave's; buffer BUF^1 is free
+    if (it + 1 < nit) load_stage(it + 1, smem + (BUF ^ 1) * STG);
+    const char* st = smem + BUF * STG;
+    slice(st, 0);
+    __builtin_amdgcn_sched_barrier(0);  // keep the two slices' S/dP accumulators from overlapping
+    if (it * 64 + 32 < N) slice(st, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int it = 0; it < nit; it += 2) {
+    iter(it, IC<0>{});
+    if (it + 1 < nit) iter(it + 1, IC<1>{});
   }
 
   if (ki < N) {
@@ -709,16 +810,18 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t
 }
 
 // ------------------------------------------------------------------ backward: dQ
-// Query-major, the forward's structure: workgroup = 4 waves x 32 queries, K/V tiles of 64 keys in
-// double-buffered LDS.  S^T = K Q^T and dP^T = V dO^T put the QUERY on the lane, so LSE and delta
-// are per-lane constants; dS^T = P^T (dP^T - delta) is directly the B operand of
-// dQ^T += K^T dS^T (K^T via ds_read_tr16_b64).  No atomics: each query block owns its dQ rows.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+// Query-major, the forward's structure: workgroup = 4 waves x 32 queries, K/V tiles of 64 keys
+// arrive by LDS-DMA into double-buffered images (swz_rt: conflict-free row AND transposed reads
+// of K).  Q is pre-scaled by c = scale * log2 e exactly as in the forward (same bf16 rounding, so
+// P is the forward's P).  S^T = K Q^T and dP^T = V dO^T put the QUERY on the lane; their chains
+// start from per-lane splats of nlse2 and ndel, so p = exp2(acc) and dS^T = p * acc, which is
+// directly the B operand of dQ^T += K^T dS^T (K^T via ds_read_tr16_b64).  No atomics.
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                   const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                  const float* __restrict__ lse,
-                                                                  const float* __restrict__ delta,
+                                                                  const float* __restrict__ nlse2,
+                                                                  const float* __restrict__ ndel,
                                                                   bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
-                                                                  float scale) {
+                                                                  int Npad, float scale) {
   constexpr int TILE = 64 * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
@@ -727,104 +830,117 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16_t* 
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
   const bf16_t* Kp = Qp + D;
-  const bf16_t* Vp = Qp + 2 * D;
   const bf16_t* Dp = dout + row0 * lddo + h * 64;
   const int qi = qb * 128 + wid * 32 + (lane & 31);
   const float c2 = scale * kLog2e;
 
   bf16x8 qf[4], df[4];
+  {
+    const int qr = qi < N ? qi : N - 1;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (qi < N) {
-      qf[s] = *(const bf16x8*)(Qp + (int64_t)qi * ldq + 16 * s + 8 * hh);
-      df[s] = *(const bf16x8*)(Dp + (int64_t)qi * lddo + 16 * s + 8 * hh);
-    } else {
-      qf[s] = bf16x8{};
-      df[s] = bf16x8{};
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c2;
+      qf[s] = __builtin_convertvector(v, bf16x8);
+      df[s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
     }
   }
-  const float lse2 = qi < N ? lse[((int64_t)b * H + h) * N + qi] * kLog2e : INFINITY;
-  const float dl = qi < N ? delta[((int64_t)b * H + h) * N + qi] : 0.f;
-  f32x16 dqacc[2];
+  f32x16 sinit, dinit, dqacc[2];
+  {
+    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
+    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
+    const float nd = qi < N ? ndel[w] : 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    dqacc[0][r] = 0.f;
-    dqacc[1][r] = 0.f;
+    for (int r = 0; r < 16; ++r) {
+      sinit[r] = nl;
+      dinit[r] = nd;
+      dqacc[0][r] = 0.f;
+      dqacc[1][r] = 0.f;
+    }
   }
 
-  uint4 rk[2], rv[2];
-  auto load_tile = [&](int kt) {
+  // per-lane LDS offsets: row reads of key (lane & 31) (+32 rows per kb: immediate), transposed
+  // reads of K rows kt and kt+8 (kt = 4hh + q4; +16 per s2, +32 per kb: immediates)
+  int roff[4];
+  {
+    const int key = lane & 31;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
-      const int gk = kt * 64 + key;
-      if (gk < N) {
-        rk[s] = *(const uint4*)(Kp + (int64_t)gk * ldq + c * 8);
-        rv[s] = *(const uint4*)(Vp + (int64_t)gk * ldq + c * 8);
-      } else {
-        rk[s] = make_uint4(0, 0, 0, 0);
-        rv[s] = make_uint4(0, 0, 0, 0);
-      }
+    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
+  }
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
+  }
+
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  auto load_tile = [&](int kt, char* buf) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const int cc0 = (ppos ^ swz_rt(prow)) << 4, cc1 = (ppos ^ swz_rt(prow + 8)) << 4;
+    const char* kb_ = (const char*)Kp + kt * tile_bytes;
+    char* dk = buf + wid * 2048;
+    char* dv = buf + TILE + wid * 2048;
+    int r0 = prow, r1 = prow + 8;
+    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (masked below)
+      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
+      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
     }
+    const char* s0 = kb_ + vopaque((uint32_t)(r0 * 2 * ldq + cc0));
+    const char* s1 = kb_ + vopaque((uint32_t)(r1 * 2 * ldq + cc1));
+    glds16(s0, dk);
+    glds16(s1, dk + 1024);
+    glds16(s0 + vdelta, dv);
+    glds16(s1 + vdelta, dv + 1024);
   };
-  auto store_tile = [&](int buf) {
-    char* sK = smem + buf * 2 * TILE;
-    char* sV = sK + TILE;
+
+  auto sub = [&](const char* sK, int kb, int key0) {
+    const char* sV = sK + TILE;
+    f32x16 sacc = sinit, dpacc = dinit;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int id = tid + 256 * s, key = id >> 3, c = id & 7;
-      *(uint4*)(sK + key * 128 + ((c ^ swz_row(key)) << 4)) = rk[s];
-      *(uint4*)(sV + key * 128 + ((c ^ swz_row(key)) << 4)) = rv[s];
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(sK + kb * 4096 + roff[s]);
+      const bf16x8 va = *(const bf16x8*)(sV + kb * 4096 + roff[s]);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
+      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpacc, 0, 0, 0);
+    }
+    if (key0 + 32 > N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[r] = -INFINITY;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float ds[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[8 * s2 + r]) * dpacc[8 * s2 + r];
+      const bf16x8 db = pack8f(ds);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = kb * 4096 + s2 * 2048;
+        const bf16x8 ka = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
+        dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db, dqacc[dt], 0, 0, 0);
+      }
     }
   };
 
   const int nkt = (N + 63) / 64;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const char* sK = smem + (kt & 1) * 2 * TILE;
-    const char* sV = sK + TILE;
-    const bool more = kt + 1 < nkt;
-    if (more) load_tile(kt + 1);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      f32x16 sacc, dpacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = 0.f;
-        dpacc[r] = 0.f;
-      }
-      const int key = kb * 32 + (lane & 31);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int off = key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4);
-        const bf16x8 ka = *(const bf16x8*)(sK + off);
-        const bf16x8 va = *(const bf16x8*)(sV + off);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
-        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpacc, 0, 0, 0);
-      }
-      float ds[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pr = __builtin_amdgcn_exp2f(fmaf(sacc[r], c2, -lse2));
-        ds[r] = pr * (dpacc[r] - dl);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 db = pack8f(ds + 8 * s);
-        const int key0 = kb * 32 + 16 * s + 4 * hh + q4;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int col = dt * 32 + g16 + p4;
-          const bf16x8 ka = tr_pair(sK, off_rowswz(key0, col), off_rowswz(key0 + 8, col));
-          dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db, dqacc[dt], 0, 0, 0);
-        }
-      }
-    }
-    if (more) store_tile((kt + 1) & 1);
+  load_tile(0, smem);
+  auto iter = [&](int kt, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (kt + 1 < nkt) load_tile(kt + 1, smem + (BUF ^ 1) * 2 * TILE);
+    const char* cur = smem + BUF * 2 * TILE;
+    sub(cur, 0, kt * 64);
+    if (kt * 64 + 32 < N) sub(cur, 1, kt * 64 + 32);
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    iter(kt, IC<0>{});
+    if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
   }
   if (qi < N) {
     bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
@@ -874,10 +990,12 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   return VS_OK;
 }
 
+static inline int64_t attn_npad(int64_t N) { return (N + 63) / 64 * 64; }
+
 extern "C" size_t vs_attn_bwd_workspace_bytes(int64_t B, int64_t N, int64_t H, int64_t Dh) {
   (void)Dh;
-  // delta [B,H,N] f32, padded to 256 B
-  return ((size_t)(B * H * N) * 4 + 255) / 256 * 256;
+  // bf16: nlse2 and ndel [B*H][Npad] f32; f32: delta [B,H,N] (smaller); 256-B padded
+  return ((size_t)(2 * B * H * attn_npad(N)) * 4 + 255) / 256 * 256;
 }
 
 extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv, int64_t ld_qkv,
@@ -896,13 +1014,19 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_dqkv % 4 == 0 && ld_do % 8 == 0 && aligned16(qkv) && aligned16(dout) &&
                    (((uintptr_t)dqkv) & 7) == 0,
                "vs_attn_bwd: bf16 rows must be 16-byte aligned");
-    hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(dgrid), dim3(256), 0, s, (const bf16_t*)o, ld_o,
-                       (const bf16_t*)dout, ld_do, delta, rows, (int)N, (int)H);
+    VS_REQUIRE(ld_o % 8 == 0 && aligned16(o) && aligned16(workspace), "vs_attn_bwd: o / workspace alignment");
+    const int64_t npad = attn_npad(N);
+    float* nlse2 = (float*)workspace;
+    float* ndel = nlse2 + B * H * npad;
+    hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H, 256)), dim3(256), 0, s, (const bf16_t*)o,
+                       ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     hipLaunchKernelGGL(attn_bwd_dkdv_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
-                       (const bf16_t*)dout, ld_do, lse, delta, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+                       (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
+                       scale);
     hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
-                       (const bf16_t*)dout, ld_do, lse, delta, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, scale);
+                       (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
+                       scale);
   } else if (dtype == VS_F32) {
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,
                        (const float*)dout, ld_do, delta, rows, (int)N, (int)H);

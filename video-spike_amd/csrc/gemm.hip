@@ -40,6 +40,7 @@ struct EpiParams {
   int64_t ld_aux_out;
   int vec_ok;  // all leading dims / pointers allow 16-B vectors on 8-column groups
   float* a_rowsum;  // optional: += sum_k A(m, k) (fused bias gradient of dW = dY^T X)
+  float* part;      // split-K partials [split][M][N] (ATOMIC with workspace), else null
 };
 
 // Row sums of the A fragments a wave consumed (lane holds row (lane & 15) of 16-row fragment i):
@@ -179,7 +180,8 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
 // row order.  `lds` must hold BM*(BN+4) floats; callers sync before (LDS reuse) — done here.
 template <int BM, int BN, int TM, int TN>
 __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const f32x4 (&acc)[TM][TN], int64_t m0,
-                                           int64_t n0, bool first_split) {
+                                           int64_t n0, int split) {
+  const bool first_split = split == 0;
   constexpr int LDT = BN + 4;  // +4 floats: 16-B aligned rows, conflict-free scalar writes
   constexpr int WM = BM / 2, WN = BN / 2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
@@ -192,6 +194,24 @@ __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const
       for (int r = 0; r < 4; ++r)
         lds[(wr * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
   __syncthreads();
+  if (e.part) {
+    // split-K partial: plain 16-B stores of this split's tile (gemm_splitk_reduce adds the splits)
+    float* pbase = e.part + (int64_t)split * e.M * e.N;
+    constexpr int C4 = BN / 4;
+    for (int idx = tid; idx < BM * C4; idx += 256) {
+      const int rr = idx / C4, c4 = idx % C4;
+      const int64_t m = m0 + rr, n = n0 + 4 * c4;
+      if (m < e.M && n < e.N) {
+        const float* src = lds + rr * LDT + 4 * c4;
+        if (n + 4 <= e.N && (e.N & 3) == 0) {
+          *(float4*)(pbase + m * e.N + n) = *(const float4*)src;
+        } else {
+          for (int k = 0; k < 4 && n + k < e.N; ++k) pbase[m * e.N + n + k] = src[k];
+        }
+      }
+    }
+    return;
+  }
   if (e.flags & VS_EPI_ATOMIC) {
     // one column per lane: a wave adds 64 consecutive floats (256 B) of a row per instruction
     for (int idx = tid; idx < BM * BN; idx += 256) {
@@ -379,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restr
     __syncthreads();
   }
   if (rowsum_on) flush_rowsum<TM>(e.a_rowsum, rs, m0 + wr * WM, e.M, lane);
-  store_tile<BM, BN, TM, TN>(e, (float*)smem, acc, m0, n0, split == 0);
+  store_tile<BM, BN, TM, TN>(e, (float*)smem, acc, m0, n0, split);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -496,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restric
     __syncthreads();
   }
   if (rowsum_on) flush_rowsum<2>(e.a_rowsum, rs, m0 + wr * 32, e.M, lane);
-  store_tile<64, 64, 2, 2>(e, smem, acc, m0, n0, split == 0);
+  store_tile<64, 64, 2, 2>(e, smem, acc, m0, n0, split);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -526,6 +546,69 @@ static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
   const int64_t max_s = nk / 8;
   if (s > max_s) s = max_s;
   return s < 1 ? 1 : (int)s;
+}
+
+// C[m, n] += bias[n] + sum_s part[s][m][n]: one float4 of C per thread, splits summed in order
+// (deterministic, unlike the atomic path).
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ part, int splits, int64_t M,
+                                                          int64_t N, float* __restrict__ c, int64_t ldc,
+                                                          const float* __restrict__ bias, int vec) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t MN = M * N;
+  if (vec) {
+    const int64_t e4 = i * 4;
+    if (e4 >= MN) return;
+    const int64_t m = e4 / N, n = e4 % N;
+    float4 acc = *(const float4*)(part + e4);
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = *(const float4*)(part + sp * MN + e4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (bias) {
+      const float4 bb = *(const float4*)(bias + n);
+      acc.x += bb.x; acc.y += bb.y; acc.z += bb.z; acc.w += bb.w;
+    }
+    float4* dst = (float4*)(c + m * ldc + n);
+    float4 o = *dst;
+    o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+    *dst = o;
+  } else {
+    if (i >= MN) return;
+    const int64_t m = i / N, n = i % N;
+    float acc = part[i];
+    for (int sp = 1; sp < splits; ++sp) acc += part[sp * MN + i];
+    if (bias) acc += bias[n];
+    c[m * ldc + n] += acc;
+  }
+}
+
+// tile / split geometry shared by vs_gemm and vs_gemm_splitk_workspace_bytes
+struct GemmPlan {
+  int BM, BN, BK;
+  GridMap g;
+};
+static GemmPlan plan_gemm(int dtype, int64_t M, int64_t N, int64_t K, int want_split, bool atomic_ok,
+                          int64_t ws_bytes) {
+  GemmPlan p;
+  if (dtype == VS_BF16) {
+    p.BM = M <= 64 ? 64 : 128;
+    p.BN = (N <= 64 || (N % 128 != 0 && N % 64 == 0 && N < 1024)) ? 64 : 128;
+    p.BK = 64;
+  } else {
+    p.BM = p.BN = 64;
+    p.BK = 32;
+  }
+  p.g.tiles_n = (int)cdiv(N, p.BN);
+  p.g.tiles_m = (int)cdiv(M, p.BM);
+  const int64_t nk = cdiv(K, p.BK);
+  int splits = pick_splits((int64_t)p.g.tiles_n * p.g.tiles_m, nk, want_split, atomic_ok);
+  if (ws_bytes > 0 && splits > 1) {  // partials must fit the workspace
+    const int64_t fit = ws_bytes / (M * N * 4);
+    if (splits > fit) splits = (int)(fit < 1 ? 1 : fit);
+  }
+  p.g.k_per_split = cdiv(nk, splits) * p.BK;
+  p.g.splits = (int)(K > 0 ? cdiv(K, p.g.k_per_split) : 1);
+  return p;
 }
 
 static bool vec_ok(const vs_gemm_desc* d) {
@@ -581,20 +664,17 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   e.aux_out = d->aux_out; e.ld_aux_out = d->ld_aux_out;
   e.vec_ok = vec_ok(d);
   e.a_rowsum = d->a_rowsum;
+  e.part = nullptr;
 
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_GEMM, s);
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
-  GridMap g;
+  const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
+  const GemmPlan plan = plan_gemm(d->dtype, d->M, d->N, d->K, d->split_k, atomic_ok, use_ws ? d->workspace_bytes : 0);
+  const GridMap& g = plan.g;
+  if (use_ws && g.splits > 1) e.part = (float*)d->workspace;
   if (d->dtype == VS_BF16) {
-    const int BM = d->M <= 64 ? 64 : 128;
-    const int BN = (d->N <= 64 || (d->N % 128 != 0 && d->N % 64 == 0 && d->N < 1024)) ? 64 : 128;
-    g.tiles_n = (int)cdiv(d->N, BN);
-    g.tiles_m = (int)cdiv(d->M, BM);
-    const int64_t nk = cdiv(d->K, 64);
-    const int splits = pick_splits((int64_t)g.tiles_n * g.tiles_m, nk, d->split_k, atomic_ok);
-    g.k_per_split = cdiv(nk, splits) * 64;
-    g.splits = (int)(d->K > 0 ? cdiv(d->K, g.k_per_split) : 1);
+    const int BM = plan.BM, BN = plan.BN;
     const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
     VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
     if (BM == 128 && BN == 128) launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
@@ -602,12 +682,6 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     else if (BN == 128) launch_bf16<64, 128>(d, (unsigned)nblk, g, e, s);
     else launch_bf16<64, 64>(d, (unsigned)nblk, g, e, s);
   } else {
-    g.tiles_n = (int)cdiv(d->N, 64);
-    g.tiles_m = (int)cdiv(d->M, 64);
-    const int64_t nk = cdiv(d->K, 32);
-    const int splits = pick_splits((int64_t)g.tiles_n * g.tiles_m, nk, d->split_k, atomic_ok);
-    g.k_per_split = cdiv(nk, splits) * 32;
-    g.splits = (int)(d->K > 0 ? cdiv(d->K, g.k_per_split) : 1);
     const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
     VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
     const float* a = (const float*)d->a;
@@ -622,6 +696,19 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     else
       hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   }
+  if (e.part) {
+    const int vec = d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->c) && (!(f & VS_EPI_BIAS) || aligned16(d->bias));
+    const int64_t n_items = vec ? d->M * d->N / 4 : d->M * d->N;
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, s, e.part, g.splits,
+                       d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
+  }
   VS_LAUNCH_CHECK();
   return VS_OK;
+}
+
+extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64_t N, int64_t K) {
+  using namespace vs;
+  if (M <= 0 || N <= 0 || K <= 0 || (dtype != VS_F32 && dtype != VS_BF16)) return 0;
+  const GemmPlan p = plan_gemm(dtype, M, N, K, 0, true, 0);
+  return p.g.splits > 1 ? (size_t)p.g.splits * (size_t)(M * N) * 4 : 0;
 }

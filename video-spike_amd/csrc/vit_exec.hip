@@ -93,6 +93,8 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   {  // dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc2;
+    g.workspace = G->gemm_ws;
+    g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, stream));
   }
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
@@ -104,6 +106,8 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   {  // dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc1;
+    g.workspace = G->gemm_ws;
+    g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, stream));
   }
   {  // dh2 = da W1
@@ -112,11 +116,13 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   // dy = dx' + LN2'(dh2)
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
-                           lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, stream));
+                           lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
   // ---- attention: y = x + o Wp^T + bp
   {  // dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_proj;
+    g.workspace = G->gemm_ws;
+    g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, stream));
   }
   {  // do = dy Wp
@@ -128,6 +134,8 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   {  // dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_qkv;
+    g.workspace = G->gemm_ws;
+    g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, stream));
     // the k bias is not a parameter (fixed 0 in the reference, mv:233): its slot stays exactly 0
     hipError_t e = hipMemsetAsync(G->b_qkv + D, 0, D * sizeof(float), (hipStream_t)stream);
@@ -139,6 +147,6 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   // dx = dy + LN1'(dh1)
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
-                           lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, stream));
+                           lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
   return VS_OK;
 }

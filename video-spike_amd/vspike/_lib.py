@@ -33,7 +33,8 @@ class GemmDesc(ctypes.Structure):
                 ("epilogue", c_u32), ("alpha", c_f32), ("bias", c_p),
                 ("residual", c_p), ("ld_residual", c_i64), ("pos", c_p), ("pos_rows", c_i64),
                 ("aux_in", c_p), ("ld_aux_in", c_i64), ("aux_out", c_p), ("ld_aux_out", c_i64),
-                ("split_k", c_i32), ("reserved", c_i32), ("a_rowsum", c_p)]
+                ("split_k", c_i32), ("reserved", c_i32), ("a_rowsum", c_p), ("workspace", c_p),
+                ("workspace_bytes", c_i64)]
 
 
 class VitLayer(ctypes.Structure):
@@ -53,7 +54,7 @@ class VitLayerGrad(ctypes.Structure):
                 ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
                 ("dx_out", c_p), ("dx_out_lp", c_p), ("dx_in", c_p), ("dx_in_lp", c_p),
                 ("d_a", c_p), ("d_h", c_p), ("dy", c_p), ("dy_lp", c_p), ("d_o", c_p), ("d_qkv", c_p),
-                ("attn_ws", c_p)]
+                ("attn_ws", c_p), ("ln_ws", c_p), ("gemm_ws", c_p), ("gemm_ws_bytes", c_i64)]
 
 
 # every entry point of include/vspike.h: name -> (restype, argtypes)
@@ -65,8 +66,10 @@ PROTOTYPES = {
     "vs_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p]),
     "vs_layernorm_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p,
                                         c_p]),
+    "vs_layernorm_bwd_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "vs_gemm_splitk_workspace_bytes": (c_sz, [c_i32, c_i64, c_i64, c_i64]),
     "vs_layernorm_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
-                                        c_i64, c_p, c_p, c_p, c_p]),
+                                        c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),
     "vs_attn_bwd_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "vs_attn_bwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,

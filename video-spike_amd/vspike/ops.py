@@ -16,8 +16,9 @@ from ._lib import check, lib, ptr, require_device, stream
 
 def gemm(a, b, c, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, ldc, epilogue=0, alpha=1.0, bias=None,
          residual=None, ld_residual=0, pos=None, pos_rows=0, aux_in=None, ld_aux_in=0, aux_out=None,
-         ld_aux_out=0, split_k=0, a_rowsum=None):
-    """C[M,N] = epilogue(alpha * A @ B); layouts as in include/vspike.h (vs_gemm)."""
+         ld_aux_out=0, split_k=0, a_rowsum=None, workspace=None):
+    """C[M,N] = epilogue(alpha * A @ B); layouts as in include/vspike.h (vs_gemm).
+    workspace: optional device tensor for split-K partials of an ATOMIC GEMM (see vs_gemm_desc)."""
     require_device(a, b, c)
     d = L.GemmDesc()
     d.dtype = L.dtype_code(a.dtype)
@@ -35,6 +36,8 @@ def gemm(a, b, c, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, ldc, epilogue=0, a
     d.aux_out, d.ld_aux_out = ptr(aux_out), ld_aux_out
     d.split_k = split_k
     d.a_rowsum = ptr(a_rowsum)
+    if workspace is not None:
+        d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     check(lib().vs_gemm(ctypes.byref(d), stream()), "vs_gemm")
     return c
 
@@ -60,14 +63,23 @@ def linear_dx(dy, w, out, *, epilogue=0, accumulate=False, **kw):
                 ldc=out.stride(0), epilogue=epilogue, **kw)
 
 
-def linear_dw(dy, x, dw, *, accumulate=True, db=None):
-    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw; split-K atomics over the M reduction).
-    db (optional, f32 [N]) += column sums of dy, fused into the same pass."""
+def splitk_workspace_bytes(dtype, M, N, K):
+    return int(lib().vs_gemm_splitk_workspace_bytes(L.dtype_code(dtype), M, N, K))
+
+
+def linear_dw(dy, x, dw, *, accumulate=True, db=None, workspace=None):
+    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (f32 dw, split-K over the M reduction).
+    db (optional, f32 [N]) += column sums of dy, fused into the same pass.  The splits are summed
+    through `workspace` (allocated here when None; False = f32 atomics instead)."""
     M, N = dy.shape
     K = x.shape[1]
     epi = L.EPI_ATOMIC if accumulate else 0
+    if accumulate and workspace is None:
+        nb = splitk_workspace_bytes(dy.dtype, N, K, M)
+        workspace = torch.empty(nb // 4 + 4, dtype=torch.float32, device=dy.device) if nb else None
+    ws = None if workspace is False else workspace
     return gemm(dy, x, dw, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=dy.stride(0), ldb=x.stride(0),
-                ldc=dw.stride(0), epilogue=epi, split_k=0 if accumulate else 1, a_rowsum=db)
+                ldc=dw.stride(0), epilogue=epi, split_k=0 if accumulate else 1, a_rowsum=db, workspace=ws)
 
 
 def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd):
@@ -79,13 +91,23 @@ def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd):
     return y
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=None):
+def layernorm_bwd_workspace_bytes(rows, cols):
+    return int(lib().vs_layernorm_bwd_workspace_bytes(rows, cols))
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=None, workspace=None):
+    """LayerNorm backward; dgamma/dbeta accumulate.  `workspace` (f32, >= layernorm_bwd_workspace_bytes)
+    is allocated here when not given; pass False to use the per-block atomic reduction instead."""
     require_device(dy, x, dx)
     rows, cols = x.shape
+    if workspace is None:
+        workspace = torch.empty(layernorm_bwd_workspace_bytes(rows, cols) // 4 + 4, dtype=torch.float32,
+                                device=x.device)
+    ws = None if workspace is False else workspace
     check(lib().vs_layernorm_bwd(rows, cols, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
                                  rstd.data_ptr(), gamma.data_ptr(), ptr(dres), dres.stride(0) if dres is not None else 0,
                                  dx.data_ptr(), dx.stride(0), ptr(dx_lp), dgamma.data_ptr(), dbeta.data_ptr(),
-                                 stream()), "vs_layernorm_bwd")
+                                 ptr(ws), stream()), "vs_layernorm_bwd")
     return dx
 
 

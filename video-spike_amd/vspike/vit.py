@@ -294,6 +294,9 @@ class VideoMAE(nn.Module):
             for k in ("dy_lp", "dxA_lp", "dxB_lp"):
                 ar.add(k, (M, D), dt)
         ar.add("attn_ws", (ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64,), torch.float32)
+        ar.add("ln_ws", (ops.layernorm_bwd_workspace_bytes(B * N, D) // 4 + 64,), torch.float32)
+        gws = max(ops.splitk_workspace_bytes(dt, m, n, M) for m, n in ((D, F), (F, D), (D, D), (3 * D, D)))
+        ar.add("gemm_ws", (gws // 4 + 64,), torch.float32)
         g = ar.allocate(dev)
         lp = dt != torch.float32
 
@@ -313,6 +316,8 @@ class VideoMAE(nn.Module):
             gs.d_a, gs.d_h, gs.dy = g["d_a"].data_ptr(), g["d_h"].data_ptr(), g["dy"].data_ptr()
             gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
             gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
+            gs.ln_ws = g["ln_ws"].data_ptr()
+            gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
             ops.vit_layer_bwd(s, gs)
             dx, dx_lp = g[nxt], (g[nxt + "_lp"] if lp else None)
             lo, hi = lay.layer_ranges[i]
