@@ -31,6 +31,7 @@ extern "C" {
 /* element types */
 #define VS_F32 0
 #define VS_BF16 1
+#define VS_U8 2   /* raw video frames only (vs_video_preprocess) */
 
 int vs_version(void);                 /* ABI version (monotonic) */
 const char* vs_last_error(void);      /* static string, last VS_EINVAL reason */
@@ -126,6 +127,20 @@ int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, cons
                 int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,
                 const float* lse, void* dqkv, int64_t ld_dqkv, void* workspace, float scale,
                 void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * On-device video preprocessing, the VideoMAE plugin's forward prologue (videomae.py:18-25):
+ * frame gather video[:, frame_idx] -> gray repeated to 3 channels -> the HF image processor's
+ * resize (shortest edge -> out_size, PIL BILINEAR on uint8 frames, reproduced bit-exactly:
+ * 22-bit fixed-point weights, horizontal then vertical pass through a uint8 intermediate) ->
+ * centre crop out_size (a no-op for square frames) -> rescale 1/255 -> (x - mean[c]) / std[c].
+ * video: (B, T, 1, H, W) contiguous, `in_dtype` VS_F32 (integer-valued 0..255, truncated like
+ * numpy astype(uint8)) or VS_U8; H == W, H <= 7 * out_size.  frame_idx: HOST array of n_frames
+ * (<= 64) source frame indices.  mean/std: HOST float[3].  out: (B, n_frames, 3, S, S) f32.
+ * ------------------------------------------------------------------------------------------ */
+int vs_video_preprocess(int32_t in_dtype, int64_t B, int64_t T, int64_t H, int64_t W, const void* video,
+                        const int32_t* frame_idx, int32_t n_frames, int64_t out_size, const float* mean,
+                        const float* std, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Tubelet patch gather (im2col) for the Conv3d patch embedding (mv:176-181, 194-195):

@@ -19,6 +19,9 @@ Reference citations (paths relative to the reference repo root):
   * `src/model/videomae/modeling_videomae.py:419-445` pre-LN block
   * `src/train.py:59` + `src/trainer/base.py:141-143` PoissonNLLLoss(log_input=True).mean()
   * `src/train.py:44-57` + `src/trainer/base.py:144-159` AdamW + OneCycleLR train step
+  * `src/model/videomae.py:10-11,18-25`             K0 preprocessing: frame gather, gray->RGB, HF image processor
+    (third-party: transformers VideoMAEImageProcessor -> PIL Image.resize BILINEAR on uint8 frames,
+    Pillow `src/libImaging/Resample.c`; rescale in float64 `image_transforms.rescale`; f32 normalise)
 """
 from __future__ import annotations
 
@@ -307,3 +310,90 @@ def compare_summary(name: str, t: np.ndarray, fx: Dict[str, np.ndarray], rtol: f
         ok &= bool(good)
         msgs.append(f"{key}{name} max|d|={err:.3e} scale={scale:.3e}")
     return ok, "; ".join(msgs)
+
+
+# ------------------------------------------------------------------------------------------------
+# K0: the VideoMAE plugin's preprocessing (src/model/videomae.py:10-11, 18-25), restated.
+# ------------------------------------------------------------------------------------------------
+IMAGENET_DEFAULT_MEAN = (0.485, 0.456, 0.406)   # the un-normalisation videomae-base's pretraining head uses
+IMAGENET_DEFAULT_STD = (0.229, 0.224, 0.225)    # (src/model/videomae/modeling_videomae.py:890-891)
+
+
+def frame_indices(n_frames: int = 16, n_source: int = 120) -> np.ndarray:
+    """`videomae.py:10-11`: (torch.linspace(0, 1, 16) * 119).long()."""
+    return (torch.linspace(0, 1, n_frames) * (n_source - 1)).long().numpy().astype(np.int32)
+
+
+_PIL_BITS = 22  # Pillow PRECISION_BITS for 8-bit images: 32 - 8 - 2
+
+
+def pil_bilinear_coeffs(in_size: int, out_size: int):
+    """Pillow Resample.c `precompute_coeffs` (bilinear, support 1) + `normalize_coeffs_8bpc`:
+    per output index: (xmin, fixed-point weights).  Python floats are IEEE doubles evaluated in
+    the C expression order, so the weights are Pillow's exactly."""
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 1.0 * filterscale
+    ss = 1.0 / filterscale
+    out = []
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = []
+        for x in range(xmax):
+            t = abs((x + xmin - center + 0.5) * ss)
+            w.append(1.0 - t if t < 1.0 else 0.0)
+        ww = 0.0
+        for v in w:
+            ww += v
+        w = [v / ww if ww != 0.0 else v for v in w]
+        k = [int(-0.5 + v * (1 << _PIL_BITS)) if v < 0 else int(0.5 + v * (1 << _PIL_BITS)) for v in w]
+        out.append((xmin, np.array(k, dtype=np.int64)))
+    return out
+
+
+def _clip8(v: np.ndarray) -> np.ndarray:
+    return np.where(v >= (1 << _PIL_BITS << 8), 255, np.where(v <= 0, 0, v >> _PIL_BITS)).astype(np.int64)
+
+
+def pil_resize_u8(img: np.ndarray, out_h: int, out_w: int) -> np.ndarray:
+    """PIL `Image.resize((out_w, out_h), BILINEAR)` of a uint8 (H, W) image: horizontal pass into a
+    uint8 intermediate, then vertical (Resample.c ImagingResampleHorizontal/Vertical_8bpc)."""
+    h, w = img.shape
+    src = img.astype(np.int64)
+    tmp = np.zeros((h, out_w), dtype=np.int64)
+    for xx, (xmin, k) in enumerate(pil_bilinear_coeffs(w, out_w)):
+        acc = np.full(h, 1 << (_PIL_BITS - 1), dtype=np.int64)
+        for i, kk in enumerate(k):
+            acc += src[:, xmin + i] * kk
+        tmp[:, xx] = _clip8(acc)
+    out = np.zeros((out_h, out_w), dtype=np.int64)
+    for yy, (ymin, k) in enumerate(pil_bilinear_coeffs(h, out_h)):
+        acc = np.full(out_w, 1 << (_PIL_BITS - 1), dtype=np.int64)
+        for j, kk in enumerate(k):
+            acc += tmp[ymin + j, :] * kk
+        out[yy, :] = _clip8(acc)
+    return out.astype(np.uint8)
+
+
+def video_preprocess(video: np.ndarray, idx: np.ndarray, size: int = 224, mean=IMAGENET_DEFAULT_MEAN,
+                     std=IMAGENET_DEFAULT_STD) -> np.ndarray:
+    """`videomae.py:18-25` for square frames: video (B, T, 1, H, W) integer-valued 0..255 ->
+    pixel_values (B, F, 3, size, size) f32.  Gray is repeated to RGB (so the three channels differ
+    only by mean/std); HF casts the float frame to uint8 (`astype`), resizes the shortest edge to
+    `size` with PIL, centre-crops `size` (a no-op here), rescales in float64
+    (`image.astype(np.float64) * (1/255)` -> f32) and normalises in f32."""
+    b, t, c, h, w = video.shape
+    assert c == 1 and h == w
+    m = np.asarray(mean, dtype=np.float32)
+    sd = np.asarray(std, dtype=np.float32)
+    out = np.empty((b, len(idx), 3, size, size), dtype=np.float32)
+    for bi in range(b):
+        for fi, src in enumerate(idx):
+            u8 = video[bi, src, 0].astype(np.uint8)
+            r = pil_resize_u8(u8, size, size)
+            x = (r.astype(np.float64) * (1 / 255)).astype(np.float32)
+            for ch in range(3):
+                out[bi, fi, ch] = (x - m[ch]) / sd[ch]
+    return out

@@ -206,6 +206,37 @@ def gen_vit_tiny1l():
     print("vit_tiny1l", fx["loss"])
 
 
+def gen_k0():
+    """K0 (src/model/videomae.py:10-11, 18-25): the reference's preprocessing call pattern on a
+    seeded video, run through the HF image processor itself (VideoMAEImageProcessor, whose
+    videomae-base settings are the class defaults apart from mean/std; the Hub's
+    preprocessor_config cannot be fetched here, so mean/std are ImageNet's, the values the
+    videomae-base pretraining head un-normalises with, modeling_videomae.py:890-891)."""
+    from transformers import VideoMAEImageProcessor
+    proc = VideoMAEImageProcessor(image_mean=list(cpu_ref.IMAGENET_DEFAULT_MEAN),
+                                  image_std=list(cpu_ref.IMAGENET_DEFAULT_STD))
+    B, T, H = 2, 120, 128
+    video = prng.video_frames(11, (B, T, 1, H, H))
+    indicies = (torch.linspace(0, 1, 16) * 119).long()                 # videomae.py:10-11
+    inputs = torch.from_numpy(video)[:, indicies]                       # videomae.py:18-22
+    inputs = inputs.squeeze(2).unsqueeze(-1)
+    inputs = inputs.repeat(1, 1, 1, 1, 3)
+    inputs = inputs.reshape(B * len(indicies), inputs.shape[2], inputs.shape[3], inputs.shape[4])
+    pv = proc(list(inputs), return_tensors="pt")["pixel_values"].squeeze(0)   # :23-24 (minus .cuda())
+    pv = pv.reshape(B, len(indicies), pv.shape[1], pv.shape[2], pv.shape[3]).numpy()
+    # the f32 output is a function of the uint8 resize: recover it exactly from channel 0
+    m0, s0 = np.float32(cpu_ref.IMAGENET_DEFAULT_MEAN[0]), np.float32(cpu_ref.IMAGENET_DEFAULT_STD[0])
+    lut = ((np.arange(256).astype(np.float64) * (1 / 255)).astype(np.float32) - m0) / s0
+    u8 = np.searchsorted(lut, pv[:, :, 0])
+    assert np.array_equal(lut[u8], pv[:, :, 0])
+    fx = {"seed": np.int64(11), "shape": np.array([B, T, 1, H, H]), "idx": indicies.numpy().astype(np.int32),
+          "mean": np.array(cpu_ref.IMAGENET_DEFAULT_MEAN, np.float32), "std": np.array(cpu_ref.IMAGENET_DEFAULT_STD, np.float32),
+          "u8_frames": np.array([0, 5, 10, 15]), "u8": u8[0, [0, 5, 10, 15]].astype(np.uint8)}
+    fx.update(cpu_ref.summarize("pixel_values", pv))
+    np.savez_compressed(os.path.join(OUT, "k0_preprocess.npz"), **fx)
+    print("k0", pv.shape, float(np.linalg.norm(pv)))
+
+
 def gen_configs():
     _, update_config, config_from_kwargs = _ref_imports()
     res = {}
@@ -222,6 +253,6 @@ def gen_configs():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l"]
+    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "k0"]
     for w in which:
         globals()["gen_" + w]()

@@ -39,6 +39,12 @@ def uniform(seed: int, n: int, name: str = "") -> np.ndarray:
     return bits.astype(np.float64) * (1.0 / 9007199254740992.0)
 
 
+def video_frames(seed: int, shape, name: str = "video") -> np.ndarray:
+    """Integer-valued float32 frames in 0..255 (decoded-mp4 pixel values), `shape` e.g. (B, 120, 1, H, W)."""
+    n = int(np.prod(shape))
+    return np.floor(uniform(seed, n, name) * 256.0).astype(np.float32).reshape(shape)
+
+
 def normal(seed: int, shape, name: str = "", std: float = 1.0, mean: float = 0.0) -> np.ndarray:
     """float32 N(mean, std) samples by Box–Muller over two uniform streams."""
     n = int(np.prod(shape)) if len(tuple(np.atleast_1d(shape))) else 1

@@ -35,7 +35,8 @@ def _rand(*shape, dtype=torch.float32, seed=0, scale=1.0):
 
 
 # ------------------------------------------------------------------------------------------ GEMM
-GEMM_SHAPES = [(64, 64, 64), (200, 136, 72), (25, 40, 16), (1568, 192, 192), (7, 576, 192), (256, 64, 2048)]
+GEMM_SHAPES = [(64, 64, 64), (200, 136, 72), (25, 40, 16), (1568, 192, 192), (7, 576, 192), (256, 64, 2048),
+               (296, 200, 128), (136, 72, 192), (264, 64, 64)]   # whole-K-in-LDS path, ragged M/N
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

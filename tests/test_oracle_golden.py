@@ -98,3 +98,20 @@ def test_vit_tiny_full_tokens_matches_reference(golden):
     ok, msg = cpu_ref.compare_summary("last_hidden", hid.numpy(), fx, rtol=1e-4, atol=1e-6)
     assert ok, msg
     np.testing.assert_allclose(out.numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+
+
+def test_k0_preprocess_oracle_matches_reference_processor(golden):
+    """K0 (videomae.py:18-25): the restated PIL bilinear resize + HF rescale/normalise reproduce the
+    HF image processor's output bit for bit (fixture made by oracle/gen_fixtures.py gen_k0)."""
+    import numpy as np
+    from oracle import cpu_ref, prng
+    fx = golden("k0_preprocess.npz")
+    video = prng.video_frames(int(fx["seed"]), tuple(int(v) for v in fx["shape"]))
+    idx = cpu_ref.frame_indices()
+    assert np.array_equal(idx, fx["idx"])
+    pv = cpu_ref.video_preprocess(video, idx, 224, fx["mean"], fx["std"])
+    m0, s0 = np.float32(fx["mean"][0]), np.float32(fx["std"][0])
+    for j, f in enumerate(fx["u8_frames"]):      # exact uint8 resize planes of the reference path
+        u8 = fx["u8"][j].astype(np.float64)
+        assert np.array_equal(((u8 * (1 / 255)).astype(np.float32) - m0) / s0, pv[0, f, 0])
+    cpu_ref.compare_summary("pixel_values", pv, fx, rtol=1e-7, atol=0.0)

@@ -284,13 +284,6 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 //     plus an immediate offset.
 // Softmax VALU of sub-block j overlaps the MFMAs of sub-block j+1 (issue order QK1, SM0, PV0,
 // SM1, PV1).
-// An opaque copy of a lane value: stops loop strength reduction from turning "uniform tile base +
-// lane offset" into one loop-carried 64-bit pointer per DMA stream (30 VGPRs in the dK/dV kernel);
-// the DMA then uses the SGPR-base + 32-bit VGPR-offset form.
-__device__ __forceinline__ uint32_t vopaque(uint32_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
 constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ float max3f(float a, float b, float c) {
@@ -352,7 +345,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
                                                                float* __restrict__ lse, int N, int H,
                                                                float scale_log2) {
   constexpr int TILE = 64 * 128;  // bytes of one 64-key x 64-dh bf16 tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  // The two K/V stages are separate __shared__ objects: alias analysis can then prove that reads
+  // of one stage never touch the DMA in flight into the other, and hipcc does not drain that
+  // prefetch (s_waitcnt vmcnt(0)) before the first LDS read of every tile, as it does with one array.
+  __shared__ __attribute__((aligned(16))) char smem0[2 * TILE];
+  __shared__ __attribute__((aligned(16))) char smem1[2 * TILE];
   VS_STAMP_AT(false);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
   const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
@@ -498,13 +495,13 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   // first costs 16 more VGPRs and drops the kernel below 3 waves/SIMD; the 2-3 co-resident waves
   // per SIMD supply the MFMA/VALU overlap instead.
   const int nkt = (N + 63) / 64;
-  load_tile(0, smem);
+  load_tile(0, smem0);
   unsigned long long t_vm = 0, t_bar = 0;
   const unsigned long long t_begin = VS_CLK();
   auto iter = [&](int kt, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    const char* cur = smem + BUF * 2 * TILE;
-    char* nxt = smem + (BUF ^ 1) * 2 * TILE;
+    const char* cur = BUF ? smem1 : smem0;
+    char* nxt = BUF ? smem0 : smem1;
 #ifdef VS_STAMP
     const unsigned long long c0 = VS_CLK();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -537,7 +534,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   const float l = pair_sum(l_half);
   const float inv = 1.f / l;
   __syncthreads();  // every wave is done with the last K/V tile
-  char* so = smem + wid * 4096;
+  char* so = (wid < 2 ? smem0 : smem1) + (wid & 1) * 4096;
   const int oq = lane & 31;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -623,13 +620,6 @@ __device__ __forceinline__ int swz_rt(int r) {
 }
 __device__ __forceinline__ int off_rtswz(int r, int c) { return r * 128 + (((c >> 3) ^ swz_rt(r)) << 4) + (c & 7) * 2; }
 
-__device__ __forceinline__ void glds16(const void* src, void* dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 16, 0, 0);
-}
-__device__ __forceinline__ void glds4(const void* src, void* dst) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 4, 0, 0);
-}
-
 __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                     const bf16_t* __restrict__ dout, int64_t lddo,
                                                                     const float* __restrict__ nlse2,
@@ -638,7 +628,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t
                                                                     int H, int Npad, float scale) {
   constexpr int QT = 64 * 128;            // one 64-query x 64-dh bf16 image
   constexpr int STG = 2 * QT + 512;       // Q, dO, nlse2[64], ndel[64]
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  __shared__ __attribute__((aligned(16))) char stg0[STG];  // two objects: see attn_fwd_bf16_kernel
+  __shared__ __attribute__((aligned(16))) char stg1[STG];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
   const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), kb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
@@ -777,13 +768,13 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t
   };
 
   const int nit = (N + 63) / 64;
-  load_stage(0, smem);
+  load_stage(0, stg0);
   auto iter = [&](int it, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of slice it landed
     __syncthreads();                                  // ... and every wave's; buffer BUF^1 is free
-    if (it + 1 < nit) load_stage(it + 1, smem + (BUF ^ 1) * STG);
-    const char* st = smem + BUF * STG;
+    if (it + 1 < nit) load_stage(it + 1, BUF ? stg0 : stg1);
+    const char* st = BUF ? stg1 : stg0;
     slice(st, 0);
     __builtin_amdgcn_sched_barrier(0);  // keep the two slices' S/dP accumulators from overlapping
     if (it * 64 + 32 < N) slice(st, 1);
@@ -823,7 +814,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_bf16_kernel(const bf16_t* 
                                                                   bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
                                                                   int Npad, float scale) {
   constexpr int TILE = 64 * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE];  // two objects: see attn_fwd_bf16_kernel
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
   const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
@@ -928,13 +920,13 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_bf16_kernel(const bf16_t* 
   };
 
   const int nkt = (N + 63) / 64;
-  load_tile(0, smem);
+  load_tile(0, kv0);
   auto iter = [&](int kt, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nkt) load_tile(kt + 1, smem + (BUF ^ 1) * 2 * TILE);
-    const char* cur = smem + BUF * 2 * TILE;
+    if (kt + 1 < nkt) load_tile(kt + 1, BUF ? kv0 : kv1);
+    const char* cur = BUF ? kv1 : kv0;
     sub(cur, 0, kt * 64);
     if (kt * 64 + 32 < N) sub(cur, 1, kt * 64 + 32);
   };

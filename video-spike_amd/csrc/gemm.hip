@@ -17,6 +17,8 @@
 //   bound, profiles/r01_v0_kernel_stats.csv).  Split-K (VS_EPI_ATOMIC) adds whole 256-B rows.
 // Grid: 1-D, tiles remapped so that consecutive tiles of one XCD (blockIdx % 8 group) share the
 //   A row-panel / the same K slice (bijective remap, cdna_hip_programming.md §5 T1).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace vs {
@@ -113,9 +115,19 @@ __device__ __forceinline__ void st8(void* p, int64_t i, int bf, const float (&v)
   }
 }
 
+// Epilogue flags are a template parameter EF for the combinations the ViT block launches (dead
+// branches vanish: the all-runtime epilogue of a 4-pass unrolled tile is ~9k instructions of
+// mostly-unused GELU/erf/atomic code); kEpiRuntime reads e.flags.
+constexpr uint32_t kEpiRuntime = 0xFFFFFFFFu;
+template <uint32_t EF>
+__device__ __forceinline__ uint32_t epi_flags(const EpiParams& e) {
+  return EF == kEpiRuntime ? e.flags : EF;
+}
+
 // elementwise part of the epilogue for one value (scalar path)
+template <uint32_t EF>
 __device__ __forceinline__ void epi_one(const EpiParams& e, int64_t m, int64_t n, float v) {
-  const uint32_t f = e.flags;
+  const uint32_t f = epi_flags<EF>(e);
   if (f & VS_EPI_BIAS) v += e.bias[n];
   if (f & VS_EPI_POS) v += e.pos[(m % e.pos_rows) * e.N + n];
   if (f & VS_EPI_GELU_BWD) v *= gelu_erf_grad(ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16));
@@ -131,8 +143,9 @@ __device__ __forceinline__ void epi_one(const EpiParams& e, int64_t m, int64_t n
 }
 
 // the same for 8 consecutive columns with 16-B vector accesses
-__device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t n, float (&v)[8]) {
-  const uint32_t f = e.flags;
+template <uint32_t EF>
+__device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t n, float (&v)[8], bool skip_bias) {
+  const uint32_t f = epi_flags<EF>(e) & (skip_bias ? ~(uint32_t)VS_EPI_BIAS : 0xFFFFFFFFu);
   float t[8];
   if (f & VS_EPI_BIAS) {
     ld8(e.bias, n, 0, t);
@@ -148,7 +161,7 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
     ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, t);
     if (f & VS_EPI_GELU_BWD) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= gelu_erf_grad(t[k]);
+      for (int k = 0; k < 8; ++k) v[k] *= e.op_bf16 ? gelu_fast_grad(t[k]) : gelu_erf_grad(t[k]);
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = t[k] > 0.f ? v[k] : 0.f;
@@ -157,7 +170,7 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
   if (f & VS_EPI_GELU) {
     st8(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = gelu_erf(e.op_bf16 ? bf2f(f2bf(v[k])) : v[k]);
+    for (int k = 0; k < 8; ++k) v[k] = e.op_bf16 ? gelu_fast(bf2f(f2bf(v[k]))) : gelu_erf(v[k]);
   }
   if (f & VS_EPI_RELU) {
 #pragma unroll
@@ -178,10 +191,11 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
 
 // Stage a BM x BN f32 tile (16x16-MFMA C layout in `acc`) through LDS and apply the epilogue in
 // row order.  `lds` must hold BM*(BN+4) floats; callers sync before (LDS reuse) — done here.
-template <int BM, int BN, int TM, int TN>
+template <int BM, int BN, int TM, int TN, uint32_t EF>
 __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const f32x4 (&acc)[TM][TN], int64_t m0,
                                            int64_t n0, int split) {
   const bool first_split = split == 0;
+  const uint32_t F = epi_flags<EF>(e);
   constexpr int LDT = BN + 4;  // +4 floats: 16-B aligned rows, conflict-free scalar writes
   constexpr int WM = BM / 2, WN = BN / 2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
@@ -212,14 +226,14 @@ __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const
     }
     return;
   }
-  if (e.flags & VS_EPI_ATOMIC) {
+  if (F & VS_EPI_ATOMIC) {
     // one column per lane: a wave adds 64 consecutive floats (256 B) of a row per instruction
     for (int idx = tid; idx < BM * BN; idx += 256) {
       const int rr = idx / BN, cc = idx % BN;
       const int64_t m = m0 + rr, n = n0 + cc;
       if (m < e.M && n < e.N) {
         float v = lds[rr * LDT + cc];
-        if ((e.flags & VS_EPI_BIAS) && first_split) v += e.bias[n];
+        if ((F & VS_EPI_BIAS) && first_split) v += e.bias[n];
         unsafeAtomicAdd((float*)e.c + m * e.ldc + n, v);
       }
     }
@@ -228,20 +242,37 @@ __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const
   constexpr int CPR = BN / 8;        // 8-column groups per row
   constexpr int RPP = 256 / CPR;     // rows per pass
   const int cg = tid % CPR;
-  for (int rr = tid / CPR; rr < BM; rr += RPP) {
-    const int64_t m = m0 + rr;
-    if (m >= e.M) break;
-    const int64_t n = n0 + cg * 8;
-    if (n >= e.N) continue;
-    const float* src = lds + rr * LDT + cg * 8;
-    if (e.vec_ok && n + 8 <= e.N) {
-      float v[8];
-      const float4 a = *(const float4*)src;
-      const float4 b = *(const float4*)(src + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      epi_eight(e, m, n, v);
-    } else {
-      for (int k = 0; k < 8 && n + k < e.N; ++k) epi_one(e, m, n + k, src[k]);
+  const int64_t n = n0 + cg * 8;     // a thread keeps its column group in every pass
+  if (n >= e.N) return;
+  if (e.vec_ok && n + 8 <= e.N) {
+    // per-column constants loaded once, all passes unrolled: their LDS reads, operand loads and
+    // stores overlap (the rolled loop paid one global-load latency per pass: ~5.5k of a ~10k-cycle
+    // K = 192 tile, scripts/stamp_gemm.py)
+    float bias8[8];
+    if (F & VS_EPI_BIAS) ld8(e.bias, n, 0, bias8);
+#pragma unroll
+    for (int p = 0; p < BM / RPP; ++p) {
+      const int rr = tid / CPR + p * RPP;
+      const int64_t m = m0 + rr;
+      if (m < e.M) {
+        const float* src = lds + rr * LDT + cg * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if (F & VS_EPI_BIAS) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += bias8[k];
+        }
+        epi_eight<EF>(e, m, n, v, true);
+      }
+    }
+  } else {
+    for (int rr = tid / CPR; rr < BM; rr += RPP) {
+      const int64_t m = m0 + rr;
+      if (m >= e.M) break;
+      const float* src = lds + rr * LDT + cg * 8;
+      for (int k = 0; k < 8 && n + k < e.N; ++k) epi_one<EF>(e, m, n + k, src[k]);
     }
   }
 }
@@ -295,6 +326,32 @@ struct OperandBf16 {
       *(uint4*)(lds + off) = reg[s];
     }
   }
+  // LDS-DMA fill of the same image (global_load_lds_dwordx4, 1-KiB pieces, the XOR swizzle moved
+  // to the per-lane source chunk): wave `wid` issues pieces wid*PPW .. +PPW.  Rows / columns past
+  // `rows` re-read the last valid ones (their outputs are never stored); k must be in range.
+  static constexpr int PIECES = BYTES / 1024, PPW = PIECES / 4;
+  __device__ __forceinline__ static void dma(char* lds, const bf16_t* __restrict__ p, int64_t ld, int64_t r0,
+                                             int64_t rows, int64_t k0, int wid, int lane) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pi = wid * PPW + j;
+      const bf16_t* src;
+      if constexpr (KC) {
+        const int r = pi * 8 + (lane >> 3), c = (lane & 7) ^ swz_kc(r);
+        const int64_t gr = r0 + r < rows ? r0 + r : rows - 1;
+        src = p + gr * ld + k0 + c * 8;
+      } else if constexpr (R == 128) {
+        const int k = pi * 4 + (lane >> 4), c = (lane & 15) ^ swz_mc<R>(k);
+        const int64_t gc = r0 + c * 8 <= rows - 8 ? r0 + c * 8 : rows - 8;
+        src = p + (k0 + k) * ld + gc;
+      } else {
+        const int k = pi * 8 + (lane >> 3), c = (lane & 7) ^ swz_mc<R>(k);
+        const int64_t gc = r0 + c * 8 <= rows - 8 ? r0 + c * 8 : rows - 8;
+        src = p + (k0 + k) * ld + gc;
+      }
+      glds16(src, lds + pi * 1024);
+    }
+  }
   // fragment of rows [rb, rb+16) for the 32-deep k step kk (0/1): lane holds rows rb+(lane&15),
   // k = 32kk + 8(lane>>4) + 0..7.
   __device__ __forceinline__ static bf16x8 frag(const char* lds, int rb, int kk, int lane) {
@@ -323,7 +380,7 @@ struct CMax {
   static constexpr int v = A > B ? A : B;
 };
 
-template <int BM, int BN, bool AKC, bool BKC>
+template <int BM, int BN, bool AKC, bool BKC, uint32_t EF>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
                                                            GridMap g, EpiParams e) {
@@ -399,7 +456,89 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const bf16_t* __restr
     __syncthreads();
   }
   if (rowsum_on) flush_rowsum<TM>(e.a_rowsum, rs, m0 + wr * WM, e.M, lane);
-  store_tile<BM, BN, TM, TN>(e, (float*)smem, acc, m0, n0, split);
+  store_tile<BM, BN, TM, TN, EF>(e, (float*)smem, acc, m0, n0, split);
+}
+
+// ----------------------------------------------------------------------------------------------
+// bf16, whole K in LDS (K = 64 * KT <= 256, no split): the skinny projections of the ViT block
+// (K = D = 192, and the N = 192 dX products of the attention/MLP inputs).  With only 3 k-steps the
+// register-staged pipeline above pays one global-load latency per k-step; here every k-step of A
+// and B is DMA'd into LDS in one burst (global_load_lds, no staging registers), one wait, one
+// barrier, then all MFMAs and the epilogue — one latency per tile, and 2 blocks per CU overlap
+// one block's loads with the other's MFMAs and stores.
+// ----------------------------------------------------------------------------------------------
+#ifdef VS_STAMP
+// diagnostic build only: per-wave shader-clock phase marks of the whole-K kernel (vs_dbg_gstamps)
+__device__ unsigned long long g_gstamp[8 * 8192];
+#define VS_GMARK(slot)                                                                        \
+  do {                                                                                        \
+    const int w_ = blockIdx.x * 4 + (threadIdx.x >> 6);                                       \
+    if ((threadIdx.x & 63) == 0 && w_ < 8192) g_gstamp[8 * w_ + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define VS_GMARK(slot)
+#endif
+
+template <int BM, int BN, int KT, bool AKC, bool BKC, uint32_t EF>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_fullk_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                 const bf16_t* __restrict__ B, int64_t ldb,
+                                                                 GridMap g, EpiParams e) {
+  using OA = OperandBf16<BM, AKC>;
+  using OB = OperandBf16<BN, BKC>;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int SMEM = CMax<KT * (OA::BYTES + OB::BYTES), BM*(BN + 4) * 4>::v;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  VS_GMARK(0);
+  int nt, mt, split;
+  map_block(g, nt, mt, split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    OA::dma(smem + t * OA::BYTES, A, lda, m0, e.M, t * 64, wid, lane);
+    OB::dma(smem + KT * OA::BYTES + t * OB::BYTES, B, ldb, n0, e.N, t * 64, wid, lane);
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  VS_GMARK(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  VS_GMARK(2);
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const char* sa = smem + t * OA::BYTES;
+    const char* sb = smem + KT * OA::BYTES + t * OB::BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = OB::frag(sb, wc * WN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  (void)split;
+  VS_GMARK(3);
+  store_tile<BM, BN, TM, TN, EF>(e, (float*)smem, acc, m0, n0, 0);
+  VS_GMARK(4);
+#ifdef VS_STAMP
+  if ((threadIdx.x & 63) == 0) {
+    const int w_ = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w_ < 8192) {
+      g_gstamp[8 * w_ + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      g_gstamp[8 * w_ + 6] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+#endif
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -516,24 +655,65 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(const float* __restric
     __syncthreads();
   }
   if (rowsum_on) flush_rowsum<2>(e.a_rowsum, rs, m0 + wr * 32, e.M, lane);
-  store_tile<64, 64, 2, 2>(e, smem, acc, m0, n0, split);
+  store_tile<64, 64, 2, 2, kEpiRuntime>(e, smem, acc, m0, n0, split);
 }
 
 // ----------------------------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------------------------
-template <int BM, int BN>
-static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
+template <int BM, int BN, uint32_t EF>
+static void launch_bf16_ef(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
   if (d->a_kcontig && d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, true>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else if (d->a_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, false>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, true, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
   else
-    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, false, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+}
+
+template <int BM, int BN, int KT, uint32_t EF>
+static void launch_bf16_fullk_ef(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e,
+                                 hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->a_kcontig && d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_fullk_kernel<BM, BN, KT, true, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, g, e);
+  else if (d->a_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_fullk_kernel<BM, BN, KT, true, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, g, e);
+  else if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_fullk_kernel<BM, BN, KT, false, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, g, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_fullk_kernel<BM, BN, KT, false, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, g, e);
+}
+
+// compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
+#define VS_EPI_SWITCH(F, CALL)                                                             \
+  switch (F) {                                                                             \
+    case 0: CALL(0u); break;                                                               \
+    case VS_EPI_BIAS: CALL((uint32_t)VS_EPI_BIAS); break;                                  \
+    case VS_EPI_BIAS | VS_EPI_RESIDUAL: CALL((uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL)); break; \
+    case VS_EPI_BIAS | VS_EPI_GELU: CALL((uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)); break;    \
+    case VS_EPI_GELU_BWD: CALL((uint32_t)VS_EPI_GELU_BWD); break;                          \
+    default: CALL(kEpiRuntime); break;                                                     \
+  }
+
+template <int BM, int BN>
+static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
+#define L_(EF) launch_bf16_ef<BM, BN, EF>(d, nblk, g, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
+}
+
+template <int BM, int BN, int KT>
+static void launch_bf16_fullk(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e,
+                              hipStream_t s) {
+#define L_(EF) launch_bf16_fullk_ef<BM, BN, KT, EF>(d, nblk, g, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
 }
 
 // Split-K for the token reductions (dW): aim at ~2 blocks per CU, at least 8 k-tiles per split
@@ -549,7 +729,8 @@ static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
 }
 
 // C[m, n] += bias[n] + sum_s part[s][m][n]: one float4 of C per thread, splits summed in order
-// (deterministic, unlike the atomic path).
+// (deterministic, unlike the atomic path), 8 loads in flight per thread (a plain loop over the
+// runtime split count issued them one at a time: 12 us for 25 MB of partials).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ part, int splits, int64_t M,
                                                           int64_t N, float* __restrict__ c, int64_t ldc,
                                                           const float* __restrict__ bias, int vec) {
@@ -559,8 +740,18 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
     const int64_t e4 = i * 4;
     if (e4 >= MN) return;
     const int64_t m = e4 / N, n = e4 % N;
-    float4 acc = *(const float4*)(part + e4);
-    for (int sp = 1; sp < splits; ++sp) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int sp = 0;
+    for (; sp + 8 <= splits; sp += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (sp + u) * MN + e4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; sp < splits; ++sp) {
       const float4 v = *(const float4*)(part + sp * MN + e4);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
@@ -575,8 +766,16 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
   } else {
     if (i >= MN) return;
     const int64_t m = i / N, n = i % N;
-    float acc = part[i];
-    for (int sp = 1; sp < splits; ++sp) acc += part[sp * MN + i];
+    float acc = 0.f;
+    int sp = 0;
+    for (; sp + 8 <= splits; sp += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(sp + u) * MN + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; sp < splits; ++sp) acc += part[sp * MN + i];
     if (bias) acc += bias[n];
     c[m * ldc + n] += acc;
   }
@@ -609,6 +808,15 @@ static GemmPlan plan_gemm(int dtype, int64_t M, int64_t N, int64_t K, int want_s
   p.g.k_per_split = cdiv(nk, splits) * p.BK;
   p.g.splits = (int)(K > 0 ? cdiv(K, p.g.k_per_split) : 1);
   return p;
+}
+
+static int getenv_flag(const char* name) {  // A/B switch for benchmarking, read once
+  static int cached = -1;
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached;
 }
 
 static bool vec_ok(const vs_gemm_desc* d) {
@@ -677,10 +885,27 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     const int BM = plan.BM, BN = plan.BN;
     const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
     VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
-    if (BM == 128 && BN == 128) launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
-    else if (BM == 128) launch_bf16<128, 64>(d, (unsigned)nblk, g, e, s);
-    else if (BN == 128) launch_bf16<64, 128>(d, (unsigned)nblk, g, e, s);
-    else launch_bf16<64, 64>(d, (unsigned)nblk, g, e, s);
+    // whole-K-in-LDS path: K = 64..192 in 64-steps, no split, no fused row sums, 128 x 64 tiles
+    // (72 KB of LDS at K = 192: 2 blocks per CU)
+    const bool fullk = g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 && BM == 128 && !d->a_rowsum &&
+                       !(f & VS_EPI_ATOMIC) && getenv_flag("VSPIKE_NO_FULLK") == 0;
+    if (fullk) {
+      GridMap gf = g;
+      gf.tiles_n = (int)cdiv(d->N, 64);
+      const int64_t nbf = (int64_t)gf.tiles_n * gf.tiles_m;
+      const int KT = (int)(d->K / 64);
+      if (KT == 1) launch_bf16_fullk<128, 64, 1>(d, (unsigned)nbf, gf, e, s);
+      else if (KT == 2) launch_bf16_fullk<128, 64, 2>(d, (unsigned)nbf, gf, e, s);
+      else launch_bf16_fullk<128, 64, 3>(d, (unsigned)nbf, gf, e, s);
+    } else if (BM == 128 && BN == 128) {
+      launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
+    } else if (BM == 128) {
+      launch_bf16<128, 64>(d, (unsigned)nblk, g, e, s);
+    } else if (BN == 128) {
+      launch_bf16<64, 128>(d, (unsigned)nblk, g, e, s);
+    } else {
+      launch_bf16<64, 64>(d, (unsigned)nblk, g, e, s);
+    }
   } else {
     const int64_t nblk = (int64_t)g.tiles_n * g.tiles_m * g.splits;
     VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
@@ -712,3 +937,10 @@ extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64
   const GemmPlan p = plan_gemm(dtype, M, N, K, 0, true, 0);
   return p.g.splits > 1 ? (size_t)p.g.splits * (size_t)(M * N) * 4 : 0;
 }
+
+#ifdef VS_STAMP
+extern "C" int vs_dbg_gstamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vs::g_gstamp), (size_t)n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif

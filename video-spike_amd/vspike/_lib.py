@@ -13,7 +13,7 @@ import torch
 
 from .build import LIB_PATH
 
-VS_F32, VS_BF16 = 0, 1
+VS_F32, VS_BF16, VS_U8 = 0, 1, 2
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM = 0, 1, 2
@@ -68,6 +68,8 @@ PROTOTYPES = {
                                         c_p]),
     "vs_layernorm_bwd_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "vs_gemm_splitk_workspace_bytes": (c_sz, [c_i32, c_i64, c_i64, c_i64]),
+    "vs_video_preprocess": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, ctypes.POINTER(c_i32), c_i32,
+                                           c_i64, ctypes.POINTER(c_f32), ctypes.POINTER(c_f32), c_p, c_p]),
     "vs_layernorm_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
                                         c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),

@@ -209,3 +209,29 @@ def timing_collect(timer: int):
 
 def attn_scale(head_dim: int = 64) -> float:
     return 1.0 / math.sqrt(head_dim)
+
+
+def video_preprocess(video, frame_idx, size=224, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), out=None):
+    """K0 on the device (videomae.py:18-25): raw (B, T, 1, H, W) float32 (integer-valued 0..255) or
+    uint8 video -> pixel_values (B, len(frame_idx), 3, size, size) f32, bit-identical to the
+    reference's HF image processor.  frame_idx: host sequence of source frame indices."""
+    require_device(video)
+    if video.dim() != 5 or video.shape[2] != 1:
+        raise L.VsError("video_preprocess: expected (B, T, 1, H, W)")
+    if video.dtype == torch.uint8:
+        code = L.VS_U8
+    elif video.dtype == torch.float32:
+        code = L.VS_F32
+    else:
+        raise L.VsError("video_preprocess: float32 or uint8 frames")
+    video = video.contiguous()
+    B, T, _, H, W = video.shape
+    idx = [int(i) for i in frame_idx]
+    if out is None:
+        out = torch.empty(B, len(idx), 3, size, size, dtype=torch.float32, device=video.device)
+    fi = (ctypes.c_int32 * len(idx))(*idx)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    sd = (ctypes.c_float * 3)(*[float(v) for v in std])
+    check(lib().vs_video_preprocess(code, B, T, H, W, video.data_ptr(), fi, len(idx), size, m, sd, out.data_ptr(),
+                                    stream()), "vs_video_preprocess")
+    return out

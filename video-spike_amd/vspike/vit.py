@@ -54,8 +54,16 @@ class VideoMAE(nn.Module):
         self.layout = VitLayout(cfg, enc_out, out_dim)
         self.enc_flat = nn.Parameter(torch.zeros(self.layout.enc.numel), requires_grad=not self.freeze_encoder)
         self.head_flat = nn.Parameter(torch.zeros(self.layout.head.numel))
-        # uniform 16-of-120 frame selection of the raw-video path (videomae.py:10-11)
+        # raw-video path (videomae.py:10-11, 18-25): uniform num_frames-of-T frame selection, then
+        # the HF image processor's resize/normalise as one device kernel (vs_video_preprocess).
+        # mean/std: the Hub preprocessor_config of videomae-base cannot be fetched here; default =
+        # ImageNet's, the values its pretraining head un-normalises with (modeling_videomae.py:890-891)
         self.register_buffer("frame_indices", (torch.linspace(0, 1, cfg.num_frames) * 119).long(), persistent=False)
+        pp = _cfg_get(config, "preprocess", None) or {}
+        self.pp_mean = tuple(float(v) for v in (pp.get("mean") if hasattr(pp, "get") and pp.get("mean") else
+                                                (0.485, 0.456, 0.406)))
+        self.pp_std = tuple(float(v) for v in (pp.get("std") if hasattr(pp, "get") and pp.get("std") else
+                                               (0.229, 0.224, 0.225)))
         self.grad_sink = None          # set by vspike.dp.GradExchange for overlapped all-reduce
         self._pos_cache = {}
         self.reset_parameters()
@@ -127,16 +135,28 @@ class VideoMAE(nn.Module):
     # ---------------------------------------------------------------------------------------
     # forward
     # ---------------------------------------------------------------------------------------
+    def raw_frame_indices(self, n_source: int):
+        """videomae.py:10-11 (written for 120 source frames: linspace(0, 1, 16) * 119)."""
+        return (torch.linspace(0, 1, self.backbone.num_frames) * (n_source - 1)).long().tolist()
+
+    def preprocess(self, video: torch.Tensor) -> torch.Tensor:
+        """Raw gray video (B, T, 1, H, W) (float 0..255 or uint8) -> pixel_values on the device."""
+        cfg = self.backbone
+        return ops.video_preprocess(video, self.raw_frame_indices(video.shape[1]), cfg.image_size, self.pp_mean,
+                                    self.pp_std)
+
     def forward(self, inputs: torch.Tensor) -> torch.Tensor:
         cfg = self.backbone
         if inputs.dim() != 5:
             raise ValueError("VideoMAE expects a 5-D tensor")
-        if tuple(inputs.shape[1:]) != (cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size):
-            raise NotImplementedError(
-                f"expected pixel_values (B, {cfg.num_frames}, {cfg.num_channels}, {cfg.image_size}, {cfg.image_size}); "
-                "the reference's CPU preprocessing of raw (B, 120, 1, 128, 128) video (videomae.py:18-25) is not "
-                "on this device path yet")
         L.require_device(inputs)
+        pixel_shape = (cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size)
+        if tuple(inputs.shape[1:]) != pixel_shape:
+            if inputs.shape[2] != 1 or inputs.shape[3] != inputs.shape[4]:
+                raise ValueError(f"expected pixel_values (B, {', '.join(map(str, pixel_shape))}) or raw gray video "
+                                 "(B, T, 1, H, H) as the reference's loader yields (videomae.py:18-25)")
+            with torch.no_grad():
+                inputs = self.preprocess(inputs.detach())
         pixels = inputs.detach().to(torch.float32).contiguous()
         return _VideoMAEFn.apply(pixels, self.enc_flat, self.head_flat, self)
 
@@ -233,9 +253,12 @@ class VideoMAE(nn.Module):
             x_flat_lp = x_flat
         z, r = act["z"], act["r"]
         z.zero_()
+        # split-K over the N*D = 301,056-long reduction; partials summed in order (deterministic)
+        hws = ops.splitk_workspace_bytes(x_flat_lp.dtype, B, self.layout.enc_out, N * D)
+        hws = torch.empty(hws // 4 + 4, dtype=torch.float32, device=dev) if hws else None
         ops.gemm(x_flat_lp, lh.view(head_lp, "enc_w"), z, M=B, N=self.layout.enc_out, K=N * D, a_kcontig=True,
                  b_kcontig=True, lda=N * D, ldb=N * D, ldc=self.layout.enc_out, epilogue=L.EPI_ATOMIC | L.EPI_BIAS,
-                 bias=lh.view(head32, "enc_b"))
+                 bias=lh.view(head32, "enc_b"), workspace=hws)
         ops.linear(z, lh.view(head32, "dec_w"), r, bias=lh.view(head32, "dec_b"))
         state = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_flat_lp": x_flat_lp,
                  "x_final": x, "B": B}
