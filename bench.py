@@ -69,6 +69,20 @@ def cpu_baseline(model_cfg, neurons, seconds):
                       f"fp32 torch-CPU oracle, {el:.1f} s"}
 
 
+def _traffic(op):
+    """HBM bytes per launch of `op` from the committed PMC summary (scripts/pmc_traffic.sh: separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), or None."""
+    import glob as _glob
+    files = sorted(_glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return round(d["ops"][op]["traffic_bytes"], 0)
+    except (KeyError, ValueError, OSError):
+        return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,7 +164,7 @@ def main():
     if dom:
         r = roof_all[dom]
         roofline = {"bound": "mfma", "kernel": dom, "achieved": round(r["achieved_tflops"], 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(r["achieved_tflops"] / peak, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(r["achieved_tflops"] / peak, 4), "traffic": _traffic(dom),
                     "avg_launch_ms": round(r["avg_ms"], 4), "flop_per_launch": r["flop_per_launch"],
                     "all": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                             for k, v in roof_all.items()}}

@@ -307,8 +307,6 @@ __device__ __forceinline__ float pair_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int I>
-using IC = std::integral_constant<int, I>;
 
 #ifdef VS_STAMP
 // Diagnostic build only (-DVS_STAMP): per wave {start, end} realtime ticks (100 MHz), HW ids, and

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "vspike.h"
@@ -118,6 +120,10 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
+// compile-time integer tag (unrolled loops over LDS stages)
+template <int I>
+using IC = std::integral_constant<int, I>;
+
 // ---- LDS-DMA (global_load_lds): one wave-instruction writes 64 x size bytes to a wave-uniform
 // LDS base + lane * size; the source address is per lane.
 // An opaque copy of a lane value: stops loop strength reduction from turning "uniform tile base +
@@ -129,6 +135,24 @@ __device__ __forceinline__ uint32_t vopaque(uint32_t x) {
 }
 __device__ __forceinline__ void glds16(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 16, 0, 0);
+}
+// The same DMA as inline asm, invisible to hipcc's waitcnt insertion.  Beside more in-flight
+// LDS-DMA stores than it can track separately, hipcc waits vmcnt(0) before every LDS read and so
+// drains a prefetch ring; a kernel using this form must order its own LDS reads after the DMA
+// with counted s_waitcnt vmcnt + barriers, and must not mix it with compiler-visible loads in the
+// same span.  M0 is saved and restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16_asm(const void* src, void* dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(VS_LDS void*)dst;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
 }
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 4, 0, 0);

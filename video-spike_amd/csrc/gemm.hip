@@ -190,89 +190,99 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
 }
 
 // Stage a BM x BN f32 tile (16x16-MFMA C layout in `acc`) through LDS and apply the epilogue in
-// row order.  `lds` must hold BM*(BN+4) floats; callers sync before (LDS reuse) — done here.
-template <int BM, int BN, int TM, int TN, uint32_t EF>
+// row order.  PARTS = 2 stages the two 64-row halves one after the other (the waves of row block
+// wr write in pass wr), halving the staging LDS; `lds` must hold (BM/PARTS)*(BN+4) floats.
+template <int BM, int BN, int TM, int TN, uint32_t EF, int PARTS = 1>
 __device__ __forceinline__ void store_tile(const EpiParams& e, float* lds, const f32x4 (&acc)[TM][TN], int64_t m0,
                                            int64_t n0, int split) {
+  static_assert(PARTS == 1 || (PARTS == 2 && BM / 2 == BM / 2 / 16 * 16), "row halves");
   const bool first_split = split == 0;
   const uint32_t F = epi_flags<EF>(e);
   constexpr int LDT = BN + 4;  // +4 floats: 16-B aligned rows, conflict-free scalar writes
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / 2, WN = BN / 2, RB = BM / PARTS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        lds[(wr * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
-  __syncthreads();
-  if (e.part) {
-    // split-K partial: plain 16-B stores of this split's tile (gemm_splitk_reduce adds the splits)
-    float* pbase = e.part + (int64_t)split * e.M * e.N;
-    constexpr int C4 = BN / 4;
-    for (int idx = tid; idx < BM * C4; idx += 256) {
-      const int rr = idx / C4, c4 = idx % C4;
-      const int64_t m = m0 + rr, n = n0 + 4 * c4;
-      if (m < e.M && n < e.N) {
-        const float* src = lds + rr * LDT + 4 * c4;
-        if (n + 4 <= e.N && (e.N & 3) == 0) {
-          *(float4*)(pbase + m * e.N + n) = *(const float4*)src;
-        } else {
-          for (int k = 0; k < 4 && n + k < e.N; ++k) pbase[m * e.N + n + k] = src[k];
-        }
-      }
-    }
-    return;
-  }
-  if (F & VS_EPI_ATOMIC) {
-    // one column per lane: a wave adds 64 consecutive floats (256 B) of a row per instruction
-    for (int idx = tid; idx < BM * BN; idx += 256) {
-      const int rr = idx / BN, cc = idx % BN;
-      const int64_t m = m0 + rr, n = n0 + cc;
-      if (m < e.M && n < e.N) {
-        float v = lds[rr * LDT + cc];
-        if ((F & VS_EPI_BIAS) && first_split) v += e.bias[n];
-        unsafeAtomicAdd((float*)e.c + m * e.ldc + n, v);
-      }
-    }
-    return;
-  }
   constexpr int CPR = BN / 8;        // 8-column groups per row
   constexpr int RPP = 256 / CPR;     // rows per pass
   const int cg = tid % CPR;
   const int64_t n = n0 + cg * 8;     // a thread keeps its column group in every pass
-  if (n >= e.N) return;
-  if (e.vec_ok && n + 8 <= e.N) {
-    // per-column constants loaded once, all passes unrolled: their LDS reads, operand loads and
-    // stores overlap (the rolled loop paid one global-load latency per pass: ~5.5k of a ~10k-cycle
-    // K = 192 tile, scripts/stamp_gemm.py)
-    float bias8[8];
-    if (F & VS_EPI_BIAS) ld8(e.bias, n, 0, bias8);
+  const bool vec = e.vec_ok && n + 8 <= e.N;
+  float bias8[8];
+  if ((F & VS_EPI_BIAS) && vec && !(F & VS_EPI_ATOMIC) && !e.part) ld8(e.bias, n, 0, bias8);
 #pragma unroll
-    for (int p = 0; p < BM / RPP; ++p) {
-      const int rr = tid / CPR + p * RPP;
-      const int64_t m = m0 + rr;
-      if (m < e.M) {
-        const float* src = lds + rr * LDT + cg * 8;
-        float v[8];
-        const float4 a = *(const float4*)src;
-        const float4 b = *(const float4*)(src + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        if (F & VS_EPI_BIAS) {
+  for (int part = 0; part < PARTS; ++part) {
+    const int64_t mp = m0 + part * RB;  // first output row of this pass
+    __syncthreads();
+    if (PARTS == 1 || wr == part) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] += bias8[k];
-        }
-        epi_eight<EF>(e, m, n, v, true);
-      }
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            lds[(wr * WM - part * RB + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] =
+                acc[i][j][r] * e.alpha;
     }
-  } else {
-    for (int rr = tid / CPR; rr < BM; rr += RPP) {
-      const int64_t m = m0 + rr;
-      if (m >= e.M) break;
-      const float* src = lds + rr * LDT + cg * 8;
-      for (int k = 0; k < 8 && n + k < e.N; ++k) epi_one<EF>(e, m, n + k, src[k]);
+    __syncthreads();
+    if (e.part) {
+      // split-K partial: plain 16-B stores of this split's tile (gemm_splitk_reduce adds the splits)
+      float* pbase = e.part + (int64_t)split * e.M * e.N;
+      constexpr int C4 = BN / 4;
+      for (int idx = tid; idx < RB * C4; idx += 256) {
+        const int rr = idx / C4, c4 = idx % C4;
+        const int64_t m = mp + rr, nn = n0 + 4 * c4;
+        if (m < e.M && nn < e.N) {
+          const float* src = lds + rr * LDT + 4 * c4;
+          if (nn + 4 <= e.N && (e.N & 3) == 0) {
+            *(float4*)(pbase + m * e.N + nn) = *(const float4*)src;
+          } else {
+            for (int k = 0; k < 4 && nn + k < e.N; ++k) pbase[m * e.N + nn + k] = src[k];
+          }
+        }
+      }
+      continue;
+    }
+    if (F & VS_EPI_ATOMIC) {
+      // one column per lane: a wave adds 64 consecutive floats (256 B) of a row per instruction
+      for (int idx = tid; idx < RB * BN; idx += 256) {
+        const int rr = idx / BN, cc = idx % BN;
+        const int64_t m = mp + rr, nn = n0 + cc;
+        if (m < e.M && nn < e.N) {
+          float v = lds[rr * LDT + cc];
+          if ((F & VS_EPI_BIAS) && first_split) v += e.bias[nn];
+          unsafeAtomicAdd((float*)e.c + m * e.ldc + nn, v);
+        }
+      }
+      continue;
+    }
+    if (n >= e.N) continue;
+    if (vec) {
+      // per-column constants loaded once, all row passes unrolled: their LDS reads, operand loads
+      // and stores overlap (the rolled loop paid one global-load latency per pass: ~5.5k of a
+      // ~10k-cycle K = 192 tile, scripts/stamp_gemm.py)
+#pragma unroll
+      for (int p = 0; p < RB / RPP; ++p) {
+        const int rr = tid / CPR + p * RPP;
+        const int64_t m = mp + rr;
+        if (m < e.M) {
+          const float* src = lds + rr * LDT + cg * 8;
+          float v[8];
+          const float4 a = *(const float4*)src;
+          const float4 b = *(const float4*)(src + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          if (F & VS_EPI_BIAS) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += bias8[k];
+          }
+          epi_eight<EF>(e, m, n, v, true);
+        }
+      }
+    } else {
+      for (int rr = tid / CPR; rr < RB; rr += RPP) {
+        const int64_t m = mp + rr;
+        if (m >= e.M) break;
+        const float* src = lds + rr * LDT + cg * 8;
+        for (int k = 0; k < 8 && n + k < e.N; ++k) epi_one<EF>(e, m, n + k, src[k]);
+      }
     }
   }
 }
@@ -330,6 +340,7 @@ struct OperandBf16 {
   // to the per-lane source chunk): wave `wid` issues pieces wid*PPW .. +PPW.  Rows / columns past
   // `rows` re-read the last valid ones (their outputs are never stored); k must be in range.
   static constexpr int PIECES = BYTES / 1024, PPW = PIECES / 4;
+  template <bool ASM = false>
   __device__ __forceinline__ static void dma(char* lds, const bf16_t* __restrict__ p, int64_t ld, int64_t r0,
                                              int64_t rows, int64_t k0, int wid, int lane) {
 #pragma unroll
@@ -349,7 +360,8 @@ struct OperandBf16 {
         const int64_t gc = r0 + c * 8 <= rows - 8 ? r0 + c * 8 : rows - 8;
         src = p + (k0 + k) * ld + gc;
       }
-      glds16(src, lds + pi * 1024);
+      if constexpr (ASM) glds16_asm(src, lds + pi * 1024);
+      else glds16(src, lds + pi * 1024);
     }
   }
   // fragment of rows [rb, rb+16) for the 32-deep k step kk (0/1): lane holds rows rb+(lane&15),
@@ -542,6 +554,98 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_fullk_kernel(const bf16_t* _
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16, long K (K % 64 == 0): 3-stage LDS-DMA ring.  Step t+2 is DMA'd while step t computes, and
+// a counted vmcnt keeps step t+1 in flight across each barrier (raw s_barrier: __syncthreads()
+// would wait vmcnt(0) and drain it).  The three stages are separate __shared__ objects, the loop
+// is unrolled by 3 so every stage index is a constant: alias analysis then keeps hipcc from
+// draining the ring before each step's LDS reads.  The register-staged kernel above had one
+// global-load latency exposed per 64-deep step.  Epilogue staged in two row halves (72 KB of LDS
+// for 128 x 64: 2 blocks per CU).
+// ----------------------------------------------------------------------------------------------
+template <int BM, int BN, bool AKC, bool BKC, uint32_t EF>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_ring_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
+                                                                GridMap g, EpiParams e) {
+  using OA = OperandBf16<BM, AKC>;
+  using OB = OperandBf16<BN, BKC>;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  constexpr int S0 = CMax<STAGE, (BM / 2) * (BN + 4) * 4>::v;
+  constexpr int PER = OA::PPW + OB::PPW;  // DMA wave-instructions per k-step
+  __shared__ __attribute__((aligned(16))) char st0[S0];
+  __shared__ __attribute__((aligned(16))) char st1[STAGE];
+  __shared__ __attribute__((aligned(16))) char st2[STAGE];
+
+  int nt, mt, split;
+  map_block(g, nt, mt, split);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
+  const int64_t k_begin = (int64_t)split * g.k_per_split;
+  const int64_t k_end = k_begin + g.k_per_split < K ? k_begin + g.k_per_split : K;
+  const int nk = (int)((k_end - k_begin) / 64);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool rowsum_on = e.a_rowsum != nullptr && nt == 0 && wc == 0;
+  float rs[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) rs[i] = 0.f;
+
+  auto issue = [&](int t, char* st) {
+    const int64_t k0 = k_begin + (int64_t)t * 64;
+    OA::template dma<true>(st, A, lda, m0, e.M, k0, wid, lane);
+    OB::template dma<true>(st + OA::BYTES, B, ldb, n0, e.N, k0, wid, lane);
+  };
+  auto compute = [&](const char* sa) {
+    const char* sb = sa + OA::BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = OB::frag(sb, wc * WN + j * 16, kk, lane);
+      if (rowsum_on) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rs[i] += (float)af[i][q];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto step = [&](int t, auto sc) {
+    constexpr int S = decltype(sc)::value;
+    const char* cur = S == 0 ? st0 : (S == 1 ? st1 : st2);
+    char* far = S == 0 ? st2 : (S == 1 ? st0 : st1);  // stage of step t + 2
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");  // step t landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's step-t pieces landed; step t-1's stage is free
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) issue(t + 2, far);
+    compute(cur);
+  };
+  if (nk > 0) issue(0, st0);
+  if (nk > 1) issue(1, st1);
+  for (int t = 0; t < nk; t += 3) {
+    step(t, IC<0>{});
+    if (t + 1 < nk) step(t + 1, IC<1>{});
+    if (t + 2 < nk) step(t + 2, IC<2>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the asm DMA is invisible to hipcc's own waits)
+  if (rowsum_on) flush_rowsum<TM>(e.a_rowsum, rs, m0 + wr * WM, e.M, lane);
+  store_tile<BM, BN, TM, TN, EF, 2>(e, (float*)st0, acc, m0, n0, split);
+}
+
+// ----------------------------------------------------------------------------------------------
 // f32 kernel (exact: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
 // ----------------------------------------------------------------------------------------------
 template <bool KC>
@@ -690,6 +794,21 @@ static void launch_bf16_fullk_ef(const vs_gemm_desc* d, unsigned nblk, const Gri
     hipLaunchKernelGGL((gemm_bf16_fullk_kernel<BM, BN, KT, false, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, g, e);
 }
 
+template <int BM, int BN, uint32_t EF>
+static void launch_bf16_ring_ef(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e,
+                                hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->a_kcontig && d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, true, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+  else if (d->a_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, true, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+  else if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, false, true, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, false, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+}
+
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
 #define VS_EPI_SWITCH(F, CALL)                                                             \
   switch (F) {                                                                             \
@@ -704,6 +823,13 @@ static void launch_bf16_fullk_ef(const vs_gemm_desc* d, unsigned nblk, const Gri
 template <int BM, int BN>
 static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
 #define L_(EF) launch_bf16_ef<BM, BN, EF>(d, nblk, g, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
+}
+
+template <int BM, int BN>
+static void launch_bf16_ring(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
+#define L_(EF) launch_bf16_ring_ef<BM, BN, EF>(d, nblk, g, e, s)
   VS_EPI_SWITCH(e.flags, L_)
 #undef L_
 }
@@ -819,6 +945,15 @@ static int getenv_flag(const char* name) {  // A/B switch for benchmarking, read
   return cached;
 }
 
+static int getenv_flag2(const char* name) {
+  static int cached = -1;
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached;
+}
+
 static bool vec_ok(const vs_gemm_desc* d) {
   const uint32_t f = d->epilogue;
   const int ovec = d->out_dtype == VS_BF16 ? 8 : 4;
@@ -833,6 +968,14 @@ static bool vec_ok(const vs_gemm_desc* d) {
 }
 
 }  // namespace vs
+
+// the same K split re-planned for 64-wide column tiles (ring kernel); splits as in the 128-wide
+// plan, re-capped by the workspace (its size was computed for the plan's split count)
+static vs::GridMap plan_gemm_bn64(const vs_gemm_desc* d, const vs::GridMap& g) {
+  vs::GridMap r = g;
+  r.tiles_n = (int)vs::cdiv(d->N, 64);
+  return r;
+}
 
 extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   using namespace vs;
@@ -897,6 +1040,12 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       if (KT == 1) launch_bf16_fullk<128, 64, 1>(d, (unsigned)nbf, gf, e, s);
       else if (KT == 2) launch_bf16_fullk<128, 64, 2>(d, (unsigned)nbf, gf, e, s);
       else launch_bf16_fullk<128, 64, 3>(d, (unsigned)nbf, gf, e, s);
+    } else if (d->K % 64 == 0 && getenv_flag2("VSPIKE_NO_RING") == 0) {
+      // long K: 3-stage DMA ring, BN = 64 tiles (72 KB of LDS at BM = 128: 2 blocks per CU)
+      GridMap gr = plan_gemm_bn64(d, g);
+      const int64_t nbr = (int64_t)gr.tiles_n * gr.tiles_m * gr.splits;
+      if (BM == 128) launch_bf16_ring<128, 64>(d, (unsigned)nbr, gr, e, s);
+      else launch_bf16_ring<64, 64>(d, (unsigned)nbr, gr, e, s);
     } else if (BM == 128 && BN == 128) {
       launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
     } else if (BM == 128) {
