@@ -252,6 +252,32 @@ def test_attention_rescale_branch_forced():
         assert rel(o.float(), o_ref) < tol
 
 
+@pytest.mark.gpu
+def test_attention_extreme_logits_move_reference():
+    """Queries whose scores all lie far below / above 0 force the forward's softmax reference off
+    its default 0 on the first block (m < -32 or > 32 in log2 units), then a late larger score
+    moves it again; the rest of the wave stays on the unshifted fast path."""
+    from vspike import ops
+    B, N, H = 1, 900, 1
+    qkv = _rand(N, 192, seed=41, scale=0.3)
+    u = torch.ones(64) / 8.0
+    qkv[:, 64:128] += u * 6.0                           # every key ~ u
+    qkv[3, 0:64] = -u * 400.0                           # query 3: all scores ~ -37..-40 (log2 ~ -55)
+    qkv[40, 0:64] = u * 400.0                           # query 40: all scores ~ +37 (log2 ~ +55)
+    qkv[70, 0:64] = qkv[800, 64:128] * 30.0             # query 70: key 800 dominates late
+    for dtype, tol in ((torch.float32, 1e-5), (torch.bfloat16, 2e-2)):
+        x = qkv.to(dtype)
+        o = torch.empty(N, 64, dtype=dtype, device=DEV)
+        lse = torch.empty(1, 1, N, device=DEV)
+        ops.attn_fwd(x.to(DEV), o, lse, B, N, H)
+        o_ref, lse_ref = _attn_ref(x.double(), B, N, H)
+        assert torch.isfinite(o.float()).all() and torch.isfinite(lse).all()
+        assert rel(o.float(), o_ref) < tol
+        assert rel(lse, lse_ref) < (1e-5 if dtype == torch.float32 else 3e-3)
+        for r in (3, 40, 70):
+            assert rel(o[r].float(), o_ref[r]) < 3 * tol, r
+
+
 # ---------------------------------------------------------------------------- im2col / misc ops
 def test_im2col_matches_oracle():
     from oracle import cpu_ref

@@ -285,6 +285,10 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 // Softmax VALU of sub-block j overlaps the MFMAs of sub-block j+1 (issue order QK1, SM0, PV0,
 // SM1, PV1).
 constexpr float kRescaleThr = 8.0f;
+constexpr float kRefBand = 32.0f;
+#ifndef VS_FWD_TOPBAR
+#define VS_FWD_TOPBAR 0
+#endif  // forward: p <= 2^32 relative to the reference (f32/bf16-safe)
 
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
@@ -338,18 +342,31 @@ __device__ __forceinline__ void stamp_acc(int slot, unsigned long long v) {
 #define VS_CLK() 0ull
 #endif
 
+// Row sums of P on the matrix pipe.  For v_mfma_f32_16x16x32_bf16 with P's packed half (pa or pb,
+// this lane's 8 keys of query lane&31) as the B operand, column n = lane&15 collects lanes n, n+16,
+// n+32, n+48 = queries n, n+16, n, n+16 in k-slot groups g = lane>>4 = 0..3.  The constant A
+// operand `sel` has row 0 = ones over groups {0, 2} and row 1 = ones over groups {1, 3}, so row 0
+// of the product is query n's sum over the block's keys and row 1 query n+16's.  Two 16-cycle
+// MFMAs per 32-key block replace 15 v_add_f32 per lane (60 VALU issue cycles).
+__device__ __forceinline__ bf16x8 rowsum_selector(int lane) {
+  const int row = lane & 15, g = lane >> 4;
+  const float one = (row == 0 && (g & 1) == 0) || (row == 1 && (g & 1) == 1) ? 1.f : 0.f;
+  const f32x8 v = {one, one, one, one, one, one, one, one};
+  return __builtin_convertvector(v, bf16x8);
+}
+
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                bf16_t* __restrict__ o, int64_t ldo,
                                                                float* __restrict__ lse, int N, int H,
                                                                float scale_log2) {
   constexpr int TILE = 64 * 128;  // bytes of one 64-key x 64-dh bf16 tile
-  // The two K/V stages are separate __shared__ objects: alias analysis can then prove that reads
-  // of one stage never touch the DMA in flight into the other, and hipcc does not drain that
-  // prefetch (s_waitcnt vmcnt(0)) before the first LDS read of every tile, as it does with one array.
+  // Two K/V stages as separate __shared__ objects (DMA into one while the other is read).
   __shared__ __attribute__((aligned(16))) char smem0[2 * TILE];
   __shared__ __attribute__((aligned(16))) char smem1[2 * TILE];
+  __shared__ int redo_flag;
   VS_STAMP_AT(false);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
@@ -358,6 +375,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   const int q0w = qb * 128 + wid * 32;  // this wave's first query
   const int qi = q0w + (lane & 31);
   const float c = scale_log2;
+  if (tid == 0) redo_flag = 0;
 
   bf16x8 qf[4];
 #pragma unroll
@@ -369,14 +387,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
     for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c;
     qf[s] = __builtin_convertvector(v, bf16x8);
   }
-  f32x16 oacc[2], cinit;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    oacc[0][r] = 0.f;
-    oacc[1][r] = 0.f;
-    cinit[r] = 0.f;
-  }
-  float m_run = -INFINITY, l_half = 0.f;
+  const bf16x8 sel = rowsum_selector(lane);
+  f32x16 oacc[2], zero16;
+  f32x4 lacc;
+  float m_run, l_half;
 
   // Per-lane LDS byte offsets, tile-invariant.  Every read is a lane base plus an immediate:
   //  K rows key = kb*32 + (lane&31): swz_row(key + 32) == swz_row(key), so kb adds 32*128 B;
@@ -399,139 +413,224 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   // K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4): one wave-instruction fills a 1-KiB
   // piece = 8 rows x 128 B, lane L writing position L*16.  The LDS images keep their XOR swizzles
   // because each lane loads the SOURCE chunk that belongs at its position: (L&7) ^ swz(row).  Wave
-  // w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1.  No staging registers, no ds_write.
+  // w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1.  The asm DMA (SGPR tile base + per-lane
+  // offset) is invisible to hipcc's waitcnt insertion, which would otherwise drain the in-flight
+  // tile before LDS reads of the other stage; ordering is the loop's explicit vmcnt(0) + barrier.
   const int prow0 = wid * 16 + (lane >> 3), ppos = lane & 7;  // rows prow0 and prow0 + 8
   const uint32_t gk0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_row(prow0)) << 4));
   const uint32_t gk1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_row(prow0 + 8)) << 4));
   const uint32_t gv0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_half(prow0)) << 4));
   const uint32_t gv1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_half(prow0 + 8)) << 4));
   const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
-  auto glds = [](const char* src, char* dst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 16, 0,
-                                     0);
-  };
   auto load_tile = [&](int kt, char* buf) {
     const char* kb = (const char*)Kp + kt * tile_bytes;
     const char* vb = kb + vdelta;
     char* dk = buf + wid * 2048;
     char* dv = buf + TILE + wid * 2048;
     if ((kt + 1) * 64 <= N) {
-      glds(kb + vopaque(gk0), dk);
-      glds(kb + vopaque(gk1), dk + 1024);
-      glds(vb + vopaque(gv0), dv);
-      glds(vb + vopaque(gv1), dv + 1024);
+      glds16_asm_so(kb, gk0, dk);
+      glds16_asm_so(kb, gk1, dk + 1024);
+      glds16_asm_so(vb, gv0, dv);
+      glds16_asm_so(vb, gv1, dv + 1024);
     } else {  // partial last tile: rows past N re-read row N-1 (finite data; its scores are masked)
       const int r0 = kt * 64 + prow0, r1 = r0 + 8;
-      const int c0 = (r0 < N ? r0 : N - 1) - kt * 64, c1 = (r1 < N ? r1 : N - 1) - kt * 64;
-      glds(kb + (int64_t)c0 * 2 * ldq + ((ppos ^ swz_row(prow0)) << 4), dk);
-      glds(kb + (int64_t)c1 * 2 * ldq + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
-      glds(vb + (int64_t)c0 * 2 * ldq + ((ppos ^ swz_half(prow0)) << 4), dv);
-      glds(vb + (int64_t)c1 * 2 * ldq + ((ppos ^ swz_half(prow0 + 8)) << 4), dv + 1024);
+      const uint32_t c0 = (uint32_t)((r0 < N ? r0 : N - 1) - kt * 64) * (uint32_t)(2 * ldq);
+      const uint32_t c1 = (uint32_t)((r1 < N ? r1 : N - 1) - kt * 64) * (uint32_t)(2 * ldq);
+      glds16_asm_so(kb, c0 + ((ppos ^ swz_row(prow0)) << 4), dk);
+      glds16_asm_so(kb, c1 + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
+      glds16_asm_so(vb, c0 + ((ppos ^ swz_half(prow0)) << 4), dv);
+      glds16_asm_so(vb, c1 + ((ppos ^ swz_half(prow0 + 8)) << 4), dv + 1024);
     }
   };
-  auto qk = [&](const char* base, int kb) {
-    f32x16 acc = cinit;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(base + kb * 4096 + kbase[s]), qf[s], acc, 0, 0,
-                                                    0);
-    return acc;
+  struct KFrag {
+    bf16x8 k[4];
   };
-  // acc = log2-domain scores relative to the reference max the QK chain was seeded with (cinit =
-  // -m_run, or 0 before the first tile).  Raises the reference when some lane's scores exceed it
-  // by more than 2^kRescaleThr (always on the first call): shifts acc by d, rescales O and l, and
-  // reports d so that an S accumulator already computed with the old reference can be shifted too.
-  auto softmax = [&](f32x16& acc, int key0, bf16x8& pa, bf16x8& pb, float& d_out) {
-    if (key0 + 32 > N) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
-    }
-    // fast path: this lane's 16 scores only (the xor-32 partner holds the query's other keys);
-    // the pair maximum is formed only on the rare wave-uniform rescale path
-    const float mx = max16(acc);
-    const bool first = m_run == -INFINITY;
-    d_out = 0.f;
-    if (__any(first || mx > kRescaleThr)) {
-      const float mxp = pair_max(mx);
-      const bool grow = first || mxp > kRescaleThr;  // identical in both lanes of a query
-      const float d = grow ? mxp : 0.f;
-      const float alpha = (grow && !first) ? __builtin_amdgcn_exp2f(-d) : 1.f;
-      m_run = grow ? (first ? d : m_run + d) : m_run;
-      l_half *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[r] -= d;
-        oacc[0][r] *= alpha;
-        oacc[1][r] *= alpha;
-        cinit[r] -= d;  // in place: the QK seed stays -m_run in one register set
-      }
-      d_out = d;
-    }
-    float p[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r]);
-    l_half += ((((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) +
-               (((p[8] + p[9]) + (p[10] + p[11])) + ((p[12] + p[13]) + (p[14] + p[15]))));
-    pa = pack8f(p);
-    pb = pack8f(p + 8);
+  struct VFrag {
+    bf16x8 v[4];
   };
-  auto pv = [&](const char* base, int kb, const bf16x8& pa, const bf16x8& pb) {
+  auto kread = [&](const char* base, int kb) {
+    KFrag f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f.k[s] = *(const bf16x8*)(base + kb * 4096 + kbase[s]);
+    return f;
+  };
+  auto vread = [&](const char* base, int kb) {
+    VFrag f;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const char* vb = base + kb * 4096 + s * 2048;
-        const bf16x8 va = tr_pair(vb, vbase[dt], vbase[dt] + 1024);
-        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, s == 0 ? pa : pb, oacc[dt], 0, 0, 0);
+        f.v[2 * s + dt] = tr_pair(vb, vbase[dt], vbase[dt] + 1024);
       }
+    return f;
+  };
+  auto pv = [&](const VFrag& f, const bf16x8& pa, const bf16x8& pb) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.v[2 * s + dt], s == 0 ? pa : pb, oacc[dt], 0, 0, 0);
   };
 
-  // One barrier per 64-key tile, at its top: it publishes tile kt (DMA issued at the top of kt-1)
-  // and retires every wave's reads of the buffer that the DMA for tile kt+1, issued right after it,
-  // overwrites.  The two 32-key halves run serially (QK, softmax, PV): issuing both QK^T halves
-  // first costs 16 more VGPRs and drops the kernel below 3 waves/SIMD; the 2-3 co-resident waves
-  // per SIMD supply the MFMA/VALU overlap instead.
+  // Softmax of one 32-key block.  acc = log2-domain scores s (Q pre-scaled by c; the MFMA chain
+  // starts from 0).
+  //  FAST pass (SAFE = 0): p = exp2(s) against a fixed reference 0 — no row maximum, no rescale,
+  //    no per-score subtraction; row sums on the matrix pipe (lacc).  Exact whenever every query's
+  //    scores stay within about [-60, 60] (log2 units); the epilogue checks the row sums and, if
+  //    any query of the workgroup is outside that band (or overflowed), the workgroup re-runs
+  //  SAFE pass (SAFE = 1): online softmax against a running reference that is raised lazily (a
+  //    wave-uniform rare branch when a score exceeds it by 2^kRefBand, guide T13) and is set from
+  //    the first block's maximum; p = exp2(s - m); VALU row sums.
+  auto softmax = [&](auto safec, f32x16& acc, int key0, bool first_blk, bf16x8& pa, bf16x8& pb) {
+    constexpr bool SAFE = decltype(safec)::value;
+    if (key0 + 32 > N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
+    }
+    float p[16];
+    if constexpr (!SAFE) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r]);
+    } else {
+      const float mx = max16(acc);
+      if (__any(first_blk || mx > m_run + kRefBand)) {
+        const float mxp = pair_max(mx);  // the query's maximum over this block's 32 keys
+        const bool move = first_blk || mxp > m_run + kRefBand;
+        const float m_new = move ? mxp : m_run;  // identical in both lanes of a query
+        const float alpha = first_blk ? 1.f : __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        l_half *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          oacc[0][r] *= alpha;
+          oacc[1][r] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r] - m_run);
+      l_half += ((((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) +
+                 (((p[8] + p[9]) + (p[10] + p[11])) + ((p[12] + p[13]) + (p[14] + p[15]))));
+    }
+    pa = pack8f(p);
+    pb = pack8f(p + 8);
+    if constexpr (!SAFE) {
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pa, lacc, 0, 0, 0);
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc, 0, 0, 0);
+    }
+  };
+
+  // Software pipeline over 64-key tiles (halves a, b).  Fragments are read one phase before their
+  // MFMAs; sched_barriers pin the reads where they are issued (left alone, the scheduler sinks each
+  // read next to its MFMA behind an lgkmcnt(0)):
+  //   QK(a) [V(a) reads] | K(b) reads, softmax(a) | PV(a) | QK(b) [V(b) reads] | softmax(b) |
+  //   vmcnt(0) + barrier: tile kt+1 landed, every wave's reads of this tile retired |
+  //   DMA tile kt+2 into this buffer, K(a) reads of tile kt+1 | PV(b) (registers only)
   const int nkt = (N + 63) / 64;
-  load_tile(0, smem0);
+  const bool active = q0w < N;  // wave-uniform: a wave whose queries are all past N only stages K/V
   unsigned long long t_vm = 0, t_bar = 0;
   const unsigned long long t_begin = VS_CLK();
-  auto iter = [&](int kt, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    const char* cur = BUF ? smem1 : smem0;
-    char* nxt = BUF ? smem0 : smem1;
-#ifdef VS_STAMP
-    const unsigned long long c0 = VS_CLK();
+  auto pass = [&](auto safec) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      oacc[0][r] = 0.f;
+      oacc[1][r] = 0.f;
+      zero16[r] = 0.f;
+    }
+    lacc = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run = 0.f;
+    l_half = 0.f;
+    load_tile(0, smem0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long c1 = VS_CLK();
     __syncthreads();
-    t_vm += c1 - c0;
-    t_bar += VS_CLK() - c1;
+    if (nkt > 1) load_tile(1, smem1);
+    KFrag ka = kread(smem0, 0);
+    auto iter = [&](int kt, auto bufc) {
+      constexpr int BUF = decltype(bufc)::value;
+      char* cur = BUF ? smem1 : smem0;
+      const char* nxt = BUF ? smem0 : smem1;
+      bf16x8 b0, b1;
+      if (active) {
+        f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka.k[0], qf[0], zero16, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const VFrag va = vread(cur, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 1; s < 4; ++s) sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka.k[s], qf[s], sa, 0, 0, 0);
+        const KFrag kb = kread(cur, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 a0, a1;
+        softmax(safec, sa, kt * 64, kt == 0, a0, a1);
+        pv(va, a0, a1);
+        f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const VFrag vb = vread(cur, 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+        softmax(safec, sb, kt * 64 + 32, false, b0, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nkt) {
+#ifdef VS_STAMP
+          const unsigned long long c0 = VS_CLK();
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const unsigned long long c1 = VS_CLK();
+          __syncthreads();
+          t_vm += c1 - c0;
+          t_bar += VS_CLK() - c1;
 #else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt landed
-    __syncthreads();                                  // ... and every other wave's
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt+1 landed
+          __syncthreads();                                  // ... every wave's; all reads of `cur` retired
 #endif
-    const bool more = kt + 1 < nkt;
-    if (more) load_tile(kt + 1, nxt);
-    f32x16 sa = qk(cur, 0);
-    bf16x8 a0, a1, b0, b1;
-    float d0, d1;
-    softmax(sa, kt * 64, a0, a1, d0);
-    pv(cur, 0, a0, a1);
-    f32x16 sb = qk(cur, 1);
-    softmax(sb, kt * 64 + 32, b0, b1, d1);
-    pv(cur, 1, b0, b1);
+          if (kt + 2 < nkt) load_tile(kt + 2, cur);
+          ka = kread(nxt, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        pv(vb, b0, b1);
+      } else if (kt + 1 < nkt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 2 < nkt) load_tile(kt + 2, cur);
+      }
+    };
+    for (int kt = 0; kt < nkt; kt += 2) {
+      iter(kt, IC<0>{});
+      if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+    }
   };
-  for (int kt = 0; kt < nkt; kt += 2) {
-    iter(kt, IC<0>{});
-    if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+
+  pass(IC<0>{});
+  // Row sum of this lane's query (lane & 31): row (q >> 4) of lacc in lane (q & 15).
+  float l;
+  {
+    const int q = lane & 31, src = (q & 15) << 2;
+    // asm: hipcc folds "q < 16 ? bpermute(x0) : bpermute(x1)" into bpermute(q < 16 ? x0 : x1),
+    // evaluating the select in the SOURCE lane (always x0 there) — wrong for queries 16..31.
+    float l0, l1;
+    asm volatile(
+        "ds_bpermute_b32 %0, %2, %3\n\t"
+        "ds_bpermute_b32 %1, %2, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(l0), "=&v"(l1)
+        : "v"(src), "v"(lacc[0]), "v"(lacc[1])
+        : "memory");
+    l = q < 16 ? l0 : l1;
+  }
+  // Fast-pass validity: the row sum of every real query within [2^-60, 2^60] (false for NaN/inf).
+  const bool bad = active && qi < N && !(l >= 0x1p-60f && l <= 0x1p60f);
+  __syncthreads();  // every wave is done with the last K/V tile; redo_flag = 0 is visible
+  if (__any(bad) && lane == 0) redo_flag = 1;
+  __syncthreads();
+  if (redo_flag) {  // workgroup-uniform: the whole workgroup streams K/V again, safe softmax
+    pass(IC<1>{});
+    l = pair_sum(l_half);
+    __syncthreads();
   }
 
   // Epilogue: O^T accumulators -> normalised bf16 rows staged through LDS (wave-private 4 KB,
   // XOR-swizzled 16-B chunks), then written as whole 128-B rows (8 lanes per row).
-  const float l = pair_sum(l_half);
   const float inv = 1.f / l;
-  __syncthreads();  // every wave is done with the last K/V tile
   char* so = (wid < 2 ? smem0 : smem1) + (wid & 1) * 4096;
   const int oq = lane & 31;
 #pragma unroll

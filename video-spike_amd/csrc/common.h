@@ -154,6 +154,21 @@ __device__ __forceinline__ void glds16_asm(const void* src, void* dst) {
       : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
       : "memory");
 }
+// The same with a wave-uniform 64-bit SGPR base and a 32-bit per-lane byte offset (saddr form:
+// one VGPR per stream instead of a 64-bit address pair).
+__device__ __forceinline__ void glds16_asm_so(const void* sbase, uint32_t voff, void* dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(VS_LDS void*)dst;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
+}
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 4, 0, 0);
 }
