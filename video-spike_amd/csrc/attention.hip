@@ -717,18 +717,18 @@ __device__ __forceinline__ int swz_rt(int r) {
 }
 __device__ __forceinline__ int off_rtswz(int r, int c) { return r * 128 + (((c >> 3) ^ swz_rt(r)) << 4) + (c & 7) * 2; }
 
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                                    const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                    const float* __restrict__ nlse2,
-                                                                    const float* __restrict__ ndel,
-                                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N,
-                                                                    int H, int Npad, float scale) {
-  constexpr int QT = 64 * 128;            // one 64-query x 64-dh bf16 image
-  constexpr int STG = 2 * QT + 512;       // Q, dO, nlse2[64], ndel[64]
-  __shared__ __attribute__((aligned(16))) char stg0[STG];  // two objects: see attn_fwd_bf16_kernel
-  __shared__ __attribute__((aligned(16))) char stg1[STG];
+constexpr int kBwdQT = 64 * 128;           // one 64-row x 64-dh bf16 image
+constexpr int kBwdStage = 2 * kBwdQT + 512;  // dK/dV stage: Q, dO, nlse2[64], ndel[64]; dQ stage: K, V
+
+__device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char* __restrict__ stg1, int blk,
+                                                   const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                   const bf16_t* __restrict__ dout, int64_t lddo,
+                                                   const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                                   bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                                   float scale) {
+  constexpr int QT = kBwdQT;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), kb = blk % nb128;
+  const int nb128 = (N + 127) / 128, kb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
@@ -904,17 +904,15 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16_kernel(const bf16_t
 // P is the forward's P).  S^T = K Q^T and dP^T = V dO^T put the QUERY on the lane; their chains
 // start from per-lane splats of nlse2 and ndel, so p = exp2(acc) and dS^T = p * acc, which is
 // directly the B operand of dQ^T += K^T dS^T (K^T via ds_read_tr16_b64).  No atomics.
-__global__ __launch_bounds__(256, 3) void attn_bwd_dq_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                                  const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                  const float* __restrict__ nlse2,
-                                                                  const float* __restrict__ ndel,
-                                                                  bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
-                                                                  int Npad, float scale) {
+__device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* __restrict__ kv1, int blk,
+                                                 const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                 const bf16_t* __restrict__ dout, int64_t lddo,
+                                                 const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                                 bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                                 float scale) {
   constexpr int TILE = 64 * 128;
-  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE];  // two objects: see attn_fwd_bf16_kernel
-  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
-  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int nb128 = (N + 127) / 128, qb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
   const bf16_t* Qp = qkv + row0 * ldq + h * 64;
@@ -1044,6 +1042,28 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_bf16_kernel(const bf16_t* 
   }
 }
 
+// ------------------------------------------------------------------ backward: one launch
+// The dK/dV and dQ passes run as ONE grid: blocks [0, nblk) are dK/dV workgroups, [nblk, 2 nblk)
+// dQ workgroups, sharing the same two LDS stages.  Each pass alone puts 2496 waves on 3072 wave
+// slots (B = 16, N = 1568, H = 3), so a third of the SIMDs carry 3 waves and the rest 2 and the
+// launch lasts as long as the 3-wave SIMDs; one grid of both lets the dispatcher backfill slots
+// freed by the (longer, dispatched first) dK/dV workgroups with dQ workgroups.
+__global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                               const bf16_t* __restrict__ dout, int64_t lddo,
+                                                               const float* __restrict__ nlse2,
+                                                               const float* __restrict__ ndel,
+                                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
+                                                               int Npad, float scale, int nblk) {
+  __shared__ __attribute__((aligned(16))) char st0[kBwdStage];  // two objects: see attn_fwd_bf16_kernel
+  __shared__ __attribute__((aligned(16))) char st1[kBwdStage];
+  const int id = blockIdx.x;
+  if (id < nblk)
+    attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
+  else
+    attn_bwd_dq_body(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
+                     scale);
+}
+
 }  // namespace vs
 
 using namespace vs;
@@ -1110,12 +1130,9 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-    hipLaunchKernelGGL(attn_bwd_dkdv_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+    hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                        (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                       scale);
-    hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
-                       (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                       scale);
+                       scale, (int)grid.x);
   } else if (dtype == VS_F32) {
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,
                        (const float*)dout, ld_do, delta, rows, (int)N, (int)H);
