@@ -103,6 +103,35 @@ def test_gemm_epilogues(dtype):
     assert rel(rb, (x.double() @ w.double().t()) * (res.to(dtype).double() > 0)) < 1e-5
 
 
+@pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("shape", [(20000, 576, 192), (25088, 768, 192), (3001, 192, 128)])
+def test_gemm_panel_path_many_items(bkc, shape):
+    """Large K <= 192 products: the GELU forward (per-tile path) and the GELU' dX product, which runs
+    on the persistent row-panel kernel (K <= 192, N % 64 == 0) at sizes where each workgroup
+    walks several (panel, chunk) items and crosses panels; GELU and GELU' epilogues, ragged M."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=11).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=12, scale=0.1).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=13).to(DEV)
+    ref = x.float() @ w.float().t() + bias
+    a = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    if bkc:
+        ops.linear(x, w, a, bias=bias, epilogue=L.EPI_GELU, aux_out=pre, ld_aux_out=N)
+        assert rel(pre.float(), ref) < 8e-3
+        assert rel(a.float(), torch.nn.functional.gelu(ref)) < 8e-3
+    else:  # dX form: B(k, n) = wt[k, n] (n-contiguous), GELU' epilogue against the saved pre
+        wt = w.t().contiguous()
+        pre.copy_(ref.to(torch.bfloat16))
+        g = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, wt, g, M=M, N=N, K=K, a_kcontig=True, b_kcontig=False, lda=K, ldb=N, ldc=N,
+                 epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=N)
+        xp = pre.float().requires_grad_()
+        gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        assert rel(g.float(), (x.float() @ w.float().t()) * gg) < 1.5e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("ws", [None, False])       # split-K partials + reduce launch, or f32 atomics
 @pytest.mark.parametrize("shape", [(64, 192, 25088), (192, 768, 25088), (104, 40, 5000)])

@@ -646,6 +646,133 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_ring_kernel(const bf16_t* __
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16 row-panel kernel for K <= 192 (the ViT block's K = D projections and dX products:
+// qkv, proj, fc1 + GELU, do, da * GELU').  These shapes are HBM-bound on the activations they
+// write (M = 25,088 tokens x N = 192..768 columns); the per-tile kernels above re-read the A panel
+// once per 64-column tile (12x for fc1) and pay one load latency per tile.  Here a persistent
+// workgroup owns a contiguous range of (128-row panel, 64-column chunk) items, panel-major:
+//   * A: each wave keeps its 32 rows x K of the panel in registers as MFMA fragments (loaded from
+//     global once per panel, 48 VGPRs at K = 192) — A is read from HBM about once;
+//   * W: the 64 x K chunk of the weight (L2-resident) is register-staged: its global loads for
+//     chunk i+1 are in flight while chunk i computes, then written into one LDS image between two
+//     barriers (guide T14);
+//   * epilogue: each wave stages its 32 x 64 f32 tile in a wave-private LDS image and writes it
+//     in the NEXT item's iteration (after the next chunk's loads are issued), whole 8-column
+//     groups per lane with 16-B accesses (bias, GELU, GELU', residual fused as elsewhere).
+// Grid = min(items, 2 workgroups x 256 CUs): one round, every CU busy, 2 workgroups per CU
+// overlap one's epilogue stores with the other's MFMAs.
+// ----------------------------------------------------------------------------------------------
+template <int KT, bool BKC, uint32_t EF>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_panel_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                 const bf16_t* __restrict__ B, int64_t ldb,
+                                                                 int64_t items, EpiParams e) {
+  using OB = OperandBf16<64, BKC>;
+  constexpr int KS = 2 * KT;           // 32-deep MFMA k-steps
+  constexpr int LDT = 64 + 4;          // staging row stride (floats)
+  __shared__ __attribute__((aligned(16))) char wimg[KT * OB::BYTES];
+  __shared__ __attribute__((aligned(16))) float stage[4][32 * LDT];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t chunks = e.N / 64;
+  const int64_t G = gridDim.x;
+  const int64_t it0 = (int64_t)blockIdx.x * items / G, it1 = ((int64_t)blockIdx.x + 1) * items / G;
+  if (it0 >= it1) return;
+  VS_GMARK(0);
+#ifdef VS_STAMP
+  if ((threadIdx.x & 63) == 0 && blockIdx.x * 4 + (threadIdx.x >> 6) < 8192)
+    g_gstamp[8 * (blockIdx.x * 4 + (threadIdx.x >> 6)) + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  bf16x8 af[2][KS];
+  auto load_a = [&](int64_t panel) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int64_t r = panel * 128 + wid * 32 + i * 16 + (lane & 15);
+      r = r < e.M ? r : e.M - 1;  // rows past M: finite data, never stored
+      const bf16_t* p = A + r * lda + 8 * (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) af[i][ks] = *(const bf16x8*)(p + 32 * ks);
+    }
+  };
+  uint4 wreg[KT][OB::CHUNKS];
+  auto load_w = [&](int64_t chunk) {
+#pragma unroll
+    for (int t = 0; t < KT; ++t) OB::load(wreg[t], B, ldb, chunk * 64, e.N, t * 64, KT * 64, tid);
+  };
+  float* st = stage[wid];
+  auto stage_acc = [&](const f32x4 (&acc)[2][4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(i * 16 + (lane >> 4) * 4 + r) * LDT + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
+  };
+  // epilogue of a staged item: lane -> rows (lane >> 3) + 8p, 8-column group lane & 7
+  auto epilogue = [&](int64_t item) {
+    const int64_t m0 = (item / chunks) * 128 + wid * 32, n = (item % chunks) * 64 + (lane & 7) * 8;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rr = p * 8 + (lane >> 3);
+      const int64_t m = m0 + rr;
+      if (m < e.M) {
+        const float* src = st + rr * LDT + (lane & 7) * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_eight<EF>(e, m, n, v, false);
+      }
+    }
+  };
+
+  int64_t panel = it0 / chunks;
+  load_a(panel);
+  load_w(it0 % chunks);
+  for (int64_t it = it0; it < it1; ++it) {
+    __syncthreads();  // every wave is done reading the W image of the previous item
+#pragma unroll
+    for (int t = 0; t < KT; ++t) OB::store(wimg + t * OB::BYTES, wreg[t], tid);
+    __syncthreads();  // W image of item `it` complete
+    if (it == it0) VS_GMARK(1);
+    if (it + 1 < it1) load_w((it + 1) % chunks);  // in flight under this item's MFMAs
+    if (it > it0) epilogue(it - 1);              // previous item's staged tile (wave-private)
+    if (it / chunks != panel) {
+      panel = it / chunks;
+      load_a(panel);
+    }
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = OB::frag(wimg + (ks >> 1) * OB::BYTES, j * 16, ks & 1, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    stage_acc(acc);
+    if (it == it0) VS_GMARK(2);
+  }
+  VS_GMARK(3);
+  epilogue(it1 - 1);
+  VS_GMARK(4);
+#ifdef VS_STAMP
+  if ((threadIdx.x & 63) == 0) {
+    const int w_ = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w_ < 8192) {
+      g_gstamp[8 * w_ + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      g_gstamp[8 * w_ + 6] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+#endif
+}
+
+// ----------------------------------------------------------------------------------------------
 // f32 kernel (exact: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
 // ----------------------------------------------------------------------------------------------
 template <bool KC>
@@ -809,6 +936,17 @@ static void launch_bf16_ring_ef(const vs_gemm_desc* d, unsigned nblk, const Grid
     hipLaunchKernelGGL((gemm_bf16_ring_kernel<BM, BN, false, false, EF>), dim3(nblk), dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
 }
 
+template <int KT, uint32_t EF>
+static void launch_bf16_panel_ef(const vs_gemm_desc* d, unsigned grid, int64_t items, const EpiParams& e,
+                                 hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, true, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, false, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
+}
+
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
 #define VS_EPI_SWITCH(F, CALL)                                                             \
   switch (F) {                                                                             \
@@ -830,6 +968,13 @@ static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, 
 template <int BM, int BN>
 static void launch_bf16_ring(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
 #define L_(EF) launch_bf16_ring_ef<BM, BN, EF>(d, nblk, g, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
+}
+
+template <int KT>
+static void launch_bf16_panel(const vs_gemm_desc* d, unsigned grid, int64_t items, const EpiParams& e, hipStream_t s) {
+#define L_(EF) launch_bf16_panel_ef<KT, EF>(d, grid, items, e, s)
   VS_EPI_SWITCH(e.flags, L_)
 #undef L_
 }
@@ -954,6 +1099,24 @@ static int getenv_flag2(const char* name) {
   return cached;
 }
 
+static int getenv_flag4(const char* name) {
+  static int cached = -1;
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached;
+}
+
+static int getenv_flag3(const char* name) {
+  static int cached = -1;
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached;
+}
+
 static bool vec_ok(const vs_gemm_desc* d) {
   const uint32_t f = d->epilogue;
   const int ovec = d->out_dtype == VS_BF16 ? 8 : 4;
@@ -1030,6 +1193,29 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     VS_REQUIRE(nblk < (1ll << 31), "vs_gemm: grid too large");
     // whole-K-in-LDS path: K = 64..192 in 64-steps, no split, no fused row sums, 128 x 64 tiles
     // (72 KB of LDS at K = 192: 2 blocks per CU)
+    // row-panel path (K <= 192, whole 64-column chunks, no split / row sums / atomics).  Measured
+    // (scripts/microbench.py, ViT-Tiny shapes): faster than the per-tile kernels only for the
+    // GELU' product (da: 43.2 -> 38.7 us); the per-tile whole-K kernel wins on the others (its
+    // 2352 short tiles balance better than 512 persistent workgroups that each load a 48-KB A panel
+    // before their first MFMA).  VSPIKE_PANEL=1 forces it for every eligible shape.
+    const bool panel = ((f & VS_EPI_GELU_BWD) || getenv_flag4("VSPIKE_PANEL")) && d->a_kcontig && g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 &&
+                       d->N % 64 == 0 && !d->a_rowsum && !(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM)) && e.vec_ok &&
+                       getenv_flag3("VSPIKE_NO_PANEL") == 0;
+    if (panel) {
+      const int64_t items = cdiv(d->M, 128) * (d->N / 64);
+      static int gcap = -1;  // A/B knob: VSPIKE_PANEL_GRID overrides the 512-workgroup cap
+      if (gcap < 0) {
+        const char* v = getenv("VSPIKE_PANEL_GRID");
+        gcap = v && atoi(v) > 0 ? atoi(v) : 512;
+      }
+      const unsigned grid = (unsigned)(items < gcap ? items : gcap);
+      const int KT = (int)(d->K / 64);
+      if (KT == 1) launch_bf16_panel<1>(d, grid, items, e, s);
+      else if (KT == 2) launch_bf16_panel<2>(d, grid, items, e, s);
+      else launch_bf16_panel<3>(d, grid, items, e, s);
+      VS_LAUNCH_CHECK();
+      return VS_OK;
+    }
     const bool fullk = g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 && BM == 128 && !d->a_rowsum &&
                        !(f & VS_EPI_ATOMIC) && getenv_flag("VSPIKE_NO_FULLK") == 0;
     if (fullk) {

@@ -8,6 +8,8 @@
 //   x' = y + a W2^T + b2 [f32]
 // Backward mirrors it with the weight gradients accumulated in f32 (split-K atomics for the
 // token-reduction dW products, whose K is B*N = 25,088 rows at the bench shape).
+#include <mutex>
+
 #include "common.h"
 
 namespace vs {
@@ -26,6 +28,49 @@ static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t 
   d.epilogue = epi;
   d.alpha = 1.0f;
   return d;
+}
+
+// Side stream for the weight-gradient products of the backward.  The four dW = dY^T X GEMMs of a
+// block (reductions over all B*N tokens, HBM-bound, each ~10-30 us of mostly load/drain latency
+// at the bench shape) depend only on tensors the main stream has already produced, and nothing on
+// the main stream reads their results within the block, so they run on a second stream: dW2 beside
+// da, dW1 beside dh2 + LN2', dWp beside do + the attention backward, dWqkv beside dh1 + LN1'.
+// The side stream forks from the caller's stream at each product's input (an event) and joins it
+// at the end of the block, so the caller's stream order is unchanged for everything downstream
+// (optimizer, gradient exchange) and buffers reused across blocks are never read late.
+// One non-blocking side stream and a small event ring per device, created on first use.
+struct SideStreams {
+  std::mutex mu;
+  hipStream_t side[64] = {};
+  hipEvent_t ev[64][8] = {};
+};
+static SideStreams g_side;
+
+static int side_for(hipStream_t main, hipStream_t* side, hipEvent_t** ev) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  VS_REQUIRE(dev >= 0 && dev < 64, "vs_vit_layer_bwd: device id out of range");
+  std::lock_guard<std::mutex> lk(g_side.mu);
+  if (!g_side.side[dev]) {
+    e = hipStreamCreateWithFlags(&g_side.side[dev], hipStreamNonBlocking);
+    if (e != hipSuccess) return (int)e;
+    for (auto& x : g_side.ev[dev]) {
+      e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+      if (e != hipSuccess) return (int)e;
+    }
+  }
+  (void)main;
+  *side = g_side.side[dev];
+  *ev = g_side.ev[dev];
+  return VS_OK;
+}
+
+// `to` waits for everything enqueued so far on `from` (event slot k)
+static int stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
+  hipError_t e = hipEventRecord(ev, from);
+  if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
+  return (int)e;
 }
 
 static int check_layer(const vs_vit_layer* L) {
@@ -88,14 +133,19 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
   const void* gx = lp ? G->dx_out_lp : (const void*)G->dx_out;  // dx' as a GEMM operand
   const void* gy = lp ? G->dy_lp : (const void*)G->dy;
+  hipStream_t ms = (hipStream_t)stream, ss = nullptr;
+  hipEvent_t* ev = nullptr;
+  VS_CALL(side_for(ms, &ss, &ev));
+  void* side = (void*)ss;
 
   // ---- MLP: x' = y + a W2^T + b2
-  {  // dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
+  VS_CALL(stream_wait(ms, ss, ev[0]));  // dx' (and the block's saved activations) ready
+  {  // [side] dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc2;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(vs_gemm(&g, side));
   }
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
     vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
@@ -103,12 +153,13 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     g.ld_aux_in = F;
     VS_CALL(vs_gemm(&g, stream));
   }
-  {  // dW1[F,D] += da^T h2;  db1 += colsum(da) fused
+  VS_CALL(stream_wait(ms, ss, ev[1]));  // da ready
+  {  // [side] dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc1;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(vs_gemm(&g, side));
   }
   {  // dh2 = da W1
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
@@ -118,12 +169,13 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
                            lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
   // ---- attention: y = x + o Wp^T + bp
-  {  // dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
+  VS_CALL(stream_wait(ms, ss, ev[2]));  // dy ready
+  {  // [side] dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_proj;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(vs_gemm(&g, side));
   }
   {  // do = dy Wp
     vs_gemm_desc g = gdesc(T, T, true, false, M, D, D, gy, D, L->w_proj, D, G->d_o, D, 0);
@@ -131,14 +183,15 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   VS_CALL(vs_attn_bwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, G->d_o, D, L->lse, G->d_qkv,
                       3 * D, G->attn_ws, L->attn_scale, stream));
-  {  // dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
+  VS_CALL(stream_wait(ms, ss, ev[3]));  // dqkv ready
+  {  // [side] dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_qkv;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(vs_gemm(&g, side));
     // the k bias is not a parameter (fixed 0 in the reference, mv:233): its slot stays exactly 0
-    hipError_t e = hipMemsetAsync(G->b_qkv + D, 0, D * sizeof(float), (hipStream_t)stream);
+    hipError_t e = hipMemsetAsync(G->b_qkv + D, 0, D * sizeof(float), ss);
     if (e != hipSuccess) return (int)e;
   }
   {  // dh1 = dqkv Wqkv
@@ -148,5 +201,6 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   // dx = dy + LN1'(dh1)
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
                            lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
+  VS_CALL(stream_wait(ss, ms, ev[4]));  // join: the block's weight gradients are complete
   return VS_OK;
 }
