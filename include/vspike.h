@@ -226,7 +226,17 @@ typedef struct vs_vit_layer_grad {
   void* ln_ws;          /* vs_layernorm_bwd_workspace_bytes(M, D) */
   void* gemm_ws;        /* split-K partials of the weight-gradient GEMMs (optional) */
   int64_t gemm_ws_bytes;
+  int32_t flags;        /* VS_BWD_* bits */
+  int32_t reserved;
 } vs_vit_layer_grad;
+
+/* The weight-gradient GEMMs of a block run on a per-device side stream.  Default: the caller's
+ * stream joins it before vs_vit_layer_bwd returns.  VS_BWD_DEFER_JOIN: no join; instead the NEXT
+ * vs_vit_layer_bwd call on this device (the next block of the same backward, reusing the same
+ * scratch buffers) waits on each product right before overwriting its input.  The weight
+ * gradients of a deferred block are therefore complete in the caller's stream order only after
+ * the next call; the last block of a backward must not set the flag. */
+#define VS_BWD_DEFER_JOIN 0x1
 
 int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
 int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);

@@ -1000,8 +1000,9 @@ static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
 }
 
 // C[m, n] += bias[n] + sum_s part[s][m][n]: one float4 of C per thread, splits summed in order
-// (deterministic, unlike the atomic path), 8 loads in flight per thread (a plain loop over the
-// runtime split count issued them one at a time: 12 us for 25 MB of partials).
+// (deterministic, unlike the atomic path).  Up to 32 splits' loads are issued before the first add
+// (the partials of a dW product are 7-13 MB spread over only ~150 workgroups: with 8 loads in
+// flight per thread the launch was latency-bound at ~20 us, 3 round trips for 22 splits).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ part, int splits, int64_t M,
                                                           int64_t N, float* __restrict__ c, int64_t ldc,
                                                           const float* __restrict__ bias, int vec) {
@@ -1012,19 +1013,15 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
     if (e4 >= MN) return;
     const int64_t m = e4 / N, n = e4 % N;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int sp = 0;
-    for (; sp + 8 <= splits; sp += 8) {
-      float4 v[8];
+    for (int sp0 = 0; sp0 < splits; sp0 += 32) {
+      float4 v[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (sp + u) * MN + e4);
+      for (int u = 0; u < 32; ++u)
+        v[u] = sp0 + u < splits ? *(const float4*)(part + (sp0 + u) * MN + e4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 32; ++u) {
         acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
       }
-    }
-    for (; sp < splits; ++sp) {
-      const float4 v = *(const float4*)(part + sp * MN + e4);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     if (bias) {
       const float4 bb = *(const float4*)(bias + n);
@@ -1038,17 +1035,57 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
     if (i >= MN) return;
     const int64_t m = i / N, n = i % N;
     float acc = 0.f;
-    int sp = 0;
-    for (; sp + 8 <= splits; sp += 8) {
-      float v[8];
+    for (int sp0 = 0; sp0 < splits; sp0 += 32) {
+      float v[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(sp + u) * MN + i];
+      for (int u = 0; u < 32; ++u) v[u] = sp0 + u < splits ? part[(sp0 + u) * MN + i] : 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < 32; ++u) acc += v[u];
     }
-    for (; sp < splits; ++sp) acc += part[sp * MN + i];
     if (bias) acc += bias[n];
     c[m * ldc + n] += acc;
+  }
+}
+
+// Few outputs, many splits (the head's z = x W_enc^T: 16 x 64 outputs, 512 splits of K): the
+// per-output kernel above runs as ONE workgroup whose threads each walk 512 splits (24 us).  Here a
+// workgroup owns one float4 of C, its 256 threads stride over the splits, and a fixed-shape LDS tree
+// adds the 256 partial sums (deterministic: the order depends only on `splits`).
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_wide(const float* __restrict__ part, int splits, int64_t M,
+                                                               int64_t N, float* __restrict__ c, int64_t ldc,
+                                                               const float* __restrict__ bias) {
+  __shared__ float4 red[256];
+  const int64_t MN = M * N;
+  const int64_t e4 = (int64_t)blockIdx.x * 4;
+  const int t = threadIdx.x;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sp = t; sp < splits; sp += 256) {
+    const float4 v = *(const float4*)(part + (int64_t)sp * MN + e4);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  red[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      const float4 o = red[t + w];
+      float4 a = red[t];
+      a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+      red[t] = a;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    float4 s = red[0];
+    const int64_t m = e4 / N, n = e4 % N;
+    if (bias) {
+      const float4 bb = *(const float4*)(bias + n);
+      s.x += bb.x; s.y += bb.y; s.z += bb.z; s.w += bb.w;
+    }
+    float4* dst = (float4*)(c + m * ldc + n);
+    float4 o = *dst;
+    o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+    *dst = o;
   }
 }
 
@@ -1259,7 +1296,11 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   if (e.part) {
     const int vec = d->N % 4 == 0 && d->ldc % 4 == 0 && aligned16(d->c) && (!(f & VS_EPI_BIAS) || aligned16(d->bias));
     const int64_t n_items = vec ? d->M * d->N / 4 : d->M * d->N;
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, s, e.part, g.splits,
+    if (vec && g.splits >= 64 && n_items <= 4096)
+      hipLaunchKernelGGL(gemm_splitk_reduce_wide, dim3((unsigned)n_items), dim3(256), 0, s, e.part, g.splits, d->M,
+                         d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr);
+    else
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, s, e.part, g.splits,
                        d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
   }
   VS_LAUNCH_CHECK();

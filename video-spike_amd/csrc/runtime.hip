@@ -48,7 +48,7 @@ ScopedTimer::~ScopedTimer() {
 
 }  // namespace vs
 
-extern "C" int vs_version(void) { return 1; }
+extern "C" int vs_version(void) { return 2; }  // 2: vs_vit_layer_grad.flags
 
 extern "C" int vs_struct_size(int which) {
   switch (which) {

@@ -39,14 +39,21 @@ static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t 
 // at the end of the block, so the caller's stream order is unchanged for everything downstream
 // (optimizer, gradient exchange) and buffers reused across blocks are never read late.
 // One non-blocking side stream and a small event ring per device, created on first use.
+// Deferred join (VS_BWD_DEFER_JOIN): instead of joining at the end of the block, the side stream
+// records one event per weight-gradient product (two parity sets, alternating per call) and the
+// NEXT block's main stream waits on each just before it overwrites the buffer that product reads
+// (d_a, dy, d_qkv, the dx ping-pong buffer) — by then the product has long finished, so the
+// cross-queue wait no longer stalls the main stream (~20 us per block at the bench shape).
 struct SideStreams {
   std::mutex mu;
   hipStream_t side[64] = {};
-  hipEvent_t ev[64][8] = {};
+  hipEvent_t ev[64][16] = {};
+  int parity[64] = {};
+  bool pending[64] = {};
 };
 static SideStreams g_side;
 
-static int side_for(hipStream_t main, hipStream_t* side, hipEvent_t** ev) {
+static int side_for(hipStream_t main, hipStream_t* side, hipEvent_t** ev, int* dev_out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return (int)e;
@@ -63,6 +70,7 @@ static int side_for(hipStream_t main, hipStream_t* side, hipEvent_t** ev) {
   (void)main;
   *side = g_side.side[dev];
   *ev = g_side.ev[dev];
+  *dev_out = dev;
   return VS_OK;
 }
 
@@ -135,8 +143,15 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   const void* gy = lp ? G->dy_lp : (const void*)G->dy;
   hipStream_t ms = (hipStream_t)stream, ss = nullptr;
   hipEvent_t* ev = nullptr;
-  VS_CALL(side_for(ms, &ss, &ev));
+  int dev = 0;
+  VS_CALL(side_for(ms, &ss, &ev, &dev));
   void* side = (void*)ss;
+  const int par = g_side.parity[dev];
+  const bool pend = g_side.pending[dev];
+  hipEvent_t* pe = ev + 8 + 4 * (1 - par);  // the previous block's products (deferred join)
+  hipEvent_t* ce = ev + 8 + 4 * par;        // this block's
+  auto wait_prev = [&](int k) -> int { return pend ? (int)hipStreamWaitEvent(ms, pe[k], 0) : 0; };
+  auto mark = [&](int k) -> int { return (int)hipEventRecord(ce[k], ss); };
 
   // ---- MLP: x' = y + a W2^T + b2
   VS_CALL(stream_wait(ms, ss, ev[0]));  // dx' (and the block's saved activations) ready
@@ -146,7 +161,9 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, side));
+    VS_CALL(mark(0));
   }
+  VS_CALL(wait_prev(1));  // d_a is read by the previous block's dW1
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
     vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
     g.aux_in = L->a_pre;
@@ -160,12 +177,14 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, side));
+    VS_CALL(mark(1));
   }
   {  // dh2 = da W1
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
     VS_CALL(vs_gemm(&g, stream));
   }
   // dy = dx' + LN2'(dh2)
+  VS_CALL(wait_prev(2));  // dy / dy_lp are read by the previous block's dWp
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
                            lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
   // ---- attention: y = x + o Wp^T + bp
@@ -176,11 +195,13 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
     VS_CALL(vs_gemm(&g, side));
+    VS_CALL(mark(2));
   }
   {  // do = dy Wp
     vs_gemm_desc g = gdesc(T, T, true, false, M, D, D, gy, D, L->w_proj, D, G->d_o, D, 0);
     VS_CALL(vs_gemm(&g, stream));
   }
+  VS_CALL(wait_prev(3));  // d_qkv is read by the previous block's dWqkv
   VS_CALL(vs_attn_bwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, G->d_o, D, L->lse, G->d_qkv,
                       3 * D, G->attn_ws, L->attn_scale, stream));
   VS_CALL(stream_wait(ms, ss, ev[3]));  // dqkv ready
@@ -193,14 +214,22 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     // the k bias is not a parameter (fixed 0 in the reference, mv:233): its slot stays exactly 0
     hipError_t e = hipMemsetAsync(G->b_qkv + D, 0, D * sizeof(float), ss);
     if (e != hipSuccess) return (int)e;
+    VS_CALL(mark(3));
   }
   {  // dh1 = dqkv Wqkv
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
     VS_CALL(vs_gemm(&g, stream));
   }
   // dx = dy + LN1'(dh1)
+  VS_CALL(wait_prev(0));  // dx_in is the previous block's dx_out, read by its dW2
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
                            lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
-  VS_CALL(stream_wait(ss, ms, ev[4]));  // join: the block's weight gradients are complete
+  if (G->flags & VS_BWD_DEFER_JOIN) {
+    g_side.pending[dev] = true;  // the next block waits on ce[] before each overwrite
+    g_side.parity[dev] = 1 - par;
+  } else {
+    VS_CALL(stream_wait(ss, ms, ev[4]));  // join: the block's weight gradients are complete
+    g_side.pending[dev] = false;
+  }
   return VS_OK;
 }

@@ -16,6 +16,7 @@ from .build import LIB_PATH
 VS_F32, VS_BF16, VS_U8 = 0, 1, 2
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
+BWD_DEFER_JOIN = 0x1
 TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM = 0, 1, 2
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
@@ -54,7 +55,8 @@ class VitLayerGrad(ctypes.Structure):
                 ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
                 ("dx_out", c_p), ("dx_out_lp", c_p), ("dx_in", c_p), ("dx_in_lp", c_p),
                 ("d_a", c_p), ("d_h", c_p), ("dy", c_p), ("dy_lp", c_p), ("d_o", c_p), ("d_qkv", c_p),
-                ("attn_ws", c_p), ("ln_ws", c_p), ("gemm_ws", c_p), ("gemm_ws_bytes", c_i64)]
+                ("attn_ws", c_p), ("ln_ws", c_p), ("gemm_ws", c_p), ("gemm_ws_bytes", c_i64),
+                ("flags", c_i32), ("reserved", c_i32)]
 
 
 # every entry point of include/vspike.h: name -> (restype, argtypes)

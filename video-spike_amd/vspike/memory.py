@@ -20,7 +20,7 @@ class Arena:
         n = 1
         for s in shape:
             n *= int(s)
-        nbytes = n * torch.tensor([], dtype=dtype).element_size()
+        nbytes = n * dtype.itemsize
         self._plan[name] = (self._bytes, tuple(int(s) for s in shape), dtype)
         self._bytes += (nbytes + _ALIGN - 1) // _ALIGN * _ALIGN
 
@@ -35,6 +35,5 @@ class Arena:
             n = 1
             for s in shape:
                 n *= s
-            es = torch.tensor([], dtype=dtype).element_size()
-            out[name] = self._buf[off:off + n * es].view(dtype).view(shape)
+            out[name] = self._buf[off:off + n * dtype.itemsize].view(dtype).view(shape)
         return out

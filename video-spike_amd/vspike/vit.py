@@ -17,6 +17,8 @@ f32 master weights and f32 weight gradients.
 from __future__ import annotations
 
 import math
+import os
+import weakref
 from typing import Optional
 
 import torch
@@ -27,8 +29,18 @@ from . import ops
 from .layout import BackboneCfg, VitLayout
 from .memory import Arena
 
+# Deferred side-stream joins (VS_BWD_DEFER_JOIN) remove the ~20 us cross-queue stall per block but
+# let the dW products spill into the next block's kernels; measured slower on the bench step
+# (6.80 vs 6.53 ms, same box, 3 A/B pairs), so they are opt-in: VSPIKE_DEFER=1.
+_DEFER = os.environ.get("VSPIKE_DEFER") == "1"
+
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+class _FwdState(dict):
+    """What one forward saves for its backward; the cached buffers it names stay reserved while
+    an instance is alive (VideoMAE._fwd_buffers holds a weak reference)."""
 
 
 def _cfg_get(config, key, default=None):
@@ -170,6 +182,8 @@ class VideoMAE(nn.Module):
         st = super().__getstate__() if hasattr(super(), "__getstate__") else self.__dict__.copy()
         st = dict(st)
         st["_pos_cache"] = {}
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache"):
+            st.pop(k, None)
         st["grad_sink"] = None
         return st
 
@@ -202,66 +216,93 @@ class VideoMAE(nn.Module):
             setattr(s, k, act[pfx + k].data_ptr())
         return s
 
-    def _lowp(self, flat):
-        if self.compute_dtype == torch.float32:
-            return flat
-        out = torch.empty(flat.shape, dtype=self.compute_dtype, device=flat.device)
-        ops.cast(flat, out)
-        return out
+    def _caches(self):
+        d = self.__dict__
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache"):
+            if k not in d:
+                d[k] = {}
+        return d["_fwd_cache"], d["_bwd_cache"], d["_gs_cache"]
 
-    def _run_forward(self, pixels, save_encoder: bool):
+    def _fwd_buffers(self, B: int, dev, save_encoder: bool):
+        """Activation arena, low-precision weight shadows and the 12 executor structs of one
+        (batch, device, save_encoder) shape: planned once, then reused every step while no live
+        autograd state holds them (a second forward before the first one's backward builds a
+        private set).  Rebuilding per step cost ~1.2 ms of host time with the GPU idle."""
+        fwd_cache, _, _ = self._caches()
+        enc32, head32 = self.enc_flat.detach(), self.head_flat.detach()
+        sig = (enc32.data_ptr(), head32.data_ptr())
+        key = (B, str(dev), save_encoder, self.compute_dtype)
+        ent = fwd_cache.get(key)
+        if ent is not None and ent["sig"] == sig and (ent["owner"] is None or ent["owner"]() is None):
+            return ent
         cfg, dt = self.backbone, self.compute_dtype
-        B = pixels.shape[0]
         N, D, Lyr = cfg.num_tokens, cfg.hidden_size, cfg.num_hidden_layers
         M = B * N
-        dev = pixels.device
-        enc32, head32 = self.enc_flat.detach(), self.head_flat.detach()
-        enc_lp, head_lp = self._lowp(enc32), self._lowp(head32)
-        le, lh = self.layout.enc, self.layout.head
-
+        lp = dt != torch.float32
         ar = Arena()
         ar.add("cols", (M, cfg.patch_dim), dt)
         ar.add("x0", (M, D), torch.float32)
-        n_sets = Lyr if save_encoder else 1
-        for j in range(n_sets):
+        for j in range(Lyr if save_encoder else 1):
             self._plan_layer(ar, f"L{j}.", B)
         for j in range(Lyr if save_encoder else 2):
             ar.add(f"X{j}", (M, D), torch.float32)
-        if dt != torch.float32:
+        if lp:
             ar.add("x_lp", (B, N * D), dt)
+            ar.add("enc_lp", (enc32.numel(),), dt)
+            ar.add("head_lp", (head32.numel(),), dt)
         ar.add("z", (B, self.layout.enc_out), torch.float32)
-        ar.add("r", (B, self.layout.out_dim), torch.float32)
+        # split-K over the N*D = 301,056-long reduction; partials summed in order (deterministic)
+        hws = ops.splitk_workspace_bytes(dt, B, self.layout.enc_out, N * D)
+        if hws:
+            ar.add("head_ws", (hws // 4 + 4,), torch.float32)
         act = ar.allocate(dev)
-
-        ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
-        ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
-                   epilogue=L.EPI_POS, pos=self._pos_table(dev), pos_rows=N)
+        enc_lp = act["enc_lp"] if lp else enc32
+        head_lp = act["head_lp"] if lp else head32
         x = act["x0"]
         structs = []
         for i in range(Lyr):
             j = i if save_encoder else 0
             x_out = act[f"X{i}"] if save_encoder else act[f"X{i % 2}"]
-            s = self._layer_struct(i, B, x, x_out, act, f"L{j}.", enc_lp, enc32)
-            ops.vit_layer_fwd(s)
-            structs.append(s)
+            structs.append(self._layer_struct(i, B, x, x_out, act, f"L{j}.", enc_lp, enc32))
             x = x_out
-        x_flat = x.view(B, N * D)
+        new = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_final": x,
+               "x_flat_lp": act["x_lp"] if lp else x.view(B, N * D), "head_ws": act.get("head_ws"),
+               "sig": sig, "owner": None}
+        if ent is None or ent["sig"] != sig:
+            fwd_cache[key] = new
+        return new
+
+    def _run_forward(self, pixels, save_encoder: bool):
+        cfg, dt = self.backbone, self.compute_dtype
+        B = pixels.shape[0]
+        N, D = cfg.num_tokens, cfg.hidden_size
+        dev = pixels.device
+        enc32, head32 = self.enc_flat.detach(), self.head_flat.detach()
+        le, lh = self.layout.enc, self.layout.head
+        ent = self._fwd_buffers(B, dev, save_encoder)
+        act, enc_lp, head_lp = ent["act"], ent["enc_lp"], ent["head_lp"]
         if dt != torch.float32:
-            ops.cast(x_flat, act["x_lp"])
-            x_flat_lp = act["x_lp"]
-        else:
-            x_flat_lp = x_flat
-        z, r = act["z"], act["r"]
+            ops.cast(enc32, enc_lp)
+            ops.cast(head32, head_lp)
+
+        ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
+        ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
+                   epilogue=L.EPI_POS, pos=self._pos_table(dev), pos_rows=N)
+        for s in ent["structs"]:
+            ops.vit_layer_fwd(s)
+        x_flat_lp = ent["x_flat_lp"]
+        if dt != torch.float32:
+            ops.cast(ent["x_final"].view(B, N * D), x_flat_lp)
+        z = act["z"]
+        r = torch.empty(B, self.layout.out_dim, dtype=torch.float32, device=dev)   # handed to the caller
         z.zero_()
-        # split-K over the N*D = 301,056-long reduction; partials summed in order (deterministic)
-        hws = ops.splitk_workspace_bytes(x_flat_lp.dtype, B, self.layout.enc_out, N * D)
-        hws = torch.empty(hws // 4 + 4, dtype=torch.float32, device=dev) if hws else None
         ops.gemm(x_flat_lp, lh.view(head_lp, "enc_w"), z, M=B, N=self.layout.enc_out, K=N * D, a_kcontig=True,
                  b_kcontig=True, lda=N * D, ldb=N * D, ldc=self.layout.enc_out, epilogue=L.EPI_ATOMIC | L.EPI_BIAS,
-                 bias=lh.view(head32, "enc_b"), workspace=hws)
+                 bias=lh.view(head32, "enc_b"), workspace=ent["head_ws"])
         ops.linear(z, lh.view(head32, "dec_w"), r, bias=lh.view(head32, "dec_b"))
-        state = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_flat_lp": x_flat_lp,
-                 "x_final": x, "B": B}
+        state = _FwdState(act=act, structs=ent["structs"], enc_lp=enc_lp, head_lp=head_lp, x_flat_lp=x_flat_lp,
+                          x_final=ent["x_final"], B=B)
+        ent["owner"] = weakref.ref(state)
         return r.view(B, 100, -1), state
 
     # ---------------------------------------------------------------------------------------
@@ -288,63 +329,93 @@ class VideoMAE(nn.Module):
         head32 = self.head_flat.detach()
         dr = d_logrates.reshape(B, lay.out_dim).to(torch.float32).contiguous()
 
+        lp = dt != torch.float32
+        _, bwd_cache, gs_cache = self._caches()
+        bkey = (B, str(dev), dt)
+        g = bwd_cache.get(bkey)
+        if g is None:
+            # backward scratch: only used inside this call, in stream order, so one set per shape
+            ar = Arena()
+            for k, shape, d in (("d_a", (M, F), dt), ("d_h", (M, D), torch.float32), ("dy", (M, D), torch.float32),
+                                ("d_o", (M, D), dt), ("d_qkv", (M, 3 * D), dt), ("dxA", (M, D), torch.float32),
+                                ("dxB", (M, D), torch.float32), ("dz", (B, lay.enc_out), torch.float32)):
+                ar.add(k, shape, d)
+            if lp:
+                for k in ("dy_lp", "dxA_lp", "dxB_lp"):
+                    ar.add(k, (M, D), dt)
+                ar.add("dz_lp", (B, lay.enc_out), dt)
+            ar.add("attn_ws", (ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64,), torch.float32)
+            ar.add("ln_ws", (ops.layernorm_bwd_workspace_bytes(B * N, D) // 4 + 64,), torch.float32)
+            gws = max(ops.splitk_workspace_bytes(dt, m, n, M) for m, n in ((D, F), (F, D), (D, D), (3 * D, D)))
+            ar.add("gemm_ws", (gws // 4 + 64,), torch.float32)
+            g = ar.allocate(dev)
+            bwd_cache[bkey] = g
+
         g_head = self._grad_buffer(self.head_flat) if want_head else None
         Gh = lambda n: lh.view(g_head, n)  # noqa: E731
         z = act["z"]
-        dz = torch.zeros(B, lay.enc_out, dtype=torch.float32, device=dev)
+        dz = g["dz"]
+        dz.zero_()
         ops.linear_dx(dr, lh.view(head32, "dec_w"), dz, accumulate=True)     # K = 100*neurons: split-K
-        if dt != torch.float32:
-            dz_lp = torch.empty(B, lay.enc_out, dtype=dt, device=dev)
+        if lp:
+            dz_lp = g["dz_lp"]
             ops.cast(dz, dz_lp)
         else:
             dz_lp = dz
         if want_head:
             ops.linear_dw(dr, z, Gh("dec_w"), db=Gh("dec_b"))
             ops.colsum(dz, Gh("enc_b"))                      # dz is B x 64: the lp copy may be rounded
-            ops.linear_dw(dz_lp, st["x_flat_lp"], Gh("enc_w"))
+            # reduction over the batch only (K = B): plain stores into the freshly zeroed buffer —
+            # f32 atomics on its 19 M elements cost 64 us
+            ops.linear_dw(dz_lp, st["x_flat_lp"], Gh("enc_w"), accumulate=False)
             self._ready(self.head_flat, 0, self.head_flat.numel())
         if not want_enc:
             return None, g_head
 
         g_enc = self._grad_buffer(self.enc_flat)
         Ge = lambda n: le.view(g_enc, n)  # noqa: E731
-        ar = Arena()
-        for k, shape, d in (("d_a", (M, F), dt), ("d_h", (M, D), torch.float32), ("dy", (M, D), torch.float32),
-                            ("d_o", (M, D), dt), ("d_qkv", (M, 3 * D), dt), ("dxA", (M, D), torch.float32),
-                            ("dxB", (M, D), torch.float32)):
-            ar.add(k, shape, d)
-        if dt != torch.float32:
-            for k in ("dy_lp", "dxA_lp", "dxB_lp"):
-                ar.add(k, (M, D), dt)
-        ar.add("attn_ws", (ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64,), torch.float32)
-        ar.add("ln_ws", (ops.layernorm_bwd_workspace_bytes(B * N, D) // 4 + 64,), torch.float32)
-        gws = max(ops.splitk_workspace_bytes(dt, m, n, M) for m, n in ((D, F), (F, D), (D, D), (3 * D, D)))
-        ar.add("gemm_ws", (gws // 4 + 64,), torch.float32)
-        g = ar.allocate(dev)
-        lp = dt != torch.float32
 
         dx, dx_lp = g["dxA"], (g["dxA_lp"] if lp else None)
         ops.linear_dx(dz_lp, lh.view(st["head_lp"], "enc_w"), dx.view(B, N * D))
         if lp:
             ops.cast(dx, dx_lp)
+        gkey = (bkey, g_enc.data_ptr())
+        grads = gs_cache.get(gkey)
+        if grads is None:
+            if len(gs_cache) > 8:
+                gs_cache.clear()
+            grads = {}
+            cur = "dxA"
+            for i in reversed(range(Lyr)):
+                gs = L.VitLayerGrad()
+                for k in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "w_qkv", "b_qkv", "w_proj", "b_proj", "w_fc1",
+                          "b_fc1", "w_fc2", "b_fc2"):
+                    setattr(gs, k, Ge(f"{i}.{k}").data_ptr())
+                nxt = "dxB" if cur == "dxA" else "dxA"
+                gs.dx_out, gs.dx_out_lp = g[cur].data_ptr(), (g[cur + "_lp"].data_ptr() if lp else None)
+                gs.dx_in, gs.dx_in_lp = g[nxt].data_ptr(), (g[nxt + "_lp"].data_ptr() if lp else None)
+                gs.d_a, gs.d_h, gs.dy = g["d_a"].data_ptr(), g["d_h"].data_ptr(), g["dy"].data_ptr()
+                gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
+                gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
+                gs.ln_ws = g["ln_ws"].data_ptr()
+                gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
+                # opt-in: every block but the last one defers its side-stream join to the next
+                gs.flags = L.BWD_DEFER_JOIN if i > 0 and _DEFER else 0
+                grads[i] = (gs, nxt)
+                cur = nxt
+            gs_cache[gkey] = grads
+        prev = None
         for i in reversed(range(Lyr)):
-            s = st["structs"][i]
-            gs = L.VitLayerGrad()
-            for k in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "w_qkv", "b_qkv", "w_proj", "b_proj", "w_fc1", "b_fc1",
-                      "w_fc2", "b_fc2"):
-                setattr(gs, k, Ge(f"{i}.{k}").data_ptr())
-            nxt = "dxB" if dx is g["dxA"] else "dxA"
-            gs.dx_out, gs.dx_out_lp = dx.data_ptr(), L.ptr(dx_lp)
-            gs.dx_in, gs.dx_in_lp = g[nxt].data_ptr(), (g[nxt + "_lp"].data_ptr() if lp else None)
-            gs.d_a, gs.d_h, gs.dy = g["d_a"].data_ptr(), g["d_h"].data_ptr(), g["dy"].data_ptr()
-            gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
-            gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
-            gs.ln_ws = g["ln_ws"].data_ptr()
-            gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
-            ops.vit_layer_bwd(s, gs)
+            gs, nxt = grads[i]
+            ops.vit_layer_bwd(st["structs"][i], gs)
             dx, dx_lp = g[nxt], (g[nxt + "_lp"] if lp else None)
-            lo, hi = lay.layer_ranges[i]
-            self._ready(self.enc_flat, lo, hi)
+            # block i's weight gradients are complete in stream order once block i-1 (which waits
+            # on them) is enqueued; the last block joins before returning
+            if prev is not None:
+                self._ready(self.enc_flat, *lay.layer_ranges[prev])
+            prev = i
+        if prev is not None:
+            self._ready(self.enc_flat, *lay.layer_ranges[prev])
         # patch embedding: dW = dx0^T cols, db = colsum(dx0); the position table is fixed
         if lp:
             ops.linear_dw(dx_lp, act["cols"], Ge("patch_w"))
@@ -360,8 +431,10 @@ class _VideoMAEFn(torch.autograd.Function):
     def forward(ctx, pixels, enc_flat, head_flat, mod):
         want_enc = bool(ctx.needs_input_grad[1])
         out, st = mod._run_forward(pixels, save_encoder=want_enc)
-        ctx.mod, ctx.st = mod, st
         ctx.want = (want_enc, bool(ctx.needs_input_grad[2]))
+        # keep the saved state (and with it the reservation of the cached buffers) only when a
+        # backward can follow
+        ctx.mod, ctx.st = mod, (st if any(ctx.want) else None)
         return out
 
     @staticmethod
