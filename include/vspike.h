@@ -182,6 +182,24 @@ int vs_adamw(int64_t n, float* param, const float* grad, float* exp_avg, float* 
              void* param_lp, const float* hyper, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Evaluation metrics of one session (src/trainer/base.py:180-198 -> src/utils/utils.py:122-175
+ * -> src/utils/metric_utils.py:36-102): gt, pred are the concatenated eval tensors
+ * [trials, T, N] f32 BEFORE base.py's transposes; log_input = 1 applies base.py:186's exp.
+ * bps over neurons 0..n_eval-1 (the reference indexes neurons with its trial loop: pass
+ * n_eval = trials, after checking trials <= N), NaN spikes masked, zero rates -> 1e-9;
+ * rsquared = sklearn r2_score per trial (neurons = samples, bins = outputs, force_finite),
+ * NaN-ignoring mean over trials; mse / mae over all elements (want_r2 computes these three).
+ * out (device f64[8]): [0] bps, [1] rsquared, [2] #NaN rates among kept spikes, [3] #negative
+ * rates, [4] #NaN/inf rsquared inputs, [5] mse, [6] mae.  The reference raises on [2], [3]
+ * (AssertionError) and [4] (ValueError); the host layer does the same.  Optional device outputs:
+ * bps_per_neuron f64[n_eval], r2_per_trial f64[trials].  f64 accumulation, fixed order.
+ * ------------------------------------------------------------------------------------------ */
+size_t vs_spike_metrics_workspace_bytes(int64_t trials, int64_t T, int64_t N);
+int vs_spike_metrics(int64_t trials, int64_t T, int64_t N, const float* gt, const float* pred,
+                     int32_t log_input, int64_t n_eval, int32_t want_r2, double* out,
+                     double* bps_per_neuron, double* r2_per_trial, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * One pre-LN ViT block (mv:419-445) as a native executor: LN1 -> QKV GEMM -> attention ->
  * out-proj + residual -> LN2 -> fc1+GELU -> fc2 + residual, and its backward.  All tensors are
  * caller-owned; `dtype` is the activation/weight element type (residual stream, LN statistics,

@@ -250,9 +250,57 @@ def gen_configs():
     print("configs", list(res))
 
 
+def _ref_metric_functions():
+    """The reference's own eval-metric functions, taken from its source files by name
+    (metric_utils.py imports `torcheval` at module level and utils.py imports plugins whose
+    dependencies are absent, so the modules cannot be imported whole).  `logger` is undefined in
+    the reference module (metric_utils.py:70); a stand-in logger is supplied."""
+    import ast
+    import logging
+    from scipy.special import gammaln
+    from sklearn.metrics import accuracy_score, r2_score as r2_score_sklearn
+    ns = {"np": np, "torch": torch, "gammaln": gammaln, "r2_score_sklearn": r2_score_sklearn,
+          "accuracy_score": accuracy_score, "logger": logging.getLogger("reference")}
+    for path, names in ((os.path.join(REF_SRC, "utils", "metric_utils.py"), ("neg_log_likelihood", "bits_per_spike")),
+                        (os.path.join(REF_SRC, "utils", "utils.py"), ("metrics_list",))):
+        tree = ast.parse(open(path).read(), filename=path)
+        defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+        assert len(defs) == len(names), (path, names)
+        exec(compile(ast.Module(body=defs, type_ignores=[]), path, "exec"), ns)
+    return ns
+
+
+def gen_metrics():
+    from oracle import metrics_ref
+    ns = _ref_metric_functions()
+    fx = {}
+    for name, (R, T, N, seed, metrics, log_input) in metrics_ref.METRIC_CASES.items():
+        gt, pred = metrics_ref.metric_case(name)
+        g = torch.from_numpy(gt)
+        p = torch.exp(torch.from_numpy(pred)) if log_input else torch.from_numpy(pred)   # base.py:186
+        res = ns["metrics_list"](gt=g.transpose(-1, 0), pred=p.transpose(-1, 0), metrics=list(metrics),
+                                 device="cpu")                                         # base.py:190-195
+        for k, v in res.items():
+            fx[f"{name}.{k}"] = np.float64(v)
+        if "bps" in metrics:
+            _g, _p = g.numpy(), p.numpy()
+            fx[f"{name}.bps_per_neuron"] = np.array(
+                [ns["bits_per_spike"](_p[:, :, [i]], _g[:, :, [i]]) for i in range(min(R, N))], dtype=np.float64)
+        print("metrics", name, {k: float(v) for k, v in res.items()})
+    # the reference's IndexError when trials > N (utils.py:128-129)
+    gt, pred = metrics_ref.metric_case("m_wide")
+    try:
+        ns["metrics_list"](gt=torch.from_numpy(gt).transpose(-1, 0),
+                           pred=torch.exp(torch.from_numpy(pred)).transpose(-1, 0), metrics=["bps"], device="cpu")
+        fx["m_wide.bps_error"] = np.array("none")
+    except IndexError as e:
+        fx["m_wide.bps_error"] = np.array("IndexError: " + str(e))
+    np.savez_compressed(os.path.join(OUT, "metrics.npz"), **fx)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "k0"]
+    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "k0", "metrics"]
     for w in which:
         globals()["gen_" + w]()

@@ -183,3 +183,67 @@ def test_state_dict_roundtrip_and_pickle(tmp_path):
         a, b = m(px), m2(px)
     # not bit-exact: the split-K head GEMM sums with f32 atomics in arrival order
     assert (a - b).abs().max().item() <= 1e-5 * a.abs().max().item()
+
+
+def test_cached_buffers_two_forwards_before_backward():
+    """The forward arena is cached per shape and reserved while its autograd state is alive: two
+    forwards before one backward (and a no-grad forward in between) must give the gradients of
+    separate passes."""
+    from vspike import poisson_nll_mean
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n)
+    px1 = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    px2 = px1.flip(0).contiguous() * 0.5
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    grads = []
+    for x in (px1, px2):
+        m.zero_grad(set_to_none=True)
+        poisson_nll_mean(m(x), y).backward()
+        grads.append((m.enc_flat.grad.clone(), m.head_flat.grad.clone()))
+    m.zero_grad(set_to_none=True)
+    o1 = m(px1)
+    o2 = m(px2)
+    with torch.no_grad():
+        o3 = m(px1)
+    assert torch.equal(o3, o1.detach())
+    (poisson_nll_mean(o1, y) + poisson_nll_mean(o2, y)).backward()
+    for k, g in enumerate((m.enc_flat.grad, m.head_flat.grad)):
+        want = grads[0][k] + grads[1][k]
+        assert float((g - want).norm() / want.norm()) < 1e-5
+    # outputs handed to the caller are not overwritten by later steps
+    o1c = o1.detach().clone()
+    m(px2)
+    assert torch.equal(o1.detach(), o1c)
+
+
+def test_eval_epoch_matches_reference_eval_flow():
+    """Trainer.eval_epoch (src/trainer/base.py:161-206) on two sessions: eval_loss and the
+    per-session bps / rsquared means against the CPU restatement of the same flow."""
+    from vspike.trainer import Trainer
+    from oracle import metrics_ref
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n)
+    batches = []
+    for eid in ("s0", "s1"):
+        for k in range(3):                       # 6 trials per session <= 16 neurons
+            px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV) * (1 + 0.1 * k)
+            y = torch.from_numpy(prng.spike_targets(40 + k + (10 if eid == "s1" else 0), (B, 100, n))).to(DEV)
+            batches.append({"video": px, "ap": y, "eid": [eid] * B})
+    res = Trainer(m, None).eval_epoch(batches)
+    losses, sess = [], {}
+    with torch.no_grad():
+        for b in batches:
+            out = m(b["video"])
+            x, t = out.double(), b["ap"].double()
+            losses.append(float((torch.exp(x) - t * x).mean()))
+            s = sess.setdefault(b["eid"][0], ([], []))
+            s[0].append(b["ap"].cpu().numpy())
+            s[1].append(out.cpu().numpy())
+    want = {"bps": [], "rsquared": []}
+    for gts, outs in sess.values():
+        r = metrics_ref.eval_session(np.concatenate(gts), np.concatenate(outs), dtype=np.float64)
+        for k in want:
+            want[k].append(r[k])
+    assert abs(res["eval_loss"] - round(float(np.mean(losses)), 5)) <= 1e-5
+    for k in want:
+        assert abs(res[f"eval_{k}"] - round(float(np.mean(want[k])), 5)) <= 1e-5, (k, res, want)

@@ -115,3 +115,28 @@ def test_k0_preprocess_oracle_matches_reference_processor(golden):
         u8 = fx["u8"][j].astype(np.float64)
         assert np.array_equal(((u8 * (1 / 255)).astype(np.float32) - m0) / s0, pv[0, f, 0])
     cpu_ref.compare_summary("pixel_values", pv, fx, rtol=1e-7, atol=0.0)
+
+
+def test_metrics_restatement_matches_reference(golden):
+    """oracle.metrics_ref (numpy, f32 like the reference) against outputs of the reference's own
+    metrics_list / bits_per_spike (utils.py:122-167, metric_utils.py:36-102) on the same inputs."""
+    import warnings
+    from oracle import metrics_ref as M
+    fx = golden("metrics.npz")
+    warnings.simplefilter("ignore", RuntimeWarning)
+    for name, (R, T, N, seed, mets, log_input) in M.METRIC_CASES.items():
+        gt, pred = M.metric_case(name)
+        if log_input:
+            res = M.eval_session(gt, pred, mets)
+        else:
+            res = M.metrics_list(np.swapaxes(gt, -1, 0), np.swapaxes(pred, -1, 0), mets)
+        for k in mets:
+            assert abs(res[k] - float(fx[f"{name}.{k}"])) <= 1e-7, (name, k, res[k], fx[f"{name}.{k}"])
+        if "bps" in mets:
+            rates = np.exp(pred) if log_input else pred
+            want = fx[f"{name}.bps_per_neuron"].copy()
+            want[np.isinf(want)] = np.nan                   # utils.py:130-131
+            got = M.per_neuron_bps(gt, rates.astype(np.float32))
+            assert np.array_equal(np.isnan(got), np.isnan(want))
+            np.testing.assert_allclose(got[~np.isnan(got)], want[~np.isnan(want)], rtol=1e-5, atol=2e-6)
+    assert str(fx["m_wide.bps_error"]).startswith("IndexError")

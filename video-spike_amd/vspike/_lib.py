@@ -86,6 +86,9 @@ PROTOTYPES = {
     "vs_poisson_nll": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_f32, c_p, c_p]),
     "vs_poisson_nll_bwd": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_adamw": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "vs_spike_metrics_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "vs_spike_metrics": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_i32, c_i64, c_i32, c_p, c_p, c_p, c_p,
+                                        c_p]),
     "vs_vit_layer_fwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), c_p]),
     "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
     "vs_timing_enable": (ctypes.c_int, [ctypes.c_int]),

@@ -15,6 +15,7 @@ import torch
 
 from .dp import GradExchange
 from .loss import poisson_nll_mean
+from .metrics import eval_session
 from .optim import FusedAdamW
 
 
@@ -64,3 +65,28 @@ class Trainer:
         self.model.train()
         losses = [self.step(model_inputs(self.config, b) if self.config else b["video"], b["ap"]) for b in batches]
         return float(torch.stack(losses).mean().item()) if losses else float("nan")
+
+    @torch.no_grad()
+    def eval_epoch(self, batches: Iterable, metrics=("bps", "rsquared")) -> dict:
+        """`src/trainer/base.py:161-206`: per batch the loss; per session (`batch['eid'][0]`) the
+        concatenated gt / log-rate outputs go through `metrics_list` (exp fused, on the device).
+        Returns the reference's `eval_res` dict: eval_loss and eval_<metric>, each rounded to 5
+        places as base.py:198,203 does."""
+        import numpy as np
+        self.model.eval()
+        losses, sessions = [], {}
+        for b in batches:
+            out = self.model(model_inputs(self.config, b) if self.config else b["video"])
+            losses.append(self.criterion(out, b["ap"]))
+            eid = b["eid"][0] if "eid" in b else "session"
+            s = sessions.setdefault(eid, {"gt": [], "preds": []})
+            s["gt"].append(b["ap"])
+            s["preds"].append(out)
+        res = {k: [] for k in metrics}
+        for s in sessions.values():
+            r = eval_session(torch.cat(s["gt"], 0), torch.cat(s["preds"], 0), metrics)
+            for k, v in r.items():
+                res[k].append(v)
+        out = {"eval_loss": round(float(np.mean([float(x) for x in losses])), 5) if losses else float("nan")}
+        out.update({f"eval_{k}": round(float(np.mean(v)), 5) for k, v in res.items()})
+        return out

@@ -409,8 +409,14 @@ class VideoMAE(nn.Module):
             gs, nxt = grads[i]
             ops.vit_layer_bwd(st["structs"][i], gs)
             dx, dx_lp = g[nxt], (g[nxt + "_lp"] if lp else None)
-            # block i's weight gradients are complete in stream order once block i-1 (which waits
-            # on them) is enqueued; the last block joins before returning
+            # joined block: its weight gradients are complete in stream order now; deferred block:
+            # once block i-1 (which waits on them) is enqueued.  The last block always joins.
+            if not gs.flags:
+                if prev is not None:
+                    self._ready(self.enc_flat, *lay.layer_ranges[prev])
+                self._ready(self.enc_flat, *lay.layer_ranges[i])
+                prev = None
+                continue
             if prev is not None:
                 self._ready(self.enc_flat, *lay.layer_ranges[prev])
             prev = i
