@@ -260,6 +260,24 @@ int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
 int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Trial shards (host side of the input path; replaces the per-trial webdataset tars of
+ * src/prepare_data.py:210-235 read by src/loader/base.py:21-41).  Fixed-size records: raw uint8
+ * frames (T, C, H, W) + f32 spike counts (ap_rows, ap_cols) + a 64-byte "<eid>_<trial>" key.
+ * vs_shard_read gathers records into caller (pinned) host buffers with `threads` parallel
+ * positional reads.  Host-only: no stream, no device memory.  Errors: VS_EINVAL / NULL with
+ * vs_shard_last_error() set.
+ * ------------------------------------------------------------------------------------------ */
+int vs_shard_write(const char* path, int64_t n, int64_t T, int64_t C, int64_t H, int64_t W,
+                   int64_t ap_rows, int64_t ap_cols, const uint8_t* video, const float* ap,
+                   const char* keys /* n x 64 bytes */);
+void* vs_shard_open(const char* path, int64_t* info /* [8]: n, T, C, H, W, ap_rows, ap_cols, record_bytes */);
+int vs_shard_key(void* shard, int64_t i, char* buf, int32_t n /* >= 65 */);
+int vs_shard_read(void* shard, const int64_t* idx, int64_t n, uint8_t* video_dst, float* ap_dst,
+                  int32_t threads);
+void vs_shard_close(void* shard);
+const char* vs_shard_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
  * Kernel timing (bench instrumentation).  When enabled, the executor brackets every launch of
  * the tracked kernels with hipEvents on the launch stream.  vs_timing_collect() synchronises on
  * the recorded events and returns per-kernel launch count and total milliseconds.

@@ -81,3 +81,34 @@ def test_videomae_forward_accepts_raw_video():
         a = m(torch.from_numpy(video).to(DEV))
         b = m(torch.from_numpy(pv).to(DEV))
     assert torch.equal(a, b)
+
+
+def test_shard_loader_to_device_feeds_the_plugin(tmp_path):
+    """Shard -> pinned host -> async H2D (uint8) -> the VideoMAE plugin's raw-video path: the batch
+    arrives intact and the uint8 frames give exactly the output of the same frames as float32
+    (the reference's loader hands the model `.float()` frames, src/loader/base.py:41)."""
+    from vspike.data import ShardLoader, write_shard
+    from vspike import VideoMAE
+    n, T, H = 4, 20, 64
+    video = (prng.uniform(77, n * T * H * H, "v") * 256).astype(np.uint8).reshape(n, T, 1, H, H)
+    ap = prng.spike_targets(78, (n, 100, 16))
+    p = str(tmp_path / "s.vss")
+    write_shard(p, video, ap, [f"e{i % 2}_{i}" for i in range(n)])
+    cfg = cpu_ref.VIT_SMALL_FIXTURE
+    conf = {"model_class": "VideoMAE", "freeze_encoder": True, "compute_dtype": "fp32",
+            "backbone": {k: getattr(cfg, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                       "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                       "num_attention_heads", "intermediate_size",
+                                                       "layer_norm_eps")},
+            "encoder": {"output_dim": 64}, "decoder": {"output_dim": 1600}}
+    m = VideoMAE(conf).to(DEV)
+    got = 0
+    for b in ShardLoader([p], batch_size=2, shuffle=False, device=DEV):
+        idx = [int(k.split("_")[1]) for k in b["__key__"]]
+        assert b["video"].is_cuda and b["video"].dtype == torch.uint8
+        assert np.array_equal(b["video"].cpu().numpy(), video[idx])
+        assert np.array_equal(b["ap"].cpu().numpy(), ap[idx])
+        with torch.no_grad():
+            assert torch.equal(m(b["video"]), m(b["video"].float()))
+        got += len(idx)
+    assert got == n

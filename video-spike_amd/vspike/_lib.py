@@ -89,6 +89,13 @@ PROTOTYPES = {
     "vs_spike_metrics_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "vs_spike_metrics": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_i32, c_i64, c_i32, c_p, c_p, c_p, c_p,
                                         c_p]),
+    "vs_shard_write": (ctypes.c_int, [ctypes.c_char_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
+                                      ctypes.c_char_p]),
+    "vs_shard_open": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.POINTER(c_i64)]),
+    "vs_shard_key": (ctypes.c_int, [ctypes.c_void_p, c_i64, ctypes.c_char_p, c_i32]),
+    "vs_shard_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(c_i64), c_i64, c_p, c_p, c_i32]),
+    "vs_shard_close": (None, [ctypes.c_void_p]),
+    "vs_shard_last_error": (ctypes.c_char_p, []),
     "vs_vit_layer_fwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), c_p]),
     "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
     "vs_timing_enable": (ctypes.c_int, [ctypes.c_int]),

@@ -43,21 +43,24 @@ def _needs(obj: str, deps) -> bool:
 def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
     hipcc = _hipcc()
-    srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip")))
+    srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip"))) + sorted(glob.glob(os.path.join(SRC_DIR, "*.cpp")))
     headers = sorted(glob.glob(os.path.join(SRC_DIR, "*.h"))) + [os.path.join(INCLUDE, "vspike.h")]
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(BUILD_DIR, os.path.basename(s)[:-4] + ".o")
+        o = os.path.join(BUILD_DIR, os.path.splitext(os.path.basename(s))[0] + ".o")
         objs.append(o)
         if force or _needs(o, [s] + headers):
             todo.append((s, o))
 
     def compile_one(so):
         s, o = so
-        cmd = [hipcc, *_flags(), "-c", s, "-o", o]
+        if s.endswith(".cpp"):     # host-only code (shard reader): plain C++
+            cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-I", INCLUDE, "-c", s, "-o", o]
+        else:
+            cmd = [hipcc, *_flags(), "-c", s, "-o", o]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {os.path.basename(s)}:\n{r.stderr[-6000:]}")
+            raise RuntimeError(f"compile failed for {os.path.basename(s)}:\n{r.stderr[-6000:]}")
         return s
 
     if todo:
@@ -66,7 +69,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
                 if verbose:
                     print(f"[vspike.build] compiled {os.path.basename(s)}", file=sys.stderr)
     if force or todo or _needs(LIB_PATH, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs, "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
