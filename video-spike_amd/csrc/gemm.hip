@@ -999,39 +999,56 @@ static int pick_splits(int64_t tiles, int64_t nk, int want, bool atomic_ok) {
   return s < 1 ? 1 : (int)s;
 }
 
-// C[m, n] += bias[n] + sum_s part[s][m][n]: one float4 of C per thread, splits summed in order
-// (deterministic, unlike the atomic path).  Up to 32 splits' loads are issued before the first add
-// (the partials of a dW product are 7-13 MB spread over only ~150 workgroups: with 8 loads in
-// flight per thread the launch was latency-bound at ~20 us, 3 round trips for 22 splits).
+// C[m, n] += bias[n] + sum_s part[s][m][n].  Vector path: a workgroup owns 64 float4 of C and
+// its 4 waves split the splits (wave w sums s = w, w+4, ...: every load of a wave's share is
+// issued before the first add), then the 4 partial float4 are added in wave order through LDS
+// (deterministic: the order depends only on `splits`).  The dW partials are 7-13 MB spread over
+// ~150 workgroups at one float4 per thread: that version was latency-bound at ~20 us per launch.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ part, int splits, int64_t M,
                                                           int64_t N, float* __restrict__ c, int64_t ldc,
                                                           const float* __restrict__ bias, int vec) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t MN = M * N;
   if (vec) {
-    const int64_t e4 = i * 4;
-    if (e4 >= MN) return;
-    const int64_t m = e4 / N, n = e4 % N;
+    __shared__ float4 red[4][64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int64_t e4 = ((int64_t)blockIdx.x * 64 + l) * 4;
+    const bool live = e4 < MN;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp0 = 0; sp0 < splits; sp0 += 32) {
-      float4 v[32];
+    if (live) {
+      for (int sp0 = w; sp0 < splits; sp0 += 4 * 16) {
+        float4 v[16];
 #pragma unroll
-      for (int u = 0; u < 32; ++u)
-        v[u] = sp0 + u < splits ? *(const float4*)(part + (sp0 + u) * MN + e4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 0; u < 16; ++u) {
+          const int sp = sp0 + 4 * u;
+          v[u] = sp < splits ? *(const float4*)(part + sp * MN + e4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
 #pragma unroll
-      for (int u = 0; u < 32; ++u) {
-        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        for (int u = 0; u < 16; ++u) {
+          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        }
       }
     }
-    if (bias) {
-      const float4 bb = *(const float4*)(bias + n);
-      acc.x += bb.x; acc.y += bb.y; acc.z += bb.z; acc.w += bb.w;
+    red[w][l] = acc;
+    __syncthreads();
+    if (w == 0 && live) {
+      float4 a = red[0][l];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float4 b = red[k][l];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      const int64_t m = e4 / N, n = e4 % N;
+      if (bias) {
+        const float4 bb = *(const float4*)(bias + n);
+        a.x += bb.x; a.y += bb.y; a.z += bb.z; a.w += bb.w;
+      }
+      float4* dst = (float4*)(c + m * ldc + n);
+      float4 o = *dst;
+      o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+      *dst = o;
     }
-    float4* dst = (float4*)(c + m * ldc + n);
-    float4 o = *dst;
-    o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
-    *dst = o;
   } else {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= MN) return;
     const int64_t m = i / N, n = i % N;
     float acc = 0.f;
@@ -1300,7 +1317,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       hipLaunchKernelGGL(gemm_splitk_reduce_wide, dim3((unsigned)n_items), dim3(256), 0, s, e.part, g.splits, d->M,
                          d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr);
     else
-      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, s, e.part, g.splits,
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, vec ? 64 : 256)), dim3(256), 0, s, e.part, g.splits,
                        d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
   }
   VS_LAUNCH_CHECK();

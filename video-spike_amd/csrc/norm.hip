@@ -231,16 +231,28 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
     pg[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     pb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR; row < rows; row += (int64_t)gridDim.x * GPB) {
-    float4 d[VEC], xv[VEC], r[VEC];
+  // rows strided by the grid; the next row's loads are issued before the current row's
+  // reductions (software prefetch: the row loop was load-latency-bound at ~2 waves per SIMD)
+  const int64_t stride = (int64_t)gridDim.x * GPB;
+  int64_t row = (int64_t)blockIdx.x * GPB + threadIdx.x / LPR;
+  float4 d[VEC], xv[VEC], r[VEC];
+  float mu = 0.f, rs = 0.f;
+  auto load_row = [&](int64_t rw, float4* dd, float4* xx, float4* rr, float& m_, float& r_) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const int c = 4 * (gl + LPR * j);
-      d[j] = *(const float4*)(dy + row * lddy + c);
-      xv[j] = *(const float4*)(x + row * ldx + c);
-      r[j] = dres ? *(const float4*)(dres + row * lddres + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      dd[j] = *(const float4*)(dy + rw * lddy + c);
+      xx[j] = *(const float4*)(x + rw * ldx + c);
+      rr[j] = dres ? *(const float4*)(dres + rw * lddres + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float mu = mean[row], rs = rstd[row];
+    m_ = mean[rw];
+    r_ = rstd[rw];
+  };
+  if (row < rows) load_row(row, d, xv, r, mu, rs);
+  for (; row < rows; row += stride) {
+    float4 dn[VEC], xn[VEC], rn[VEC];
+    float mun = 0.f, rsn = 0.f;
+    if (row + stride < rows) load_row(row + stride, dn, xn, rn, mun, rsn);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
@@ -270,6 +282,14 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
       *(float4*)(dx + row * lddx + c) = o;
       if (dx_lp) st4(dx_lp + row * lddx + c, o);
     }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      d[j] = dn[j];
+      xv[j] = xn[j];
+      r[j] = rn[j];
+    }
+    mu = mun;
+    rs = rsn;
   }
   // dgamma/dbeta: reduce the groups of the wave (same gl), then the 4 waves in LDS; one f32
   // atomic per column per block
@@ -335,7 +355,7 @@ __global__ __launch_bounds__(256) void ln_partsum_kernel(const float* __restrict
   }
 }
 
-constexpr int kLnBwdBlocks = 512;  // vectorised backward grid cap (= partial rows in the workspace)
+constexpr int kLnBwdBlocks = 1024;  // vectorised backward grid cap (= partial rows in the workspace)
 
 // cols -> (LPR, VEC) of the vectorised kernels; 0 = none
 static inline int ln_vec_lpr(int64_t cols) {
