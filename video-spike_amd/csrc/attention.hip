@@ -666,8 +666,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 // Per (batch, head, query): nlse2 = -LSE * log2(e) and ndel = -delta (delta = rowsum(dO * O)),
 // stored [B*H][Npad] with Npad = N rounded up to 64 and the padding set to (-inf, 0): the dK/dV
 // kernel DMAs 64-query slices of them straight into LDS and seeds its S / dP accumulators with
-// them, and a padded query then contributes exactly P = 0, dS = 0.  One thread per (row, head),
-// eight 16-B loads of O and of dO.
+// them, and a padded query then contributes exactly P = 0, dS = 0.  Four lanes per (row, head),
+// two 16-B loads of O and of dO each, then a 2-step shuffle (one thread per (row, head) with 16
+// loads in its chain was latency-bound: 14 us for 19 MB).
 __global__ __launch_bounds__(256) void attn_rowprep_kernel(const bf16_t* __restrict__ o, int64_t ldo,
                                                            const bf16_t* __restrict__ dout, int64_t lddo,
                                                            const float* __restrict__ lse, float* __restrict__ nlse2,
@@ -675,19 +676,27 @@ __global__ __launch_bounds__(256) void attn_rowprep_kernel(const bf16_t* __restr
                                                            int Npad) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * 256;
-  if (t < B * N * H) {
-    const int64_t row = t / H;
-    const int h = (int)(t % H);
+  const int64_t pair = t >> 2;          // (row, head)
+  const int q = (int)(t & 3);           // 16-column quarter of the head
+  float acc = 0.f;
+  const bool live = pair < B * N * H;
+  int64_t row = 0;
+  int h = 0;
+  if (live) {
+    row = pair / H;
+    h = (int)(pair % H);
+    const bf16x8* op = (const bf16x8*)(o + row * ldo + h * 64 + q * 16);
+    const bf16x8* dp = (const bf16x8*)(dout + row * lddo + h * 64 + q * 16);
+    const bf16x8 a0 = op[0], a1 = op[1], g0 = dp[0], g1 = dp[1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = fmaf((float)a0[k], (float)g0[k], acc);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = fmaf((float)a1[k], (float)g1[k], acc);
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  if (live && q == 0) {
     const int64_t b = row / N, n = row % N;
-    const bf16x8* op = (const bf16x8*)(o + row * ldo + h * 64);
-    const bf16x8* dp = (const bf16x8*)(dout + row * lddo + h * 64);
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bf16x8 a = op[j], g = dp[j];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc = fmaf((float)a[k], (float)g[k], acc);
-    }
     const int64_t w = (b * H + h) * Npad + n;
     ndel[w] = -acc;
     nlse2[w] = -lse[(b * H + h) * N + n] * kLog2e;
@@ -1127,7 +1136,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     const int64_t npad = attn_npad(N);
     float* nlse2 = (float*)workspace;
     float* ndel = nlse2 + B * H * npad;
-    hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H, 256)), dim3(256), 0, s, (const bf16_t*)o,
+    hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
