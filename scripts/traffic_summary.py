@@ -22,7 +22,7 @@ def main(d, out):
         write = sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])
         kern[name.split("(")[0]] = {"fetch_bytes_x2": 2 * fetch, "write_bytes": write, "traffic_bytes": 2 * fetch + write,
                                     "launches": len(c["FETCH_SIZE"])}
-    groups = {"attn_bwd": ["attn_rowprep_kernel", "attn_bwd_dkdv_bf16_kernel", "attn_bwd_dq_bf16_kernel"],
+    groups = {"attn_bwd": ["attn_rowprep_kernel", "attn_bwd_bf16_kernel", "attn_bwd_dkdv_bf16_kernel", "attn_bwd_dq_bf16_kernel"],
               "attn_fwd": ["attn_fwd_bf16_kernel"]}
     grouped = {}
     for g, parts in groups.items():
