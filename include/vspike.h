@@ -253,8 +253,11 @@ typedef struct vs_vit_layer_grad {
  * vs_vit_layer_bwd call on this device (the next block of the same backward, reusing the same
  * scratch buffers) waits on each product right before overwriting its input.  The weight
  * gradients of a deferred block are therefore complete in the caller's stream order only after
- * the next call; the last block of a backward must not set the flag. */
+ * the next call; the last block of a backward must not set the flag.  VS_BWD_DEFER_LAST: the
+ * caller's stream joins the first three products (dW2, dW1, dWproj) at the end of the block and
+ * defers only dWqkv, which the next call waits on before overwriting d_qkv; same last-block rule. */
 #define VS_BWD_DEFER_JOIN 0x1
+#define VS_BWD_DEFER_LAST 0x2
 
 int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
 int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);

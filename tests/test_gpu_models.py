@@ -247,3 +247,31 @@ def test_eval_epoch_matches_reference_eval_flow():
     assert abs(res["eval_loss"] - round(float(np.mean(losses)), 5)) <= 1e-5
     for k in want:
         assert abs(res[f"eval_{k}"] - round(float(np.mean(want[k])), 5)) <= 1e-5, (k, res, want)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_deferred_side_stream_joins_give_identical_grads(mode):
+    """VS_BWD_DEFER_JOIN / VS_BWD_DEFER_LAST only move where the caller's stream waits on the
+    side-stream weight-gradient products; the products must equal those of a join at every block
+    end over two steps (buffers reused across blocks).  The split-K dW sums are fixed-order, but the
+    fused bias-gradient row sums add f32 atomics in arrival order, so the bar is 1e-5 of the norm
+    (a read of a half-overwritten buffer would be off by O(1))."""
+    import vspike.vit as V
+    from vspike import poisson_nll_mean
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    grads = {}
+    old = V._DEFER
+    try:
+        for m_ in (0, mode):
+            V._DEFER = m_
+            m = _vit_model(cfg, 64, n, dtype="bf16")
+            for _ in range(2):
+                m.enc_flat.grad = None
+                poisson_nll_mean(m(px), y).backward()
+            torch.cuda.synchronize()
+            grads[m_] = m.enc_flat.grad.detach().cpu().clone()
+    finally:
+        V._DEFER = old
+    assert (grads[0] - grads[mode]).norm().item() <= 1e-5 * grads[0].norm().item()

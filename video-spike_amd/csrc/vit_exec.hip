@@ -49,7 +49,7 @@ struct SideStreams {
   hipStream_t side[64] = {};
   hipEvent_t ev[64][16] = {};
   int parity[64] = {};
-  bool pending[64] = {};
+  int pending[64] = {};  // bit k: the previous block's product k is not joined yet
 };
 static SideStreams g_side;
 
@@ -147,10 +147,10 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(side_for(ms, &ss, &ev, &dev));
   void* side = (void*)ss;
   const int par = g_side.parity[dev];
-  const bool pend = g_side.pending[dev];
+  const int pend = g_side.pending[dev];
   hipEvent_t* pe = ev + 8 + 4 * (1 - par);  // the previous block's products (deferred join)
   hipEvent_t* ce = ev + 8 + 4 * par;        // this block's
-  auto wait_prev = [&](int k) -> int { return pend ? (int)hipStreamWaitEvent(ms, pe[k], 0) : 0; };
+  auto wait_prev = [&](int k) -> int { return (pend >> k) & 1 ? (int)hipStreamWaitEvent(ms, pe[k], 0) : 0; };
   auto mark = [&](int k) -> int { return (int)hipEventRecord(ce[k], ss); };
 
   // ---- MLP: x' = y + a W2^T + b2
@@ -225,11 +225,18 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
                            lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
   if (G->flags & VS_BWD_DEFER_JOIN) {
-    g_side.pending[dev] = true;  // the next block waits on ce[] before each overwrite
+    g_side.pending[dev] = 0xF;  // the next block waits on ce[] before each overwrite
+    g_side.parity[dev] = 1 - par;
+  } else if (G->flags & VS_BWD_DEFER_LAST) {
+    // join dW2, dW1, dWp (finished during the attention backward, so this wait does not stall);
+    // only dWqkv, still running beside dh1 + LN1', is joined by the next block before its
+    // attention backward overwrites d_qkv
+    VS_CALL((int)hipStreamWaitEvent(ms, ce[2], 0));
+    g_side.pending[dev] = 0x8;
     g_side.parity[dev] = 1 - par;
   } else {
     VS_CALL(stream_wait(ss, ms, ev[4]));  // join: the block's weight gradients are complete
-    g_side.pending[dev] = false;
+    g_side.pending[dev] = 0;
   }
   return VS_OK;
 }

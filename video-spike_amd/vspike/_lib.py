@@ -17,6 +17,7 @@ VS_F32, VS_BF16, VS_U8 = 0, 1, 2
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 BWD_DEFER_JOIN = 0x1
+BWD_DEFER_LAST = 0x2
 TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM = 0, 1, 2
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,

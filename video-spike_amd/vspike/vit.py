@@ -29,10 +29,13 @@ from . import ops
 from .layout import BackboneCfg, VitLayout
 from .memory import Arena
 
-# Deferred side-stream joins (VS_BWD_DEFER_JOIN) remove the ~20 us cross-queue stall per block but
-# let the dW products spill into the next block's kernels; measured slower on the bench step
-# (6.80 vs 6.53 ms, same box, 3 A/B pairs), so they are opt-in: VSPIKE_DEFER=1.
-_DEFER = os.environ.get("VSPIKE_DEFER") == "1"
+# Side-stream joins of the block backward.  A join at every block end costs a ~24 us cross-queue
+# stall per block (the main stream waits on the dWqkv product, which the side stream finishes last).
+# Deferring every product (VS_BWD_DEFER_JOIN, VSPIKE_DEFER=1) removes the stall but lets the dW
+# products spill into the next block's kernels (6.61 ms/step); deferring only dWqkv
+# (VS_BWD_DEFER_LAST, the default) keeps the other three joined: 6.33 vs 6.41 ms/step for
+# join-every-block (VSPIKE_DEFER=0), same box, 3 round-robin runs of 30 steps (scripts/ab_env.sh).
+_DEFER = {"0": 0, "1": 1, "last": 2}.get(os.environ.get("VSPIKE_DEFER", "last"), 2)
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -400,7 +403,7 @@ class VideoMAE(nn.Module):
                 gs.ln_ws = g["ln_ws"].data_ptr()
                 gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
                 # opt-in: every block but the last one defers its side-stream join to the next
-                gs.flags = L.BWD_DEFER_JOIN if i > 0 and _DEFER else 0
+                gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER else 0)
                 grads[i] = (gs, nxt)
                 cur = nxt
             gs_cache[gkey] = grads
