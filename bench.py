@@ -5,16 +5,27 @@ on 16x224x224 clips (1568 tokens) -> Linear(1568*192 -> 64) -> Linear(64 -> 100*
 PoissonNLL mean, full backward INCLUDING the encoder (freeze_encoder: false), fused AdamW +
 OneCycleLR step, bf16 compute / f32 accumulate, batch 16 clips per GPU, synthetic data
 (random pixels, Poisson spike targets) resident in HBM.  One process per GPU; for N > 1 each
-rank trains its own 16 clips and gradients are all-reduced over RCCL (weak scaling).
+rank trains its own 16 clips and gradients are all-reduced over RCCL (weak scaling).  `--model
+vmae_video --neurons 512` runs C3 (ViT-Base, the reference plugin's own width).
 
-Prints ONE JSON line (rank 0).  `roofline` is measured live with hipEvents bracketing every
-attention launch on its own stream inside the timed region; `cpu_baseline` times the CPU fp32
-oracle (oracle/cpu_ref.py, a torch-CPU restatement of the same step) on the host cores.
+Prints ONE JSON line (rank 0):
+  * `value` = clips/s over EXACTLY `--steps` train steps, timers off, barrier + synchronize on
+    both sides, max over ranks;
+  * `roofline`: a SEPARATE instrumented pass (`--profile-steps`, after the timed region) brackets
+    every launch of every kernel class with hipEvents on its own launch stream (libvspike timers)
+    and sums the classes' algorithmic bytes / flops; the dominant class is the one with the most
+    kernel time per step, reported against its bound (HBM bytes for GEMMs, LayerNorm, AdamW;
+    MFMA flops for attention), with every class listed under `all`;
+  * `cpu_baseline`: the CPU fp32 oracle (oracle/cpu_ref.py, a torch-CPU restatement of the same
+    step) on the host cores, per BASELINE.md's plan (median of 5 after a warm-up, fwd and fwd+bwd,
+    B=1 and B=4), bounded in time; `parity` compares its B=4 loss with the HIP path's on the same
+    clips and initial weights.
 """
 import argparse
+import glob
 import json
-import math
 import os
+import statistics
 import sys
 import time
 
@@ -28,59 +39,93 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0       # HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s is the measured copy rate
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--profile-steps", type=int, default=10, help="instrumented steps after the timed region")
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
     ap.add_argument("--neurons", type=int, default=128)
     ap.add_argument("--model", default="vmae_tiny", help="config/model/<name>.yaml")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-oracle baseline")
+    ap.add_argument("--freeze", action="store_true", help="reference default: encoder frozen (head-only training)")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="budget of the CPU-oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timers", action="store_true", help="do not bracket kernels with hipEvents")
     return ap.parse_args()
 
 
-def cpu_baseline(model_cfg, neurons, seconds):
-    """Oracle (torch-CPU fp32 restatement) train step fwd+bwd on batch-1 clips, bounded in time."""
-    from oracle import cpu_ref, prng
-    bb = model_cfg["backbone"]
-    cfg = cpu_ref.ViTCfg(**{k: (float(v) if k == "layer_norm_eps" else int(v)) for k, v in bb.items()})
-    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, neurons))
-    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 1))
-    y = torch.from_numpy(prng.spike_targets(1, (1, 100, neurons)))
-    threads = torch.get_num_threads()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False), y)
-        loss.backward()
-        for p in P.values():
-            p.grad = None
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or (n >= 2 and el * (n + 1) / n > 2 * seconds):
-            break
-    return {"value": n / el, "unit": "clips/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} clips x fwd+bwd (ViT-Tiny/16 encoder trainable + head + PoissonNLL), batch 1, "
-                      f"fp32 torch-CPU oracle, {el:.1f} s"}
-
-
-def _traffic(op):
-    """HBM bytes per launch of `op` from the committed PMC summary (scripts/pmc_traffic.sh: separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950 correction), or None."""
-    import glob as _glob
-    files = sorted(_glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
-    if not files:
-        return None
+def _cpu_model_name():
     try:
-        d = json.load(open(files[-1]))
-        return round(d["ops"][op]["traffic_bytes"], 0)
-    except (KeyError, ValueError, OSError):
-        return None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, params, pixels, target, seconds):
+    """BASELINE.md CPU plan: the oracle (torch-CPU fp32 restatement of the step) per clip, fwd and
+    fwd+bwd at B=1 and B=4, median of up to 5 runs after one warm-up, on the host threads this
+    process may use (the box's OMP_NUM_THREADS share; `nproc` there counts the whole machine)."""
+    from oracle import cpu_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    P = cpu_ref.to_torch(params)
+    res, t_start, budget_left = {}, time.perf_counter(), seconds
+    loss4 = None
+    for B in (1, 4):
+        px, y = pixels[:B], target[:B]
+        for mode in ("fwd", "fwd_bwd"):
+            def run():
+                if mode == "fwd":
+                    with torch.no_grad():
+                        return cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                loss.backward()
+                for p in P.values():
+                    p.grad = None
+                return loss.detach()
+            t0 = time.perf_counter()
+            loss = run()                                        # warm-up
+            w = time.perf_counter() - t0
+            if B == 4 and mode == "fwd":
+                loss4 = float(loss)
+            left = max(budget_left - (time.perf_counter() - t_start), 0.0)
+            reps = int(max(1, min(5, left / 4 / max(w, 1e-3))))
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                run()
+                ts.append(time.perf_counter() - t0)
+            res[f"B{B}_{mode}_s_per_clip"] = round(statistics.median(ts) / B, 4)
+            res[f"B{B}_{mode}_runs"] = reps
+    elapsed = time.perf_counter() - t_start
+    value = 1.0 / res["B4_fwd_bwd_s_per_clip"]
+    out = {"value": round(value, 4), "unit": "clips/sec", "cores": threads, "kind": "port",
+           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of "
+                     f"{res['B4_fwd_bwd_runs']} after 1 warm-up ({elapsed:.1f} s of CPU work in all)",
+           "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(), "threads_used": threads},
+           "detail": res}
+    return out, loss4
+
+
+def _traffic_lookup(kind):
+    """HBM bytes per launch of a kernel class from the newest committed PMC summary
+    (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950
+    correction), with the file it came from; None when no summary covers that class."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            return round(d["ops"][kind]["traffic_bytes"], 0), os.path.relpath(f, ROOT)
+        except (KeyError, ValueError, OSError):
+            continue
+    return None, None
 
 
 def main():
@@ -104,70 +149,91 @@ def main():
                              os.path.join(cfg_dir, "train", "vmae_video.yaml"))
     config["model"]["decoder"]["output_dim"] = 100 * args.neurons       # src/train.py:41
     config["model"]["compute_dtype"] = args.dtype
-    config["model"]["freeze_encoder"] = False
-    torch.manual_seed(1234 + rank)
+    config["model"]["freeze_encoder"] = bool(args.freeze)
+    torch.manual_seed(1234)                      # identical replicas (GradExchange also broadcasts)
     model = VideoMAE(config["model"]).to(dev)
     bb = model.backbone
     B = args.batch
-    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    g = torch.Generator(device=dev).manual_seed(100 + rank)             # each rank its own clips
     pixels = torch.randn(B, bb.num_frames, bb.num_channels, bb.image_size, bb.image_size, device=dev, generator=g)
     lam = torch.exp(torch.randn(B, 100, args.neurons, device=dev, generator=g) - 2.0).clamp(0.01, 5.0)
     target = torch.poisson(lam, generator=g)
-    total = args.warmup + args.steps
+    do_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    parity = None
+    if do_cpu:   # initial weights and the HIP loss on the first 4 clips, for the in-run parity check
+        init_params = {k: v.detach().cpu().numpy() for k, v in model.reference_state_dict(modern_names=True).items()}
+        with torch.no_grad():
+            gpu_loss4 = float(poisson_nll_mean(model(pixels[:4]), target[:4]))
+    total = args.warmup + args.steps + args.profile_steps
     opt, sched = build_optimizer(model, config, total_steps=total, world=world)
     exchange = GradExchange(model) if world > 1 else None
     trainer = Trainer(model, opt, sched, criterion=poisson_nll_mean, exchange=exchange)
 
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         trainer.step(pixels, target)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    timers = 0 if args.no_timers else (1 << L.TIMER_ATTN_FWD) | (1 << L.TIMER_ATTN_BWD)
-    ops.timing_enable(timers)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier_sync()
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
         losses.append(trainer.step(pixels, target))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier_sync()
     elapsed = time.perf_counter() - t0
-    kern = {}
-    for name, tid in (("attn_fwd", L.TIMER_ATTN_FWD), ("attn_bwd", L.TIMER_ATTN_BWD)):
-        n, ms = ops.timing_collect(tid) if timers else (0, 0.0)
-        kern[name] = (n, ms)
-    ops.timing_enable(0)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(losses[-1].item())
 
+    # ---- instrumented pass (not part of `value`): every kernel class timed on its own stream
+    kern = {}
+    if args.profile_steps > 0:
+        ops.timing_enable((1 << len(L.TIMER_NAMES)) - 1)
+        for _ in range(args.profile_steps):
+            trainer.step(pixels, target)
+        barrier_sync()
+        for tid, name in enumerate(L.TIMER_NAMES):
+            kern[name] = ops.timing_collect(tid, with_bytes=True)
+        ops.timing_enable(0)
+
     clips = world * B * args.steps
     value = clips / elapsed
     N, H, Lyr = bb.num_tokens, bb.num_attention_heads, bb.num_hidden_layers
     fwd_flop = 4.0 * B * H * N * N * 64                 # QK^T + PV per launch (one layer)
-    per = {"attn_fwd": fwd_flop, "attn_bwd": 2.5 * fwd_flop}
+    peak_mfma = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
     roof_all = {}
-    for k, (n, ms) in kern.items():
-        if n:
-            avg_s = ms / n / 1e3
-            ach = per[k] / avg_s / 1e12
-            roof_all[k] = {"launches": n, "avg_ms": ms / n, "flop_per_launch": per[k], "achieved_tflops": ach}
-    dom = max(roof_all, key=lambda k: roof_all[k]["avg_ms"] * roof_all[k]["launches"]) if roof_all else None
-    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    for name, (n, ms, nbytes) in kern.items():
+        if not n:
+            continue
+        per_step = n / args.profile_steps
+        avg_s = ms / n / 1e3
+        if name in ("attn_fwd", "attn_bwd"):
+            work = fwd_flop if name == "attn_fwd" else 2.5 * fwd_flop      # BASELINE.md convention
+            ach = work / avg_s / 1e12
+            ent = {"bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 2), "peak": peak_mfma,
+                   "frac": round(ach / peak_mfma, 4), "work_per_launch": work}
+        else:
+            ach = nbytes / (ms / 1e3) / 1e9                                 # bytes-weighted over launches
+            ent = {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                   "frac": round(ach / PEAK_HBM_GBS, 4), "work_per_launch": round(nbytes / n, 0)}
+        ent.update({"ms_per_step": round(ms / args.profile_steps, 4), "launches_per_step": round(per_step, 2),
+                    "avg_launch_us": round(1e3 * ms / n, 2)})
+        roof_all[name] = ent
     roofline = None
-    if dom:
+    if roof_all:
+        dom = max(roof_all, key=lambda k: roof_all[k]["ms_per_step"])
         r = roof_all[dom]
-        roofline = {"bound": "mfma", "kernel": dom, "achieved": round(r["achieved_tflops"], 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(r["achieved_tflops"] / peak, 4), "traffic": _traffic(dom),
-                    "avg_launch_ms": round(r["avg_ms"], 4), "flop_per_launch": r["flop_per_launch"],
-                    "all": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                            for k, v in roof_all.items()}}
+        traffic, tsrc = _traffic_lookup(dom)
+        roofline = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
+                    "frac": r["frac"], "traffic": traffic, "traffic_source": tsrc,
+                    "avg_launch_ms": round(r["avg_launch_us"] / 1e3, 4), "work_per_launch": r["work_per_launch"],
+                    "timing": f"hipEvents per launch on the launch stream, {args.profile_steps} instrumented steps",
+                    "all": roof_all}
     # algorithmic train FLOPs per clip (BASELINE.md convention: train = 3 x forward)
     D, F, K = bb.hidden_size, bb.intermediate_size, bb.patch_dim
     fwd_clip = Lyr * (2 * N * D * 3 * D + 2 * N * D * D + 4 * N * D * F + 4 * N * N * D) + 2 * N * K * D \
@@ -175,21 +241,34 @@ def main():
     step_tflops = 3 * fwd_clip * B * world * args.steps / elapsed / 1e12
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(config["model"], args.neurons, args.cpu_seconds)
+    if do_cpu:
+        from oracle import cpu_ref
+        ccfg = cpu_ref.ViTCfg(**{k: getattr(bb, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                             "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                             "num_attention_heads", "intermediate_size",
+                                                             "layer_norm_eps")})
+        cpu, cpu_loss4 = cpu_baseline(ccfg, init_params, pixels[:4].cpu(), target[:4].cpu(), args.cpu_seconds)
+        parity = {"what": "PoissonNLL of the first 4 clips at the initial weights: HIP path vs CPU fp32 oracle",
+                  "hip": round(gpu_loss4, 7), "cpu_fp32": round(cpu_loss4, 7),
+                  "rel": round(abs(gpu_loss4 - cpu_loss4) / abs(cpu_loss4), 7),
+                  "tolerance": 1e-4 if args.dtype == "fp32" else 2e-3}
 
     if rank == 0:
+        workload = ("C3 ViT-Base/16" if bb.hidden_size == 768 else "C2 ViT-Tiny/16" if bb.hidden_size == 192
+                    else f"ViT d{bb.hidden_size}")
         line = {
             "metric": "clips/sec (16-frame 224x224) train step", "value": round(value, 3), "unit": "clips/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (randn pixels, Poisson targets), random-init",
-            "config": {"workload": "C2 ViT-Tiny/16 16x224x224 -> 128 neurons, encoder+head fwd+bwd+AdamW",
+            "config": {"workload": f"{workload} {bb.num_frames}x{bb.image_size}x{bb.image_size} -> {args.neurons} "
+                                   f"neurons, {'head only (encoder frozen)' if args.freeze else 'encoder+head'} "
+                                   "fwd+bwd+AdamW",
                        "model": args.model, "global_batch": B * world, "clips_per_gpu": B, "seq_len": N,
                        "parallelism": f"dp{world}"},
-            "mfma_util_pct": round(100.0 * step_tflops / peak, 2),
+            "mfma_util_pct": round(100.0 * step_tflops / peak_mfma, 2),
             "model_tflops": round(step_tflops, 2),
-            "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(final_loss, 6),
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

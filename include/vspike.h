@@ -246,21 +246,27 @@ typedef struct vs_vit_layer_grad {
   int64_t gemm_ws_bytes;
   int32_t flags;        /* VS_BWD_* bits */
   int32_t reserved;
+  void* chain;          /* vs_bwd_chain of this backward sequence (side stream + join state), or
+                           NULL: the weight-gradient products then run on the caller's stream */
 } vs_vit_layer_grad;
 
-/* The weight-gradient GEMMs of a block run on a per-device side stream.  Default: the caller's
- * stream joins it before vs_vit_layer_bwd returns.  VS_BWD_DEFER_JOIN: no join; instead the NEXT
- * vs_vit_layer_bwd call on this device (the next block of the same backward, reusing the same
- * scratch buffers) waits on each product right before overwriting its input.  The weight
+/* With a chain, the weight-gradient GEMMs of a block run on the chain's side stream.  Default: the
+ * caller's stream joins it before vs_vit_layer_bwd returns.  VS_BWD_DEFER_JOIN: no join; instead
+ * the NEXT vs_vit_layer_bwd call with the same chain (the next block of the same backward, reusing
+ * the same scratch buffers) waits on each product right before overwriting its input.  The weight
  * gradients of a deferred block are therefore complete in the caller's stream order only after
  * the next call; the last block of a backward must not set the flag.  VS_BWD_DEFER_LAST: the
  * caller's stream joins the first three products (dW2, dW1, dWproj) at the end of the block and
- * defers only dWqkv, which the next call waits on before overwriting d_qkv; same last-block rule. */
+ * defers only dWqkv, which the next call waits on before overwriting d_qkv; same last-block rule.
+ * Both flags need a chain.  A chain is not thread-safe: one backward sequence uses it at a time
+ * (each model / thread creates its own).  Destroying a chain does not wait for its side stream. */
 #define VS_BWD_DEFER_JOIN 0x1
 #define VS_BWD_DEFER_LAST 0x2
 
 int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
 int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);
+int vs_bwd_chain_create(void** chain);   /* on the current device */
+int vs_bwd_chain_destroy(void* chain);
 
 /* ------------------------------------------------------------------------------------------
  * Trial shards (host side of the input path; replaces the per-trial webdataset tars of
@@ -281,16 +287,25 @@ void vs_shard_close(void* shard);
 const char* vs_shard_last_error(void);
 
 /* ------------------------------------------------------------------------------------------
- * Kernel timing (bench instrumentation).  When enabled, the executor brackets every launch of
- * the tracked kernels with hipEvents on the launch stream.  vs_timing_collect() synchronises on
- * the recorded events and returns per-kernel launch count and total milliseconds.
+ * Kernel timing (bench instrumentation).  When enabled, every launch of a tracked entry point is
+ * bracketed with hipEvents on its launch stream, and the ALGORITHMIC bytes (or flops) of the call
+ * are added to the timer: the bytes a perfect kernel must move (operands read once, outputs
+ * written once; split-K partials, re-reads and padding excluded) — the numerator of a roofline
+ * fraction.  vs_timing_collect() synchronises on the recorded events and returns the launch
+ * count, total milliseconds and total algorithmic bytes of one timer.
  * ------------------------------------------------------------------------------------------ */
-#define VS_TIMER_ATTN_FWD 0
-#define VS_TIMER_ATTN_BWD 1
-#define VS_TIMER_GEMM     2
-#define VS_TIMER_COUNT    3
+#define VS_TIMER_ATTN_FWD 0   /* vs_attn_fwd (bytes: Q,K,V,O,LSE) */
+#define VS_TIMER_ATTN_BWD 1   /* vs_attn_bwd incl. the row prep (bytes: Q,K,V,O,dO,LSE,dQKV) */
+#define VS_TIMER_GEMM     2   /* vs_gemm, activation products (no VS_EPI_ATOMIC) */
+#define VS_TIMER_GEMM_DW  3   /* vs_gemm with VS_EPI_ATOMIC: the token-reduction dW products + reduce */
+#define VS_TIMER_LN_FWD   4   /* vs_layernorm_fwd */
+#define VS_TIMER_LN_BWD   5   /* vs_layernorm_bwd (+ its partial-sum reduction) */
+#define VS_TIMER_ADAMW    6   /* vs_adamw */
+#define VS_TIMER_MISC     7   /* vs_cast, vs_colsum, vs_patch_im2col, vs_poisson_nll(_bwd) */
+#define VS_TIMER_COUNT    8
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
+int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */
 
 #ifdef __cplusplus
 }

@@ -278,10 +278,11 @@ def train_curve(forward, params: Dict[str, torch.Tensor], batches, lr=5e-5, wd=0
 FULL_GRAD_LIMIT = 65536
 
 
-def summarize(name: str, t: np.ndarray, seed: int = 7) -> Dict[str, np.ndarray]:
-    """Full tensor when small, else (norm, 3 seeded projections, first 512 values)."""
+def summarize(name: str, t: np.ndarray, seed: int = 7, full_limit: int = FULL_GRAD_LIMIT) -> Dict[str, np.ndarray]:
+    """Full tensor when small (<= full_limit elements), else (norm, 3 seeded projections, first
+    512 values)."""
     t = np.array(t, dtype=np.float32, copy=True)       # never keep a view of a live .grad
-    if t.size <= FULL_GRAD_LIMIT:
+    if t.size <= full_limit:
         return {"full/" + name: t}
     flat = t.reshape(-1).astype(np.float64)
     projs = np.array([float(flat @ prng.normal(seed, (flat.size,), f"{name}#proj{i}").astype(np.float64))
@@ -298,7 +299,7 @@ def compare_summary(name: str, t: np.ndarray, fx: Dict[str, np.ndarray], rtol: f
         err = np.abs(t - ref)
         ok = bool(np.all(err <= atol + rtol * np.abs(ref)))
         return ok, f"{name}: max|d|={err.max():.3e} max|ref|={np.abs(ref).max():.3e}"
-    mine = summarize(name, t, seed)
+    mine = summarize(name, t, seed, full_limit=0)
     msgs, ok = [], True
     for key in ("norm/", "proj/", "head/"):
         ref, got = fx[key + name], mine[key + name]
@@ -310,6 +311,23 @@ def compare_summary(name: str, t: np.ndarray, fx: Dict[str, np.ndarray], rtol: f
         ok &= bool(good)
         msgs.append(f"{key}{name} max|d|={err:.3e} scale={scale:.3e}")
     return ok, "; ".join(msgs)
+
+
+def summary_rel_error(name: str, t: np.ndarray, fx: Dict[str, np.ndarray], seed: int = 7) -> float:
+    """One norm-relative error figure of `t` against its fixture entry (the bar for reduced
+    precision, where element-wise relative tolerances are meaningless near zero): for a full tensor
+    ||t - ref|| / ||ref||; for a summarised one the largest of |norm - ref| and |proj_i - ref_i|
+    over the reference norm, and of the leading values' max|diff| over their max|ref|."""
+    t = np.asarray(t, dtype=np.float64)
+    if "full/" + name in fx:
+        ref = fx["full/" + name].astype(np.float64)
+        return float(np.linalg.norm((t - ref).ravel()) / max(np.linalg.norm(ref.ravel()), 1e-30))
+    mine = summarize(name, t, seed, full_limit=0)
+    nrm = max(float(fx["norm/" + name][0]), 1e-30)
+    e = max(abs(float(mine["norm/" + name][0]) - nrm), float(np.abs(mine["proj/" + name] - fx["proj/" + name]).max()))
+    head = fx["head/" + name].astype(np.float64)
+    eh = float(np.abs(mine["head/" + name] - head).max() / max(np.abs(head).max(), 1e-30))
+    return max(e / nrm, eh)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -206,6 +206,71 @@ def gen_vit_tiny1l():
     print("vit_tiny1l", fx["loss"])
 
 
+def _grads_summary_small(named_grads, full_limit=4096):
+    out = {}
+    for name, g in named_grads.items():
+        out.update(cpu_ref.summarize(name, g.detach().numpy(), full_limit=full_limit))
+    return out
+
+
+def gen_vit_tiny12():
+    """The bench geometry (BASELINE C2: ViT-Tiny/16, 12 layers, 16x224x224 -> 1568 tokens, n=128),
+    trainable encoder, B=2: forward, every gradient (summarised), and a 4-step train curve with
+    the reference's optimiser (AdamW wd 0.01 + OneCycleLR) at lr 1e-6: the YAML's 5e-5 moves the
+    301,056-wide head input by ~12 logits per step with these seeded weights and the curve diverges."""
+    cfg = cpu_ref.VIT_TINY
+    B, enc_out, n = 2, 64, 128
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    hid = m.video_mae(pixel_values=px).last_hidden_state
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(cpu_ref.summarize("last_hidden", hid.detach().numpy(), full_limit=0))
+    fx.update(_grads_summary_small({k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}))
+    _load_vit(m, cfg, enc_out, n)
+    for k, p in m.named_parameters():
+        p.requires_grad = ".key.bias" not in k
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=400 + s)),
+                torch.from_numpy(prng.spike_targets(450 + s, (B, 100, n)))) for s in range(4)]
+    fx["curve_train"] = _ref_train_loop(m, batches, [p for p in m.parameters() if p.requires_grad], lr=1e-6)
+    np.savez_compressed(os.path.join(OUT, "vit_tiny12.npz"), **fx)
+    print("vit_tiny12", fx["loss"], fx["curve_train"])
+
+
+def gen_vit_base1l():
+    """The reference plugin's real width (videomae-base: d768, 12 heads, videomae.py:7-8; C3's
+    n=512) with one layer, full 1568 tokens, B=1: trainable forward+backward, and a 3-step curve in
+    the reference's default frozen-encoder mode (videomae.py:12,17,34-36)."""
+    cfg = cpu_ref.ViTCfg(num_hidden_layers=1)
+    B, enc_out, n = 1, 64, 512
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(_grads_summary_small({k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}))
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = True
+    for p in m.video_mae.parameters():
+        p.requires_grad = False
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=500 + s)),
+                torch.from_numpy(prng.spike_targets(550 + s, (B, 100, n)))) for s in range(3)]
+    fx["curve_frozen"] = _ref_train_loop(m, batches, list(m.parameters()), lr=2e-7)
+    np.savez_compressed(os.path.join(OUT, "vit_base1l.npz"), **fx)
+    print("vit_base1l", fx["loss"], fx["curve_frozen"])
+
+
 def gen_k0():
     """K0 (src/model/videomae.py:10-11, 18-25): the reference's preprocessing call pattern on a
     seeded video, run through the HF image processor itself (VideoMAEImageProcessor, whose
@@ -301,6 +366,7 @@ def gen_metrics():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "k0", "metrics"]
+    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "vit_tiny12", "vit_base1l", "k0",
+                             "metrics"]
     for w in which:
         globals()["gen_" + w]()

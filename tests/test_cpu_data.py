@@ -83,3 +83,40 @@ def test_loader_epoch_covers_every_trial_once(shards):
     assert first == again                                          # seeded order
     ld2 = ShardLoader(paths, 4, seed=3, device="cpu", drop_last=True)
     assert len(ld2) == 3 and all(len(b["__key__"]) == 4 for b in ld2)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("drop_last", [False, True])
+def test_loader_data_parallel_ranks_split_each_global_batch(shards, tmp_path, world, drop_last):
+    """every rank walks the same seeded permutation; each global batch
+    (batch_size * world records) is cut into `world` disjoint per-rank slices."""
+    from vspike.data import ShardLoader, write_shard
+    n = 45                                                     # not a multiple of 2*3 nor 8*3
+    video = (prng.uniform(300, n * 4 * 1 * 8 * 8, "v") * 256).astype(np.uint8).reshape(n, 4, 1, 8, 8)
+    p = str(tmp_path / "dp.vss")
+    write_shard(p, video, prng.spike_targets(301, (n, 100, 3)), [f"e{i % 3}_{i}" for i in range(n)])
+    bs = 3
+    loaders = [ShardLoader([p], bs, seed=5, device="cpu", rank=r, world=world, drop_last=drop_last)
+               for r in range(world)]
+    for epoch in range(2):
+        per_rank = [[b["__key__"] for b in ld] for ld in loaders]
+        nb = len(per_rank[0])
+        assert all(len(x) == nb == len(loaders[0]) for x in per_rank)          # equal step counts
+        assert all(len(k) == bs for x in per_rank for k in x)                   # full per-rank batches
+        for step in range(nb):
+            glob = [k for r in range(world) for k in per_rank[r][step]]
+            if not (not drop_last and step == nb - 1):
+                assert len(set(glob)) == bs * world                            # disjoint slices
+        covered = {k for x in per_rank for b in x for k in b}
+        if drop_last:
+            assert nb == n // (bs * world) and len(covered) == nb * bs * world
+        else:
+            assert covered == {f"e{i % 3}_{i}" for i in range(n)}              # every record seen
+        # identical permutation on every rank: the concatenated slices are one seeded order
+        want = ShardLoader([p], bs * world, seed=5, device="cpu", drop_last=drop_last).rank_batches(epoch)
+        for step in range(min(nb, len(want))):
+            if len(want[step]) == bs * world:
+                got = np.concatenate([loaders[r].rank_batches(epoch)[step] for r in range(world)])
+                assert np.array_equal(got, want[step])
+    with pytest.raises(ValueError):
+        ShardLoader([p], bs, device="cpu", rank=world, world=world)

@@ -78,13 +78,16 @@ def test_config_loader_matches_reference(golden):
 
 def test_vit_layout_covers_reference_names():
     from oracle import cpu_ref
-    from vspike.layout import BackboneCfg, VitLayout
+    from vspike.layout import BackboneCfg, VitLayout, modern_name
     cfg = BackboneCfg(image_size=112, num_frames=8, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
                       intermediate_size=512)
     lay = VitLayout(cfg, 64, 1600)
     names = [n for n, *_ in lay.hf_items()]
-    ref = [n for n in cpu_ref.vit_param_shapes(cpu_ref.VIT_SMALL_FIXTURE, 64, 16)]
-    assert sorted(names) == sorted(ref)
+    # transformers 4.38 spelling (reference pin, env.yaml:30; modeling_videomae.py:216-218)
+    assert "video_mae.encoder.layer.1.attention.attention.q_bias" in names
+    assert "video_mae.encoder.layer.1.attention.attention.v_bias" in names
+    ref = [n for n in cpu_ref.vit_param_shapes(cpu_ref.VIT_SMALL_FIXTURE, 64, 16)]   # newer HF spelling
+    assert sorted(modern_name(n) for n in names) == sorted(ref)
     for s in list(lay.enc.slots.values()) + list(lay.head.slots.values()):
         assert s.offset % 64 == 0
 
@@ -101,11 +104,40 @@ def test_vit_module_builds_on_cpu_and_maps_weights():
     assert not m.enc_flat.requires_grad        # reference default: frozen encoder (videomae.py:34-36)
     params = cpu_ref.make_vit_params(cfg, 64, 16)
     m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
-    back = m.reference_state_dict()
+    back = m.reference_state_dict(modern_names=True)
     for k, v in params.items():
         assert np.array_equal(back[k].numpy(), v), k
     with pytest.raises(Exception):
         m(torch.zeros(1, 8, 3, 112, 112))      # CPU tensor: no fallback path
+
+
+def test_vit_loads_reference_era_checkpoint_names():
+    """A state_dict saved by the reference (transformers 4.38: `q_bias` / `v_bias`, no key bias)
+    loads strictly and round-trips; the newer names load to the same weights."""
+    from oracle import cpu_ref
+    from vspike import VideoMAE
+    from vspike.layout import modern_name
+    cfg = cpu_ref.VIT_SMALL_FIXTURE
+    conf = {"backbone": {"image_size": 112, "num_frames": 8, "hidden_size": 128, "num_hidden_layers": 2,
+                         "num_attention_heads": 2, "intermediate_size": 512},
+            "encoder": {"output_dim": 64}, "decoder": {"output_dim": 1600}}
+    params = cpu_ref.make_vit_params(cfg, 64, 16)
+    legacy = {}
+    m0 = VideoMAE(conf)
+    for name, *_ in m0.layout.hf_items():
+        legacy[name] = torch.from_numpy(params[modern_name(name)])
+    assert any(k.endswith("attention.attention.q_bias") for k in legacy)
+    m = VideoMAE(conf)
+    m.load_reference_state_dict(legacy, strict=True)
+    back = m.reference_state_dict()
+    assert set(back) == set(legacy)
+    for k, v in legacy.items():
+        assert torch.equal(back[k], v), k
+    m2 = VideoMAE(conf)
+    m2.load_reference_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+    assert torch.equal(m.enc_flat, m2.enc_flat) and torch.equal(m.head_flat, m2.head_flat)
+    with pytest.raises(KeyError):
+        m.load_reference_state_dict({k: v for k, v in legacy.items() if not k.endswith("q_bias")}, strict=True)
 
 
 def _dp_worker(rank, world, port, out):
@@ -124,7 +156,11 @@ def _dp_worker(rank, world, port, out):
             self.grad_sink = None
 
     m = Fake()
+    with torch.no_grad():                          # replicas initialised differently ...
+        m.enc_flat.fill_(10.0 + rank)
+        m.extra.fill_(-rank)
     ex = GradExchange(m, bucket_mb=0.001)          # 262 elements per bucket -> several buckets
+    init = (m.enc_flat.detach().clone(), m.extra.detach().clone())    # ... rank 0's after the broadcast
     gh = ex.grad_buffer(m.head_flat)
     gh += rank + 1
     ex.mark_ready(m.head_flat, 0, 300)
@@ -134,7 +170,7 @@ def _dp_worker(rank, world, port, out):
         ex.mark_ready(m.enc_flat, lo, lo + 100)
     m.extra.grad = torch.full((7,), float(rank))
     ex.finish()
-    out[rank] = (m.head_flat.grad.clone(), m.enc_flat.grad.clone(), m.extra.grad.clone())
+    out[rank] = (m.head_flat.grad.clone(), m.enc_flat.grad.clone(), m.extra.grad.clone(), init)
     dist.destroy_process_group()
 
 
@@ -149,7 +185,8 @@ def test_grad_exchange_gloo_world2():
     out = mgr.dict()
     mp.spawn(_dp_worker, args=(2, port, out), nprocs=2, join=True)
     for r in range(2):
-        h, e, x = out[r]
+        h, e, x, (p_enc, p_extra) = out[r]
+        assert torch.all(p_enc == 10.0) and torch.all(p_extra == 0.0)      # DDP-style broadcast from rank 0
         assert torch.all(h == 3.0)
         ref = torch.cat([torch.full((100,), 3.0 * (lo + 1)) for lo in range(0, 1000, 100)])
         assert torch.equal(e, ref)

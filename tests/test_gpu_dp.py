@@ -1,0 +1,165 @@
+"""Data parallel and the reference's real caller, on the GPU through the HIP path.
+
+* GradExchange (vspike.dp) driven by the REAL VideoMAE backward (deferred side-stream joins,
+  mark_ready ranges in reverse layer order): two ranks on one GPU over gloo, each on its half of a
+  batch; the exchanged gradient / world must equal the single-process gradient of the whole batch
+  (the reference's DP is accelerate -> DDP, src/train.py:61-64).
+* torch DDP — what `accelerator.prepare` wraps a model in when launched multi-process — around the
+  plugin, as is (DDP's own all-reduce at the end of the backward) and with `vspike.dp.attach_ddp`
+  (the all-reduce overlapped with the backward through a DDP communication hook).
+* accelerate itself at world size 1: `Accelerator().prepare(model, optimizer, scheduler)` and
+  `accelerator.backward(loss)` (src/train.py:61-64, src/trainer/base.py:150) reproduce the
+  reference's loss curve; the unwrapped module survives torch.save / torch.load (base.py:212,285-291).
+Two ranks share cuda:0 (RCCL refuses two ranks on one device, so these use gloo; the RCCL path is
+the same code with backend "nccl", exercised by bench.py --gpus N).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _cfg(layers):
+    return cpu_ref.ViTCfg(image_size=112, num_frames=8, hidden_size=128, num_hidden_layers=layers,
+                          num_attention_heads=2, intermediate_size=512)
+
+
+def _model(cfg, dtype, n=16, freeze=False):
+    from vspike import VideoMAE
+    conf = {"model_class": "VideoMAE", "freeze_encoder": freeze, "compute_dtype": dtype,
+            "backbone": {k: getattr(cfg, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                       "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                       "num_attention_heads", "intermediate_size")},
+            "encoder": {"output_dim": 64}, "decoder": {"output_dim": 100 * n}}
+    m = VideoMAE(conf).to(DEV)
+    m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_vit_params(cfg, 64, n).items()})
+    return m
+
+
+def _batch(cfg, B=4, n=16, step=0):
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=700 + step))
+    y = torch.from_numpy(prng.spike_targets(750 + step, (B, 100, n)))
+    return px, y
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, layers, dtype, out):
+    import torch.distributed as dist
+    from vspike import poisson_nll_mean
+    from vspike.dp import GradExchange, attach_ddp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg(layers)
+    torch.manual_seed(100 + rank)                  # replicas built differently: the broadcast aligns them
+    m = _model(cfg, dtype)
+    if rank == 1:
+        with torch.no_grad():
+            m.head_flat.add_(0.5)
+    per = 4 // world
+    if mode == "exchange":
+        ex = GradExchange(m, bucket_mb=0.25)        # ~65 K floats per bucket: many buckets in flight
+        net = m
+    else:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        net = DDP(m, device_ids=[0])
+        ex = attach_ddp(net, bucket_mb=0.25) if mode == "ddp_attach" else None
+    for step in range(2):                           # DDP rebuilds its buckets after the first step
+        px, y = _batch(cfg, step=step)
+        m.zero_grad(set_to_none=True)
+        loss = poisson_nll_mean(net(px[rank * per:(rank + 1) * per].to(DEV)), y[rank * per:(rank + 1) * per].to(DEV))
+        loss.backward()
+        if mode == "exchange":
+            ex.finish()
+    torch.cuda.synchronize()
+    scale = 1.0 / world if mode == "exchange" else 1.0           # DDP averages; the exchange sums
+    out[rank] = (m.enc_flat.grad.detach().cpu() * scale, m.head_flat.grad.detach().cpu() * scale)
+    dist.destroy_process_group()
+
+
+def _single_process_grads(layers, dtype):
+    from vspike import poisson_nll_mean
+    cfg = _cfg(layers)
+    m = _model(cfg, dtype)
+    px, y = _batch(cfg, step=1)
+    m.zero_grad(set_to_none=True)
+    poisson_nll_mean(m(px.to(DEV)), y.to(DEV)).backward()
+    torch.cuda.synchronize()
+    return m.enc_flat.grad.detach().cpu(), m.head_flat.grad.detach().cpu()
+
+
+@pytest.mark.parametrize("mode,layers,dtype,tol", [
+    ("exchange", 2, "fp32", 1e-5),
+    ("exchange", 4, "bf16", 1e-4),        # 4 layers: consecutive deferred joins (VS_BWD_DEFER_LAST)
+    ("ddp", 2, "fp32", 1e-5),
+    ("ddp_attach", 4, "bf16", 1e-4),
+])
+def test_two_ranks_equal_single_process_batch(mode, layers, dtype, tol):
+    import torch.multiprocessing as mp
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), mode, layers, dtype, out), nprocs=world, join=True)
+    ge, gh = _single_process_grads(layers, dtype)
+    for r in range(world):
+        e, h = out[r]
+        for got, want, what in ((e, ge, "encoder"), (h, gh, "head")):
+            err = float((got - want).norm() / want.norm())
+            print(f"\n[{mode} {dtype} rank {r}] {what} grad rel err {err:.2e}")
+            assert err < tol, (mode, r, what, err)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_accelerate_prepare_backward_and_checkpoint(golden, tmp_path):
+    """The reference's caller, unchanged: Accelerator().prepare(model, optimizer, lr_scheduler)
+    (src/train.py:61-64) and accelerator.backward(loss) (src/trainer/base.py:150) over 4 steps of
+    the vit_small fixture's trainable-encoder curve; then the whole-module checkpoint of
+    base.py:285-291 (torch.save({'model': module, 'epoch'})) reloads and computes the same outputs."""
+    from accelerate import Accelerator
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_small.npz")
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _model(cfg, "fp32", n)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=4, max_lr=1e-5, pct_start=0.15, div_factor=10)
+    accelerator = Accelerator()
+    model, optimizer, lr_scheduler = accelerator.prepare(m, opt, sched)
+    losses = []
+    for s in range(4):
+        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=300 + s)).to(accelerator.device)
+        y = torch.from_numpy(prng.spike_targets(350 + s, (B, 100, n))).to(accelerator.device)
+        loss = poisson_nll_mean(model(px), y)
+        accelerator.backward(loss)
+        optimizer.step()
+        lr_scheduler.step()
+        optimizer.zero_grad()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, fx["curve_train"], rtol=1e-3)
+    module = accelerator.unwrap_model(model)
+    torch.save({"model": module, "epoch": 3}, tmp_path / "model_best.pt")
+    back = torch.load(tmp_path / "model_best.pt", weights_only=False)["model"]   # our own file
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=9)).to(DEV)
+    with torch.no_grad():
+        a, b = module(px), back(px)
+    assert (a - b).abs().max().item() <= 1e-6 * a.abs().max().item()

@@ -42,6 +42,7 @@ def _maxrel(a, b):
 
 def test_vit_small_fp32_forward_backward_matches_reference(golden):
     from vspike import poisson_nll_mean
+    from vspike.layout import modern_name
     fx = golden("vit_small.npz")
     cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
     m = _vit_model(cfg, 64, n)
@@ -57,7 +58,7 @@ def test_vit_small_fp32_forward_backward_matches_reference(golden):
     for name, which, slot, rows in m.layout.hf_items():
         flat = m.enc_flat.grad if which == "enc" else m.head_flat.grad
         t = (m.layout.enc if which == "enc" else m.layout.head).view(flat, slot)
-        sd[name] = (t if rows is None else t[rows]).detach().cpu().numpy()
+        sd[modern_name(name)] = (t if rows is None else t[rows]).detach().cpu().numpy()
     for name, g in sd.items():
         shape = cpu_ref.vit_param_shapes(cfg, 64, n)[name]
         ok, msg = cpu_ref.compare_summary(name, g.reshape(shape), fx, rtol=1e-3, atol=1e-8)
@@ -172,7 +173,7 @@ def test_vit_bf16_trains_and_matches_fp32_gradients_direction():
 def test_state_dict_roundtrip_and_pickle(tmp_path):
     cfg = cpu_ref.VIT_SMALL_FIXTURE
     m = _vit_model(cfg, 64, 16)
-    sd = m.reference_state_dict()
+    sd = m.reference_state_dict(modern_names=True)
     ref = cpu_ref.make_vit_params(cfg, 64, 16)
     for k, v in ref.items():
         assert np.array_equal(sd[k].cpu().numpy(), v), k

@@ -1,0 +1,257 @@
+"""Parity of the BENCHED path: the bf16 HIP path at the bench geometry (BASELINE C2: ViT-Tiny/16,
+12 layers, 16x224x224 -> 1568 tokens, n=128, trainable encoder) and at the reference plugin's real
+width (C3: videomae-base d768 / 12 heads, n=512), against fixtures generated from the reference
+itself (oracle/gen_fixtures.py: HF VideoMAEModel + the head of src/model/videomae.py:13-14,28-31).
+
+Tolerances (documented; measured values are printed with -s):
+  * fp32 mode: log-rates 1e-4 of max|ref| (north star), grads 1e-3 of the tensor norm, loss
+    1e-5 relative, loss curve 1e-3 relative (north star).
+  * bf16 mode (activations and weight shadows rounded to bf16 = 2^-9 relative per element, f32
+    accumulation, f32 residual stream / master weights / weight gradients): BF16_OUT of max|ref| on
+    log-rates, BF16_LOSS relative on the loss and on every step of the loss curve, BF16_GRAD
+    norm-relative (cpu_ref.summary_rel_error) on every gradient.
+  * attention alone at the bench grids (B=16: H=3 -> 624 workgroups, H=12 -> 2496) against an fp64
+    reference: the tolerances of tests/test_gpu_ops.py::test_attention_fwd_bwd.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+BF16_OUT = 3e-2      # log-rates, relative to max|ref|
+BF16_LOSS = 2e-3     # loss and loss-curve steps, relative
+BF16_GRAD = 4e-2     # norm-relative gradient error
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _vit_model(cfg, enc_out, n, dtype, freeze=False):
+    from vspike import VideoMAE
+    conf = {"model_class": "VideoMAE", "freeze_encoder": freeze, "compute_dtype": dtype,
+            "backbone": {k: getattr(cfg, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                       "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                       "num_attention_heads", "intermediate_size",
+                                                       "layer_norm_eps")},
+            "encoder": {"output_dim": enc_out}, "decoder": {"output_dim": 100 * n}}
+    m = VideoMAE(conf).to(DEV)
+    m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_vit_params(cfg, enc_out, n).items()})
+    return m
+
+
+def _maxrel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _named_grads(m):
+    from vspike.layout import modern_name
+    out = {}
+    for name, which, slot, rows in m.layout.hf_items():
+        flat = m.enc_flat.grad if which == "enc" else m.head_flat.grad
+        t = (m.layout.enc if which == "enc" else m.layout.head).view(flat, slot)
+        out[modern_name(name)] = (t if rows is None else t[rows]).detach().cpu().numpy()
+    return out
+
+
+def _fwd_bwd_case(fx, cfg, B, n, dtype):
+    from vspike import poisson_nll_mean
+    m = _vit_model(cfg, 64, n, dtype)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    out = m(px)
+    loss = poisson_nll_mean(out, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+    g = _named_grads(m)
+    errs = {k: cpu_ref.summary_rel_error(k, v.reshape(shapes[k]), fx) for k, v in g.items()}
+    out_err = _maxrel(out.detach().cpu(), fx["log_rates"])
+    loss_err = abs(loss.item() - fx["loss"][0]) / abs(fx["loss"][0])
+    worst = max(errs, key=errs.get)
+    print(f"\n[{dtype}] log-rate err {out_err:.3e}  loss err {loss_err:.3e}  worst grad {worst} {errs[worst]:.3e}")
+    return m, g, out_err, loss_err, errs
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_tiny12_bench_geometry_forward_backward(golden, dtype):
+    """C2 geometry, 12 layers, full tokens, B=2: log-rates, loss and all 183 gradients."""
+    fx = golden("vit_tiny12.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 2, 128
+    m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype)
+    if dtype == "fp32":
+        assert out_err < 1e-4 and loss_err < 1e-5
+        shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+        for k, v in g.items():
+            ok, msg = cpu_ref.compare_summary(k, v.reshape(shapes[k]), fx, rtol=1e-3, atol=1e-8)
+            assert ok, msg
+    else:
+        assert out_err < BF16_OUT and loss_err < BF16_LOSS
+        bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
+        assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_tiny12_bench_geometry_loss_curve(golden, dtype):
+    """4 optimiser steps (FusedAdamW + OneCycleLR, the reference's loop body base.py:144-159) at
+    the bench geometry, trainable encoder, against the reference's curve."""
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_tiny12.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 2, 128
+    m = _vit_model(cfg, 64, n, dtype)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-6, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=4, max_lr=1e-6, pct_start=0.15, div_factor=10)
+    losses = []
+    for s in range(4):
+        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=400 + s)).to(DEV)
+        y = torch.from_numpy(prng.spike_targets(450 + s, (B, 100, n))).to(DEV)
+        loss = poisson_nll_mean(m(px), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    rel = np.abs(np.array(losses) - fx["curve_train"]) / np.abs(fx["curve_train"])
+    print(f"\n[{dtype}] curve {losses} ref {fx['curve_train'].tolist()} max rel {rel.max():.3e}")
+    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_base_one_layer_forward_backward(golden, dtype):
+    """C3 width (d768, 12 heads -> B*H = 12 attention heads per clip), full tokens, n=512."""
+    fx = golden("vit_base1l.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_hidden_layers=1), 1, 512
+    m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype)
+    if dtype == "fp32":
+        assert out_err < 1e-4 and loss_err < 1e-5
+        shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+        for k, v in g.items():
+            ok, msg = cpu_ref.compare_summary(k, v.reshape(shapes[k]), fx, rtol=1e-3, atol=1e-8)
+            assert ok, msg
+    else:
+        assert out_err < BF16_OUT and loss_err < BF16_LOSS
+        bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
+        assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_base_frozen_encoder_loss_curve(golden, dtype):
+    """The reference's default training mode (encoder frozen under no_grad, videomae.py:12,17,34-36;
+    AdamW over the head) at videomae-base width."""
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_base1l.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_hidden_layers=1), 1, 512
+    m = _vit_model(cfg, 64, n, dtype, freeze=True)
+    assert not m.enc_flat.requires_grad
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=2e-7, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=3, max_lr=2e-7, pct_start=0.15, div_factor=10)
+    losses = []
+    for s in range(3):
+        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=500 + s)).to(DEV)
+        y = torch.from_numpy(prng.spike_targets(550 + s, (B, 100, n))).to(DEV)
+        loss = poisson_nll_mean(m(px), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    rel = np.abs(np.array(losses) - fx["curve_frozen"]) / np.abs(fx["curve_frozen"])
+    print(f"\n[{dtype}] frozen curve {losses} max rel {rel.max():.3e}")
+    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+
+
+# ------------------------------------------------------------------------ attention, bench grids
+def _attn_ref64(qkv, do, B, N, H, scale=0.125):
+    """fp64 reference on the device (the CPU would take minutes at B*H = 192), in head chunks."""
+    D = H * 64
+    x = qkv.double().view(B, N, 3, H, 64)
+    g = do.double().view(B, N, H, 64)
+    o = torch.empty(B, N, H, 64, dtype=torch.float64, device=qkv.device)
+    lse = torch.empty(B, H, N, dtype=torch.float64, device=qkv.device)
+    dqkv = torch.empty(B, N, 3, H, 64, dtype=torch.float64, device=qkv.device)
+    for b in range(B):
+        q = x[b, :, 0].transpose(0, 1).clone().requires_grad_()
+        k = x[b, :, 1].transpose(0, 1).clone().requires_grad_()
+        v = x[b, :, 2].transpose(0, 1).clone().requires_grad_()
+        s = (q @ k.transpose(-1, -2)) * scale
+        ob = torch.softmax(s, -1) @ v
+        dq, dk, dv = torch.autograd.grad(ob, (q, k, v), g[b].transpose(0, 1))
+        o[b] = ob.detach().transpose(0, 1)
+        lse[b] = torch.logsumexp(s.detach(), -1)
+        dqkv[b, :, 0], dqkv[b, :, 1], dqkv[b, :, 2] = dq.transpose(0, 1), dk.transpose(0, 1), dv.transpose(0, 1)
+    return o.view(B * N, D), lse, dqkv.view(B * N, 3 * D)
+
+
+def _rel(a, b):
+    return float((a.double() - b).norm() / b.norm())
+
+
+@pytest.mark.parametrize("H", [3, 12])
+def test_attention_bf16_at_bench_grid(H):
+    """B=16, N=1568: the grids the bench (H=3, 624 workgroups per pass, XCD-remapped) and C3
+    (H=12, 2496) launch; the row prep + fused dK/dV / dQ backward on the forward's own O and LSE."""
+    from vspike import ops
+    B, N = 16, 1568
+    D = H * 64
+    g = torch.Generator(device=DEV).manual_seed(1234 + H)
+    # activations of the scale a trained ViT shows: |scores| up to ~20
+    qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 1.2).to(torch.bfloat16)
+    do = torch.randn(B * N, D, device=DEV, generator=g).to(torch.bfloat16)
+    o = torch.empty(B * N, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, o, lse, B, N, H)
+    dqkv = torch.empty(B * N, 3 * D, dtype=torch.bfloat16, device=DEV)
+    ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=DEV)
+    ops.attn_bwd(qkv, o, do, lse, dqkv, ws, B, N, H)
+    torch.cuda.synchronize()
+    o_ref, lse_ref, d_ref = _attn_ref64(qkv, do, B, N, H)
+    eo, el = _rel(o.float(), o_ref), _rel(lse, lse_ref)
+    parts = [_rel(dqkv[:, i * D:(i + 1) * D].float(), d_ref[:, i * D:(i + 1) * D]) for i in range(3)]
+    print(f"\n[attn B=16 H={H}] o {eo:.3e} lse {el:.3e} dq {parts[0]:.3e} dk {parts[1]:.3e} dv {parts[2]:.3e}")
+    assert eo < 1.5e-2 and el < 3e-3
+    assert max(parts) < 3e-2, parts
+    # every (batch, head) block covered: per-head errors, not only the global norm
+    per = ((o.float().double() - o_ref).view(B, N, H, 64).norm(dim=(1, 3)) /
+           o_ref.view(B, N, H, 64).norm(dim=(1, 3)))
+    assert float(per.max()) < 3e-2
+
+
+# ------------------------------------------------------------------ deferred joins, many layers
+@pytest.mark.parametrize("mode", [1, 2])
+def test_deferred_joins_four_layers_per_layer_grads(mode):
+    """VS_BWD_DEFER_JOIN / _LAST with 4 layers (several deferred blocks in a row: alternating event
+    parity, pending bits carried forward) over two steps: every layer's gradient slice equals the
+    join-every-block result (norm-relative 1e-5: the fused bias row sums add f32 atomics)."""
+    import vspike.vit as V
+    from vspike import poisson_nll_mean
+    cfg = cpu_ref.ViTCfg(image_size=112, num_frames=8, hidden_size=128, num_hidden_layers=4,
+                         num_attention_heads=2, intermediate_size=512)
+    B, n = 2, 16
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    grads = {}
+    old = V._DEFER
+    try:
+        for m_ in (0, mode):
+            V._DEFER = m_
+            m = _vit_model(cfg, 64, n, "bf16")
+            for _ in range(2):
+                m.enc_flat.grad = None
+                poisson_nll_mean(m(px), y).backward()
+            torch.cuda.synchronize()
+            grads[m_] = (m.enc_flat.grad.detach().clone(), m.layout)
+    finally:
+        V._DEFER = old
+    (g0, lay), (g1, _) = grads[0], grads[mode]
+    for i, (lo, hi) in enumerate(lay.layer_ranges):
+        a, b = g0[lo:hi], g1[lo:hi]
+        assert float((a - b).norm()) <= 1e-5 * float(a.norm()), i

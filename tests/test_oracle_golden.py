@@ -100,6 +100,61 @@ def test_vit_tiny_full_tokens_matches_reference(golden):
     np.testing.assert_allclose(out.numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
 
 
+def test_vit_tiny12_bench_geometry_matches_reference(golden):
+    """The bench geometry (C2: ViT-Tiny, 12 layers, 1568 tokens, n=128, trainable encoder), B=2:
+    log-rates, last hidden state and every gradient, plus the 4-step train curve."""
+    fx = golden("vit_tiny12.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 2, 128
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    hid = cpu_ref.videomae_encoder(px, P, cfg)
+    ok, msg = cpu_ref.compare_summary("last_hidden", hid.detach().numpy(), fx, rtol=1e-4, atol=1e-6)
+    assert ok, msg
+    out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-5 * abs(fx["loss"][0])
+    loss.backward()
+    for k, p in P.items():
+        if ".key.bias" in k:
+            continue
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=5e-4, atol=1e-7)
+        assert ok, msg
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=400 + s)),
+                torch.from_numpy(prng.spike_targets(450 + s, (B, 100, n)))) for s in range(4)]
+    fwd = lambda x, PP: cpu_ref.videomae_plugin_forward(x, PP, cfg, freeze_encoder=False)  # noqa: E731
+    curve = cpu_ref.train_curve(fwd, P, batches, lr=1e-6)
+    np.testing.assert_allclose(curve, fx["curve_train"], rtol=1e-4)
+
+
+def test_vit_base_one_layer_matches_reference(golden):
+    """The reference plugin's real width (videomae-base d768 / 12 heads, C3's n=512), 1 layer, B=1:
+    trainable fwd+bwd, and the default frozen-encoder curve."""
+    fx = golden("vit_base1l.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_hidden_layers=1), 1, 512
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B))
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n)))
+    out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    loss.backward()
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-5 * abs(fx["loss"][0])
+    for k, p in P.items():
+        if ".key.bias" in k:
+            continue
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=5e-4, atol=1e-7)
+        assert ok, msg
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=500 + s)),
+                torch.from_numpy(prng.spike_targets(550 + s, (B, 100, n)))) for s in range(3)]
+    fwd = lambda x, PP: cpu_ref.videomae_plugin_forward(x, PP, cfg, freeze_encoder=True)  # noqa: E731
+    curve = cpu_ref.train_curve(fwd, P, batches, lr=2e-7, trainable=lambda k: not k.startswith("video_mae."))
+    np.testing.assert_allclose(curve, fx["curve_frozen"], rtol=1e-4)
+
+
 def test_k0_preprocess_oracle_matches_reference_processor(golden):
     """K0 (videomae.py:18-25): the restated PIL bilinear resize + HF rescale/normalise reproduce the
     HF image processor's output bit for bit (fixture made by oracle/gen_fixtures.py gen_k0)."""

@@ -1090,7 +1090,8 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   VS_REQUIRE(qkv && o && lse, "vs_attn_fwd: null pointer");
   VS_REQUIRE(ld_qkv >= 3 * H * 64 && ld_o >= H * 64, "vs_attn_fwd: leading dims too small");
   hipStream_t s = (hipStream_t)stream;
-  ScopedTimer timer(VS_TIMER_ATTN_FWD, s);
+  const double es = dtype == VS_BF16 ? 2.0 : 4.0;
+  ScopedTimer timer(VS_TIMER_ATTN_FWD, s, (double)(B * N * H * 64) * 4.0 * es + (double)(B * H * N) * 4.0);
   if (dtype == VS_BF16) {
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
@@ -1124,7 +1125,8 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   VS_REQUIRE(ld_qkv >= 3 * H * 64 && ld_dqkv >= 3 * H * 64 && ld_o >= H * 64 && ld_do >= H * 64,
              "vs_attn_bwd: leading dims too small");
   hipStream_t s = (hipStream_t)stream;
-  ScopedTimer timer(VS_TIMER_ATTN_BWD, s);
+  const double es = dtype == VS_BF16 ? 2.0 : 4.0;
+  ScopedTimer timer(VS_TIMER_ATTN_BWD, s, (double)(B * N * H * 64) * 8.0 * es + (double)(B * H * N) * 4.0);
   float* delta = (float*)workspace;
   const int64_t rows = B * N;
   const unsigned dgrid = (unsigned)cdiv(rows * H, 4);

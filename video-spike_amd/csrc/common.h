@@ -47,7 +47,7 @@ struct ScopedTimer {
   int timer;
   hipStream_t stream;
   void* ev_end;
-  ScopedTimer(int t, hipStream_t s);
+  ScopedTimer(int t, hipStream_t s, double algorithmic_bytes = 0.0);
   ~ScopedTimer();
 };
 

@@ -238,6 +238,7 @@ extern "C" int vs_patch_im2col(int32_t out_dtype, int64_t B, int64_t F, int64_t 
   const int64_t total8 = B * (F / tubelet) * (H / patch) * (W / patch) * C * tubelet * patch * patch / 8;
   if (total8 == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_MISC, s, (double)total8 * 8.0 * (4.0 + (double)esize(out_dtype)));
   const unsigned g = grid_for(total8);
   if (out_dtype == VS_BF16)
     hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(g), dim3(256), 0, s, pixels, (bf16_t*)cols, B, (int)F, (int)C,
@@ -263,6 +264,7 @@ extern "C" int vs_colsum(int32_t dtype, int64_t rows, int64_t cols, const void* 
   VS_REQUIRE(x && out && ldx >= cols, "vs_colsum: bad args");
   if (rows == 0 || cols == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_MISC, s, (double)rows * (double)cols * (double)esize(dtype) + (double)cols * 8.0);
   const int vec = dtype == VS_BF16 ? 8 : 4;
   if (cols % 8 == 0 && ldx % vec == 0 && aligned16(x)) {
     const int64_t cb = cdiv(cols, 256);
@@ -295,6 +297,7 @@ extern "C" int vs_cast(int32_t in_dtype, int32_t out_dtype, int64_t n, const voi
   VS_REQUIRE(in && out && n >= 0, "vs_cast: bad args");
   if (n == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_MISC, s, (double)n * (double)(esize(in_dtype) + esize(out_dtype)));
   if (in_dtype == VS_F32 && out_dtype == VS_BF16) {
     VS_REQUIRE(aligned16(in) && (((uintptr_t)out) & 7u) == 0, "vs_cast: misaligned");
     hipLaunchKernelGGL(cast_f32_bf16, dim3(grid_for(n, 4)), dim3(256), 0, s, (const float*)in, (bf16_t*)out, n);
@@ -320,6 +323,7 @@ extern "C" int vs_poisson_nll(int64_t n, const float* log_rate, const float* tar
                               float grad_scale, void* workspace, void* stream) {
   VS_REQUIRE(n > 0 && log_rate && target && loss_out && workspace, "vs_poisson_nll: bad args");
   hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_MISC, s, (double)n * (dx ? 12.0 : 8.0));
   int nb = (int)cdiv(n, 256);
   if (nb > kPoissonBlocks) nb = kPoissonBlocks;
   hipLaunchKernelGGL(poisson_stage1, dim3(nb), dim3(256), 0, s, log_rate, target, dx, grad_scale / (float)n, n,
@@ -342,6 +346,8 @@ extern "C" int vs_adamw(int64_t n, float* param, const float* grad, float* exp_a
                         const float* hyper, void* stream) {
   VS_REQUIRE(param && grad && exp_avg && exp_avg_sq && hyper && n >= 0, "vs_adamw: bad args");
   if (n == 0) return VS_OK;
+  // algorithmic bytes: param, exp_avg, exp_avg_sq read + written, grad read, bf16 shadow written
+  ScopedTimer timer(VS_TIMER_ADAMW, (hipStream_t)stream, (double)n * (28.0 + (param_lp ? 2.0 : 0.0)));
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, param, grad, exp_avg,
                      exp_avg_sq, (bf16_t*)param_lp, hyper);
   VS_LAUNCH_CHECK();

@@ -1184,6 +1184,22 @@ static bool vec_ok(const vs_gemm_desc* d) {
   return ok;
 }
 
+// Bytes a perfect kernel moves for this call (the roofline numerator): A and B read once, C written
+// once (read too when accumulated into), every epilogue operand read / written once.
+static double gemm_algorithmic_bytes(const vs_gemm_desc* d) {
+  const double ea = esize(d->dtype), ec = esize(d->out_dtype), mn = (double)d->M * (double)d->N;
+  const uint32_t f = d->epilogue;
+  double b = ((double)d->M + (double)d->N) * (double)d->K * ea + mn * ec;
+  if (f & (VS_EPI_ATOMIC | VS_EPI_ACCUM)) b += mn * 4.0;
+  if (f & VS_EPI_BIAS) b += (double)d->N * 4.0;
+  if (f & VS_EPI_RESIDUAL) b += mn * 4.0;
+  if (f & VS_EPI_POS) b += (double)(d->pos_rows < d->M ? d->pos_rows : d->M) * (double)d->N * 4.0;
+  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) b += mn * ea;
+  if (f & VS_EPI_GELU) b += mn * ea;
+  if (d->a_rowsum) b += (double)d->M * 8.0;
+  return b;
+}
+
 }  // namespace vs
 
 // the same K split re-planned for 64-wide column tiles (ring kernel); splits as in the 128-wide
@@ -1235,7 +1251,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   e.part = nullptr;
 
   hipStream_t s = (hipStream_t)stream;
-  ScopedTimer timer(VS_TIMER_GEMM, s);
+  ScopedTimer timer((f & VS_EPI_ATOMIC) ? VS_TIMER_GEMM_DW : VS_TIMER_GEMM, s, gemm_algorithmic_bytes(d));
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
   const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
   const GemmPlan plan = plan_gemm(d->dtype, d->M, d->N, d->K, d->split_k, atomic_ok, use_ws ? d->workspace_bytes : 0);

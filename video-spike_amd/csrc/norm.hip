@@ -408,6 +408,9 @@ extern "C" int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, con
   VS_REQUIRE(cols > 0 && cols <= 1024, "vs_layernorm_fwd: cols must be in [1, 1024]");
   if (rows == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
+  // algorithmic bytes: x read, y written, mean / rstd written, gamma / beta read
+  ScopedTimer timer(VS_TIMER_LN_FWD, s,
+                    (double)rows * (double)cols * (4.0 + (double)esize(y_dtype)) + (double)rows * 8.0 + (double)cols * 8.0);
   const int lpr = ln_vec_lpr(cols);
   if (lpr && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(gamma) && aligned16(beta) &&
       (((uintptr_t)y) & (y_dtype == VS_BF16 ? 7 : 15)) == 0) {
@@ -449,6 +452,10 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
   VS_REQUIRE(cols > 0 && cols <= 1024, "vs_layernorm_bwd: cols must be in [1, 1024]");
   if (rows == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
+  // algorithmic bytes: dy, x, (dres) read, dx (+ its bf16 copy) written, row stats, gamma, dgamma/dbeta
+  ScopedTimer timer(VS_TIMER_LN_BWD, s,
+                    (double)rows * (double)cols * (12.0 + (dres ? 4.0 : 0.0) + (dx_lp ? 2.0 : 0.0)) +
+                        (double)rows * 8.0 + (double)cols * 20.0);
   const int lpr = ln_vec_lpr(cols);
   if (lpr && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && (!dres || (lddres % 4 == 0 && aligned16(dres))) &&
       aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(gamma) && (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {

@@ -21,6 +21,7 @@ struct TimerState {
   unsigned mask = 0;  // bit t set: timer t records
   std::vector<hipEvent_t> pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[VS_TIMER_COUNT];
+  double bytes[VS_TIMER_COUNT] = {};
   hipEvent_t get() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -34,9 +35,10 @@ struct TimerState {
 };
 static TimerState g_t;
 
-ScopedTimer::ScopedTimer(int t, hipStream_t s) : timer(t), stream(s), ev_end(nullptr) {
+ScopedTimer::ScopedTimer(int t, hipStream_t s, double algorithmic_bytes) : timer(t), stream(s), ev_end(nullptr) {
   if (!((g_t.mask >> t) & 1u)) return;
   std::lock_guard<std::mutex> lk(g_t.mu);
+  g_t.bytes[t] += algorithmic_bytes;
   hipEvent_t a = g_t.get(), b = g_t.get();
   (void)hipEventRecord(a, s);
   g_t.pairs[t].push_back({a, b});
@@ -48,7 +50,7 @@ ScopedTimer::~ScopedTimer() {
 
 }  // namespace vs
 
-extern "C" int vs_version(void) { return 2; }  // 2: vs_vit_layer_grad.flags
+extern "C" int vs_version(void) { return 3; }  // 2: vs_vit_layer_grad.flags; 3: .chain
 
 extern "C" int vs_struct_size(int which) {
   switch (which) {
@@ -83,7 +85,15 @@ extern "C" int vs_timing_enable(int on) {
       }
       v.clear();
     }
+    for (auto& b : vs::g_t.bytes) b = 0.0;
   }
+  return VS_OK;
+}
+
+extern "C" int vs_timing_bytes(int timer, double* algorithmic_bytes) {
+  VS_REQUIRE(timer >= 0 && timer < VS_TIMER_COUNT, "vs_timing_bytes: bad timer id");
+  std::lock_guard<std::mutex> lk(vs::g_t.mu);
+  if (algorithmic_bytes) *algorithmic_bytes = vs::g_t.bytes[timer];
   return VS_OK;
 }
 
@@ -104,6 +114,7 @@ extern "C" int vs_timing_collect(int timer, int64_t* launches, double* total_ms)
     vs::g_t.pool.push_back(p.second);
   }
   vs::g_t.pairs[timer].clear();
+  vs::g_t.bytes[timer] = 0.0;
   if (launches) *launches = n;
   if (total_ms) *total_ms = tot;
   return VS_OK;

@@ -8,8 +8,6 @@
 //   x' = y + a W2^T + b2 [f32]
 // Backward mirrors it with the weight gradients accumulated in f32 (split-K atomics for the
 // token-reduction dW products, whose K is B*N = 25,088 rows at the bench shape).
-#include <mutex>
-
 #include "common.h"
 
 namespace vs {
@@ -38,41 +36,22 @@ static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t 
 // The side stream forks from the caller's stream at each product's input (an event) and joins it
 // at the end of the block, so the caller's stream order is unchanged for everything downstream
 // (optimizer, gradient exchange) and buffers reused across blocks are never read late.
-// One non-blocking side stream and a small event ring per device, created on first use.
 // Deferred join (VS_BWD_DEFER_JOIN): instead of joining at the end of the block, the side stream
 // records one event per weight-gradient product (two parity sets, alternating per call) and the
 // NEXT block's main stream waits on each just before it overwrites the buffer that product reads
 // (d_a, dy, d_qkv, the dx ping-pong buffer) — by then the product has long finished, so the
 // cross-queue wait no longer stalls the main stream (~20 us per block at the bench shape).
-struct SideStreams {
-  std::mutex mu;
-  hipStream_t side[64] = {};
-  hipEvent_t ev[64][16] = {};
-  int parity[64] = {};
-  int pending[64] = {};  // bit k: the previous block's product k is not joined yet
+// All of that state (side stream, events, parity, pending bits) lives in a caller-owned
+// vs_bwd_chain, one per backward sequence: two backwards interleaved on one device (two models,
+// or threads) each carry their own chain and never consume each other's events.  Without a chain
+// the products run on the caller's stream (no fork, no join, nothing deferred).
+struct BwdChain {
+  int device = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev[16] = {};
+  int parity = 0;
+  int pending = 0;  // bit k: the previous block's product k is not joined yet
 };
-static SideStreams g_side;
-
-static int side_for(hipStream_t main, hipStream_t* side, hipEvent_t** ev, int* dev_out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return (int)e;
-  VS_REQUIRE(dev >= 0 && dev < 64, "vs_vit_layer_bwd: device id out of range");
-  std::lock_guard<std::mutex> lk(g_side.mu);
-  if (!g_side.side[dev]) {
-    e = hipStreamCreateWithFlags(&g_side.side[dev], hipStreamNonBlocking);
-    if (e != hipSuccess) return (int)e;
-    for (auto& x : g_side.ev[dev]) {
-      e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
-      if (e != hipSuccess) return (int)e;
-    }
-  }
-  (void)main;
-  *side = g_side.side[dev];
-  *ev = g_side.ev[dev];
-  *dev_out = dev;
-  return VS_OK;
-}
 
 // `to` waits for everything enqueued so far on `from` (event slot k)
 static int stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
@@ -141,20 +120,29 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
   const void* gx = lp ? G->dx_out_lp : (const void*)G->dx_out;  // dx' as a GEMM operand
   const void* gy = lp ? G->dy_lp : (const void*)G->dy;
-  hipStream_t ms = (hipStream_t)stream, ss = nullptr;
-  hipEvent_t* ev = nullptr;
-  int dev = 0;
-  VS_CALL(side_for(ms, &ss, &ev, &dev));
+  hipStream_t ms = (hipStream_t)stream;
+  BwdChain* ch = (BwdChain*)G->chain;
+  VS_REQUIRE(ch || !(G->flags & (VS_BWD_DEFER_JOIN | VS_BWD_DEFER_LAST)),
+             "vs_vit_layer_bwd: deferred joins need a vs_bwd_chain");
+  if (ch) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    VS_REQUIRE(dev == ch->device, "vs_vit_layer_bwd: chain belongs to another device");
+  }
+  hipStream_t ss = ch ? ch->side : ms;
   void* side = (void*)ss;
-  const int par = g_side.parity[dev];
-  const int pend = g_side.pending[dev];
-  hipEvent_t* pe = ev + 8 + 4 * (1 - par);  // the previous block's products (deferred join)
-  hipEvent_t* ce = ev + 8 + 4 * par;        // this block's
+  hipEvent_t* ev = ch ? ch->ev : nullptr;
+  const int par = ch ? ch->parity : 0;
+  const int pend = ch ? ch->pending : 0;
+  hipEvent_t* pe = ch ? ev + 8 + 4 * (1 - par) : nullptr;  // the previous block's products (deferred join)
+  hipEvent_t* ce = ch ? ev + 8 + 4 * par : nullptr;        // this block's
   auto wait_prev = [&](int k) -> int { return (pend >> k) & 1 ? (int)hipStreamWaitEvent(ms, pe[k], 0) : 0; };
-  auto mark = [&](int k) -> int { return (int)hipEventRecord(ce[k], ss); };
+  auto mark = [&](int k) -> int { return ch ? (int)hipEventRecord(ce[k], ss) : 0; };
+  auto fork = [&](int k) -> int { return ch ? stream_wait(ms, ss, ev[k]) : 0; };
 
   // ---- MLP: x' = y + a W2^T + b2
-  VS_CALL(stream_wait(ms, ss, ev[0]));  // dx' (and the block's saved activations) ready
+  VS_CALL(fork(0));  // dx' (and the block's saved activations) ready
   {  // [side] dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc2;
@@ -170,7 +158,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     g.ld_aux_in = F;
     VS_CALL(vs_gemm(&g, stream));
   }
-  VS_CALL(stream_wait(ms, ss, ev[1]));  // da ready
+  VS_CALL(fork(1));  // da ready
   {  // [side] dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_fc1;
@@ -188,7 +176,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
                            lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
   // ---- attention: y = x + o Wp^T + bp
-  VS_CALL(stream_wait(ms, ss, ev[2]));  // dy ready
+  VS_CALL(fork(2));  // dy ready
   {  // [side] dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_proj;
@@ -204,7 +192,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(wait_prev(3));  // d_qkv is read by the previous block's dWqkv
   VS_CALL(vs_attn_bwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, G->d_o, D, L->lse, G->d_qkv,
                       3 * D, G->attn_ws, L->attn_scale, stream));
-  VS_CALL(stream_wait(ms, ss, ev[3]));  // dqkv ready
+  VS_CALL(fork(3));  // dqkv ready
   {  // [side] dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
     g.a_rowsum = G->b_qkv;
@@ -224,19 +212,51 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(wait_prev(0));  // dx_in is the previous block's dx_out, read by its dW2
   VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
                            lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
+  if (!ch) return VS_OK;
   if (G->flags & VS_BWD_DEFER_JOIN) {
-    g_side.pending[dev] = 0xF;  // the next block waits on ce[] before each overwrite
-    g_side.parity[dev] = 1 - par;
+    ch->pending = 0xF;  // the next block waits on ce[] before each overwrite
+    ch->parity = 1 - par;
   } else if (G->flags & VS_BWD_DEFER_LAST) {
     // join dW2, dW1, dWp (finished during the attention backward, so this wait does not stall);
     // only dWqkv, still running beside dh1 + LN1', is joined by the next block before its
     // attention backward overwrites d_qkv
     VS_CALL((int)hipStreamWaitEvent(ms, ce[2], 0));
-    g_side.pending[dev] = 0x8;
-    g_side.parity[dev] = 1 - par;
+    ch->pending = 0x8;
+    ch->parity = 1 - par;
   } else {
     VS_CALL(stream_wait(ss, ms, ev[4]));  // join: the block's weight gradients are complete
-    g_side.pending[dev] = 0;
+    ch->pending = 0;
   }
+  return VS_OK;
+}
+
+extern "C" int vs_bwd_chain_create(void** chain) {
+  VS_REQUIRE(chain, "vs_bwd_chain_create: null out pointer");
+  *chain = nullptr;
+  BwdChain* c = new BwdChain();
+  hipError_t e = hipGetDevice(&c->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  for (int i = 0; i < 16 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    vs_bwd_chain_destroy(c);
+    return (int)e;
+  }
+  *chain = c;
+  return VS_OK;
+}
+
+extern "C" int vs_bwd_chain_destroy(void* chain) {
+  BwdChain* c = (BwdChain*)chain;
+  if (!c) return VS_OK;
+  int dev = -1;
+  (void)hipGetDevice(&dev);
+  if (dev != c->device) (void)hipSetDevice(c->device);
+  // work still queued on the side stream keeps running: destroy returns without waiting, and
+  // HIP releases the stream and events once their pending work has completed
+  for (auto& x : c->ev)
+    if (x) (void)hipEventDestroy(x);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  if (dev >= 0 && dev != c->device) (void)hipSetDevice(dev);
+  delete c;
   return VS_OK;
 }

@@ -18,7 +18,8 @@ EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 BWD_DEFER_JOIN = 0x1
 BWD_DEFER_LAST = 0x2
-TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM = 0, 1, 2
+TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM, TIMER_GEMM_DW, TIMER_LN_FWD, TIMER_LN_BWD, TIMER_ADAMW, TIMER_MISC = range(8)
+TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "adamw", "misc")
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_size_t)
@@ -57,7 +58,7 @@ class VitLayerGrad(ctypes.Structure):
                 ("dx_out", c_p), ("dx_out_lp", c_p), ("dx_in", c_p), ("dx_in_lp", c_p),
                 ("d_a", c_p), ("d_h", c_p), ("dy", c_p), ("dy_lp", c_p), ("d_o", c_p), ("d_qkv", c_p),
                 ("attn_ws", c_p), ("ln_ws", c_p), ("gemm_ws", c_p), ("gemm_ws_bytes", c_i64),
-                ("flags", c_i32), ("reserved", c_i32)]
+                ("flags", c_i32), ("reserved", c_i32), ("chain", c_p)]
 
 
 # every entry point of include/vspike.h: name -> (restype, argtypes)
@@ -99,8 +100,11 @@ PROTOTYPES = {
     "vs_shard_last_error": (ctypes.c_char_p, []),
     "vs_vit_layer_fwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), c_p]),
     "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
+    "vs_bwd_chain_create": (ctypes.c_int, [ctypes.POINTER(c_p)]),
+    "vs_bwd_chain_destroy": (ctypes.c_int, [c_p]),
     "vs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "vs_timing_collect": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
+    "vs_timing_bytes": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
 }
 
 _LIB = None
@@ -153,3 +157,24 @@ def require_device(*tensors) -> None:
     for t in tensors:
         if t is not None and not t.is_cuda:
             raise VsError("vspike ops run on the GPU only (tensor on %s); there is no CPU fallback" % t.device)
+
+
+class BwdChain:
+    """Owner of one vs_bwd_chain (side stream + deferred-join state of one backward sequence).
+    Created on the current device; destroyed with the object."""
+
+    def __init__(self):
+        h = c_p()
+        check(lib().vs_bwd_chain_create(ctypes.byref(h)), "vs_bwd_chain_create")
+        self.handle = h.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().vs_bwd_chain_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -107,10 +107,19 @@ class TrialShard:
 
 class ShardLoader:
     """Batches of {'video': (B, T, C, H, W) uint8, 'ap': (B, rows, cols) f32 — on `device` —
-    'eid': [...], '__key__': [...]} from one or more shards (all of one geometry)."""
+    'eid': [...], '__key__': [...]} from one or more shards (all of one geometry).
+
+    Data parallel: with `world` > 1, `batch_size` is the per-rank batch and every
+    rank walks the SAME seeded per-epoch permutation of all records in global batches of
+    `batch_size * world`; rank r takes slice r of each global batch, so the ranks' batches are
+    disjoint and together cover the global batch.  An incomplete last global batch is dropped
+    (`drop_last`) or filled from the start of the permutation (every rank then still gets the
+    same number of full batches: no rank waits at the gradient all-reduce for one that ran out).
+    The reference splits by trial file (src/utils/dataset_utils.py:50-88) and its supervised entry
+    does not shard the loaders at all (src/train.py:61-64 prepares only model/optimizer/scheduler)."""
 
     def __init__(self, paths: Sequence[str], batch_size: int, shuffle: bool = True, seed: int = 0, device="cuda",
-                 drop_last: bool = False, threads: int = 8, prefetch: int = 2):
+                 drop_last: bool = False, threads: int = 8, prefetch: int = 2, rank: int = 0, world: int = 1):
         self.shards: List[TrialShard] = [TrialShard(p) for p in paths]
         if not self.shards:
             raise ValueError("ShardLoader: no shards")
@@ -122,21 +131,38 @@ class ShardLoader:
         self.keys = [self.shards[si].key(r) for si, r in self.index]
         self.batch_size, self.shuffle, self.seed, self.drop_last = int(batch_size), shuffle, int(seed), drop_last
         self.device, self.threads, self.prefetch = torch.device(device), int(threads), max(1, int(prefetch))
+        self.rank, self.world = int(rank), int(world)
+        if not (0 <= self.rank < self.world):
+            raise ValueError(f"ShardLoader: rank {rank} outside world {world}")
+        if self.world > 1 and len(self.index) < self.batch_size * self.world and drop_last:
+            raise ValueError("ShardLoader: fewer records than one global batch with drop_last")
         self.epoch = 0
 
     def __len__(self):
-        n = len(self.index)
-        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+        n, g = len(self.index), self.batch_size * self.world
+        return n // g if self.drop_last else -(-n // g)
 
-    def _order(self):
+    def rank_batches(self, epoch: int):
+        """Record numbers of this rank's batches in `epoch` (deterministic; no side effects)."""
         order = np.arange(len(self.index))
         if self.shuffle:
-            np.random.RandomState(self.seed + self.epoch).shuffle(order)
+            np.random.RandomState(self.seed + epoch).shuffle(order)
+        bs, W = self.batch_size, self.world
+        if W == 1:
+            batches = [order[i:i + bs] for i in range(0, len(order), bs)]
+            if self.drop_last and batches and len(batches[-1]) < bs:
+                batches.pop()
+            return batches
+        g = bs * W
+        n_glob = len(order) // g if self.drop_last else -(-len(order) // g)
+        need = n_glob * g
+        if need > len(order):                       # fill the last global batch from the start
+            order = np.concatenate([order, np.resize(order, need - len(order))])
+        return [order[k * g + self.rank * bs: k * g + (self.rank + 1) * bs] for k in range(n_glob)]
+
+    def _order(self):
+        batches = self.rank_batches(self.epoch)
         self.epoch += 1
-        bs = self.batch_size
-        batches = [order[i:i + bs] for i in range(0, len(order), bs)]
-        if self.drop_last and batches and len(batches[-1]) < bs:
-            batches.pop()
         return batches
 
     def _host_slots(self):

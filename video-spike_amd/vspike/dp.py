@@ -10,7 +10,10 @@ the backward.  MI355X-first design:
   * finished ranges are coalesced into buckets of >= `bucket_mb` and launched immediately with
     `async_op=True`: RCCL's stream waits on the current stream at the call, so the collective of
     bucket k runs on its own stream while the backward kernels of layer k-1 execute;
-  * no 1/world scaling pass: the optimizer folds it in (`FusedAdamW(grad_scale=1/world)`).
+  * no 1/world scaling pass: the optimizer folds it in (`FusedAdamW(grad_scale=1/world)`);
+  * like DDP's constructor, every parameter and buffer is broadcast from the group's first rank
+    once at construction, so all replicas start from the same weights whatever each rank's
+    initialisation seed was.
 Parameters that never report ranges (e.g. the Linear plugin's per-layer tensors) are reduced
 in `finish()` as one flattened call.
 """
@@ -23,15 +26,24 @@ import torch.distributed as dist
 
 
 class GradExchange:
-    def __init__(self, model: torch.nn.Module, bucket_mb: float = 32.0, group=None):
+    def __init__(self, model: torch.nn.Module, bucket_mb: float = 32.0, group=None, return_grads: bool = False):
+        """return_grads: the model's autograd Function hands the (being-reduced) sink buffers back
+        to autograd as the gradients instead of installing them as `.grad` itself — the mode DDP
+        needs (its reducer fires on those gradients, `attach_ddp`)."""
         self.model = model
         self.group = group
+        self.return_grads = return_grads
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
         self._buffers: Dict[int, torch.Tensor] = {}
         self._pending: Dict[int, List[Tuple[int, int]]] = {}
         self._works = []
         self._sunk = set()
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            with torch.no_grad():
+                for t in list(model.parameters()) + list(model.buffers()):
+                    dist.broadcast(t.data, src=src, group=group)
         if hasattr(model, "grad_sink"):
             model.grad_sink = self
             self._sunk = {id(model.enc_flat), id(model.head_flat)} if hasattr(model, "enc_flat") else set()
@@ -45,8 +57,13 @@ class GradExchange:
         else:
             buf.zero_()
         self._pending[id(p)] = []
-        p.grad = buf
+        if not self.return_grads:
+            p.grad = buf
         return buf
+
+    def reduced(self, p: torch.Tensor):
+        """The all-reduced (summed) gradient buffer of a sink parameter, or None."""
+        return self._buffers.get(id(p))
 
     def mark_ready(self, p: torch.Tensor, lo: int, hi: int) -> None:
         if self.world == 1 or hi <= lo:
@@ -80,8 +97,8 @@ class GradExchange:
                 for a, b in spans:
                     self._launch(self._buffers[pid][a:b])
                 spans.clear()
-            rest = [p for p in self.model.parameters()
-                    if p.grad is not None and id(p) not in self._sunk]
+            rest = [] if self.return_grads else [p for p in self.model.parameters()   # DDP reduces those
+                                                 if p.grad is not None and id(p) not in self._sunk]
             if rest:
                 flat = torch.cat([p.grad.reshape(-1) for p in rest])
                 dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
@@ -93,3 +110,45 @@ class GradExchange:
         for w in self._works:
             w.wait()
         self._works.clear()
+
+
+# ------------------------------------------------------------------------------------------------
+# Under accelerate / torch DDP (the reference's caller: src/train.py:61-64 `accelerator.prepare`,
+# src/trainer/base.py:150 `accelerator.backward`).
+#
+# Without anything from this module the plugins already train correctly under DDP: the VideoMAE
+# autograd Function returns the two flat gradients at the end of its hand-sequenced backward and
+# DDP's reducer all-reduces (averages) them — but only then, with no overlap, because to autograd
+# the whole backward is one node.  `attach_ddp(ddp_model)` restores the overlap without replacing
+# DDP: a GradExchange sink launches the bucketed all-reduces DURING the backward (head first, then
+# encoder layers in reverse), and a DDP communication hook hands DDP those already-reduced
+# gradients (averaged) instead of starting its own all-reduce.  Parameters without a sink range
+# (e.g. the Linear plugin's) take DDP's default all-reduce in the same hook.
+# ------------------------------------------------------------------------------------------------
+def _overlap_hook(exchange: "GradExchange", bucket):
+    import torch.distributed.algorithms.ddp_comm_hooks.default_hooks as dh
+    params = bucket.parameters()
+    if not all(exchange.reduced(p) is not None for p in params):
+        return dh.allreduce_hook(exchange.group, bucket)
+    exchange.finish()                      # this step's early all-reduces have landed (stream order)
+    buf = bucket.buffer()
+    off = 0
+    for p in params:
+        n = p.numel()
+        buf[off:off + n].copy_(exchange.reduced(p).reshape(-1)).div_(exchange.world)
+        off += n
+    fut = torch.futures.Future()
+    fut.set_result(buf)
+    return fut
+
+
+def attach_ddp(ddp_model, bucket_mb: float = 32.0) -> "GradExchange":
+    """Overlap the gradient all-reduce with the backward for a DDP-wrapped vspike plugin (e.g. the
+    module `accelerator.prepare` returned).  Returns the exchange; nothing else changes in the
+    caller: DDP still averages, the optimizer keeps grad_scale 1."""
+    module = ddp_model.module
+    ex = GradExchange(module, bucket_mb=bucket_mb, group=ddp_model.process_group, return_grads=True)
+    if hasattr(module, "grad_sink"):
+        module.grad_sink = ex
+    ddp_model.register_comm_hook(ex, _overlap_hook)
+    return ex

@@ -76,6 +76,19 @@ class FlatLayout:
         return flat[s.offset:s.offset + s.numel].view(s.shape)
 
 
+# transformers 4.38 (reference pin) -> newer transformers names of the Q/V biases
+LEGACY_BIAS_ALIASES = {"attention.attention.q_bias": "attention.attention.query.bias",
+                       "attention.attention.v_bias": "attention.attention.value.bias"}
+
+
+def modern_name(name: str) -> str:
+    """The newer-transformers spelling of a reference (4.38) state_dict name."""
+    for old, new in LEGACY_BIAS_ALIASES.items():
+        if name.endswith(old):
+            return name[: -len(old)] + new
+    return name
+
+
 LAYER_KEYS = ("ln1_g", "ln1_b", "w_qkv", "b_qkv", "w_proj", "b_proj", "ln2_g", "ln2_b", "w_fc1", "b_fc1",
               "w_fc2", "b_fc2")
 
@@ -107,7 +120,12 @@ class VitLayout:
 
     # ---- reference state_dict names -----------------------------------------------------------
     def hf_items(self):
-        """Yield (hf_name, which_flat, slot_name, row_slice) for every reference parameter."""
+        """Yield (hf_name, which_flat, slot_name, row_slice) for every reference parameter.
+
+        Names are those of the transformers version the reference pins (4.38.2, env.yaml:30):
+        the Q/V biases are separate parameters `attention.attention.q_bias` / `v_bias` and there is
+        no key bias (vendored modeling_videomae.py:216-218, 233).  Newer transformers store them as
+        `query.bias` / `value.bias` (+ a `key.bias`): see `modern_name` / `LEGACY_BIAS_ALIASES`."""
         D = self.cfg.hidden_size
         yield "video_mae.embeddings.patch_embeddings.projection.weight", "enc", "patch_w", None
         yield "video_mae.embeddings.patch_embeddings.projection.bias", "enc", "patch_b", None
@@ -116,8 +134,8 @@ class VitLayout:
             yield p + "attention.attention.query.weight", "enc", f"{i}.w_qkv", slice(0, D)
             yield p + "attention.attention.key.weight", "enc", f"{i}.w_qkv", slice(D, 2 * D)
             yield p + "attention.attention.value.weight", "enc", f"{i}.w_qkv", slice(2 * D, 3 * D)
-            yield p + "attention.attention.query.bias", "enc", f"{i}.b_qkv", slice(0, D)
-            yield p + "attention.attention.value.bias", "enc", f"{i}.b_qkv", slice(2 * D, 3 * D)
+            yield p + "attention.attention.q_bias", "enc", f"{i}.b_qkv", slice(0, D)
+            yield p + "attention.attention.v_bias", "enc", f"{i}.b_qkv", slice(2 * D, 3 * D)
             yield p + "attention.output.dense.weight", "enc", f"{i}.w_proj", None
             yield p + "attention.output.dense.bias", "enc", f"{i}.b_proj", None
             yield p + "intermediate.dense.weight", "enc", f"{i}.w_fc1", None

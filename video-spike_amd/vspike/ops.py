@@ -200,11 +200,14 @@ def timing_enable(mask: int):
     check(lib().vs_timing_enable(int(mask)), "vs_timing_enable")
 
 
-def timing_collect(timer: int):
+def timing_collect(timer: int, with_bytes: bool = False):
+    """(launches, total ms) of one timer, and its total algorithmic bytes with `with_bytes`."""
     n = ctypes.c_int64(0)
     ms = ctypes.c_double(0.0)
+    nb = ctypes.c_double(0.0)
+    check(lib().vs_timing_bytes(timer, ctypes.byref(nb)), "vs_timing_bytes")
     check(lib().vs_timing_collect(timer, ctypes.byref(n), ctypes.byref(ms)), "vs_timing_collect")
-    return int(n.value), float(ms.value)
+    return (int(n.value), float(ms.value), float(nb.value)) if with_bytes else (int(n.value), float(ms.value))
 
 
 def attn_scale(head_dim: int = 64) -> float:

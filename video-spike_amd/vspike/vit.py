@@ -26,7 +26,7 @@ from torch import nn
 
 from . import _lib as L
 from . import ops
-from .layout import BackboneCfg, VitLayout
+from .layout import BackboneCfg, VitLayout, modern_name
 from .memory import Arena
 
 # Side-stream joins of the block backward.  A join at every block end costs a ~24 us cross-queue
@@ -111,32 +111,37 @@ class VideoMAE(nn.Module):
     def _flat_layout(self, which):
         return self.layout.enc if which == "enc" else self.layout.head
 
-    def reference_state_dict(self):
-        """Parameters under the reference plugin's names (HF VideoMAEModel + two Linears)."""
+    def reference_state_dict(self, modern_names: bool = False):
+        """Parameters under the reference plugin's names (HF VideoMAEModel + two Linears): the
+        transformers 4.38 spelling the reference pins (`...attention.attention.q_bias` / `v_bias`),
+        or with `modern_names` the newer `query.bias` / `value.bias`."""
         out = {}
         for name, which, slot, rows in self.layout.hf_items():
             t = self._flat_layout(which).view(self._flat(which).detach(), slot)
             if slot == "patch_w":
                 t = t.view(self.backbone.hidden_size, self.backbone.num_channels, self.backbone.tubelet_size,
                            self.backbone.patch_size, self.backbone.patch_size)
-            out[name] = (t if rows is None else t[rows]).clone()
+            out[modern_name(name) if modern_names else name] = (t if rows is None else t[rows]).clone()
         return out
 
     @torch.no_grad()
     def load_reference_state_dict(self, sd, strict: bool = True):
-        """Load reference-named weights (e.g. a videomae-base checkpoint + head).  The k-bias of
-        newer HF versions must be zero (4.38 has none: modeling_videomae.py:233)."""
+        """Load reference-named weights (e.g. a videomae-base checkpoint + head, or a reference
+        `model_best.pt` state_dict).  Q/V biases are accepted under the 4.38 names the reference
+        pins (`q_bias` / `v_bias`, modeling_videomae.py:216-218) or the newer `query.bias` /
+        `value.bias`; a newer version's `key.bias` must be zero (4.38 has none: :233)."""
         seen = set()
         for name, which, slot, rows in self.layout.hf_items():
-            if name not in sd:
+            key = name if name in sd else modern_name(name)
+            if key not in sd:
                 if strict:
                     raise KeyError(f"missing {name}")
                 continue
             dst = self._flat_layout(which).view(self._flat(which), slot)
-            src = torch.as_tensor(sd[name]).to(dst.device, torch.float32).reshape(
+            src = torch.as_tensor(sd[key]).to(dst.device, torch.float32).reshape(
                 dst[rows].shape if rows is not None else dst.shape)
             (dst[rows] if rows is not None else dst).copy_(src)
-            seen.add(name)
+            seen.add(key)
         for k, v in sd.items():
             if k.endswith("attention.attention.key.bias"):
                 if torch.as_tensor(v).abs().max() != 0:
@@ -185,7 +190,7 @@ class VideoMAE(nn.Module):
         st = super().__getstate__() if hasattr(super(), "__getstate__") else self.__dict__.copy()
         st = dict(st)
         st["_pos_cache"] = {}
-        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache"):
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains"):
             st.pop(k, None)
         st["grad_sink"] = None
         return st
@@ -221,10 +226,22 @@ class VideoMAE(nn.Module):
 
     def _caches(self):
         d = self.__dict__
-        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache"):
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains"):
             if k not in d:
                 d[k] = {}
         return d["_fwd_cache"], d["_bwd_cache"], d["_gs_cache"]
+
+    def _chain(self, dev):
+        """This model's vs_bwd_chain on `dev`: the side stream and deferred-join state of its
+        block backwards (one backward sequence of a model runs at a time, as its scratch is
+        shared too)."""
+        self._caches()
+        chains = self.__dict__["_chains"]
+        key = str(dev)
+        if key not in chains:
+            with torch.cuda.device(dev):
+                chains[key] = L.BwdChain()
+        return chains[key]
 
     def _fwd_buffers(self, B: int, dev, save_encoder: bool):
         """Activation arena, low-precision weight shadows and the 12 executor structs of one
@@ -401,6 +418,7 @@ class VideoMAE(nn.Module):
                 gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
                 gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
                 gs.ln_ws = g["ln_ws"].data_ptr()
+                gs.chain = self._chain(dev).handle
                 gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
                 # opt-in: every block but the last one defers its side-stream join to the next
                 gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER else 0)
@@ -452,6 +470,7 @@ class _VideoMAEFn(torch.autograd.Function):
         mod = ctx.mod
         g_enc, g_head = mod._run_backward(ctx.st, grad, *ctx.want)
         ctx.st = None
-        if mod.grad_sink is not None:          # the sink owns .grad (all-reduced in place)
-            return None, None, None, None
+        sink = mod.grad_sink
+        if sink is not None and not getattr(sink, "return_grads", False):
+            return None, None, None, None      # the sink owns .grad (all-reduced in place)
         return None, g_enc, g_head, None
