@@ -134,7 +134,8 @@ def test_gemm_panel_path_many_items(bkc, shape):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("ws", [None, False])       # split-K partials + reduce launch, or f32 atomics
-@pytest.mark.parametrize("shape", [(64, 192, 25088), (192, 768, 25088), (104, 40, 5000)])
+@pytest.mark.parametrize("shape", [(64, 192, 25088), (192, 768, 25088), (104, 40, 5000), (768, 192, 25088),
+                                   (576, 192, 3136), (192, 192, 1568), (192, 1536, 25088), (8, 16, 70)])
 def test_gemm_splitk_atomic_accumulates(dtype, ws, shape):
     from vspike import ops
     M, N, K = shape                    # the dW shapes: reduction over B*N tokens (+ a ragged one)
@@ -150,6 +151,29 @@ def test_gemm_splitk_atomic_accumulates(dtype, ws, shape):
         c2 = torch.ones(M, N, device=DEV)
         ops.linear_dw(dy.to(DEV), x.to(DEV), c2, workspace=ws)
         assert torch.equal(c, c2)
+
+
+@pytest.mark.parametrize("bm", [64, 128, 192])
+@pytest.mark.parametrize("shape", [(192, 768, 3136 + 40), (576, 192, 1568), (200, 72, 999)])
+def test_dw_kernel_every_tile_height(monkeypatch, bm, shape):
+    """The token-reduction dW kernel (gemm_dw.hip) at every tile height, with ragged tiles, a
+    partial last token step, swapped operands (M > N: C stored transposed, bias = column sums of
+    the swapped B) and the fixed-order split reduce: bit-identical reruns."""
+    from vspike import ops
+    monkeypatch.setenv("VSPIKE_DW_BM", str(bm))
+    M, N, K = shape
+    dy = _rand(K, M, seed=18).to(torch.bfloat16).to(DEV)
+    x = _rand(K, N, seed=19).to(torch.bfloat16).to(DEV)
+    outs = []
+    for _ in range(2):
+        c = torch.full((M, N), 0.5, device=DEV)
+        db = torch.full((M,), -1.0, device=DEV)
+        ops.linear_dw(dy, x, c, db=db)
+        outs.append((c, db))
+    ref = dy.double().t() @ x.double() + 0.5
+    assert rel(outs[0][0], ref) < 2e-5
+    assert rel(outs[0][1], dy.double().sum(0) - 1.0) < 2e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 def test_gemm_splitk_workspace_bias_once():

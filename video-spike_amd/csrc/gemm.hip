@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "gemm_dw.h"
 
 namespace vs {
 
@@ -1171,6 +1172,11 @@ static int getenv_flag3(const char* name) {
   return cached;
 }
 
+static int getenv_flag5(const char* name) {
+  const char* v = getenv(name);
+  return (v && v[0] && v[0] != '0') ? 1 : 0;
+}
+
 static bool vec_ok(const vs_gemm_desc* d) {
   const uint32_t f = d->epilogue;
   const int ovec = d->out_dtype == VS_BF16 ? 8 : 4;
@@ -1254,6 +1260,13 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   ScopedTimer timer((f & VS_EPI_ATOMIC) ? VS_TIMER_GEMM_DW : VS_TIMER_GEMM, s, gemm_algorithmic_bytes(d));
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
   const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
+  // token-reduction weight gradients (dW = dY^T X, both operands token-major): the dedicated
+  // split-K kernel with a fixed-order reduce (gemm_dw.hip)
+  static const int no_dw = getenv_flag5("VSPIKE_DW_OLD");
+  if (!no_dw && d->dtype == VS_BF16 && d->out_dtype == VS_F32 && f == VS_EPI_ATOMIC && !d->a_kcontig &&
+      !d->b_kcontig && d->split_k <= 0 && use_ws && d->K >= 1 && d->M % 8 == 0 && d->N % 8 == 0 &&
+      d->lda % 8 == 0 && d->ldb % 8 == 0 && (size_t)d->workspace_bytes >= dw_workspace_bytes(d->M, d->N, d->K))
+    return launch_dw(d, s);
   const GemmPlan plan = plan_gemm(d->dtype, d->M, d->N, d->K, d->split_k, atomic_ok, use_ws ? d->workspace_bytes : 0);
   const GridMap& g = plan.g;
   if (use_ws && g.splits > 1) e.part = (float*)d->workspace;
@@ -1344,7 +1357,12 @@ extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64
   using namespace vs;
   if (M <= 0 || N <= 0 || K <= 0 || (dtype != VS_F32 && dtype != VS_BF16)) return 0;
   const GemmPlan p = plan_gemm(dtype, M, N, K, 0, true, 0);
-  return p.g.splits > 1 ? (size_t)p.g.splits * (size_t)(M * N) * 4 : 0;
+  size_t b = p.g.splits > 1 ? (size_t)p.g.splits * (size_t)(M * N) * 4 : 0;
+  if (dtype == VS_BF16) {  // the dW kernel's partial tiles + bias sums (if this shape is a dW product)
+    const size_t dw = dw_workspace_bytes(M, N, K);
+    if (dw > b) b = dw;
+  }
+  return b;
 }
 
 #ifdef VS_STAMP

@@ -1,0 +1,27 @@
+// gemm_dw.h — the token-reduction weight-gradient GEMM (gemm_dw.hip), used by vs_gemm.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vspike.h"
+
+namespace vs {
+
+struct DwGrid {
+  int tiles_m, tiles_n, splits, ksteps;  // ksteps: 64-token steps per split
+};
+
+struct DwPlan {
+  bool valid, swap;  // swap: the kernel runs on (B, A) and stores C transposed
+  int BM;            // output rows per tile (64, 128 or 192); 64 columns
+  DwGrid g;
+  int64_t part_floats, sum_floats;
+};
+
+DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
+size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int launch_dw(const vs_gemm_desc* d, hipStream_t s);
+
+}  // namespace vs

@@ -1,0 +1,391 @@
+// gemm_dw.hip — the weight-gradient products of the backward: C[M,N] += A^T B over the token axis.
+//
+// Replaces the dW half of autograd for every nn.Linear / Conv3d-as-GEMM of the encoder
+// (accelerator.backward, src/trainer/base.py:150): dW2 = dx'^T a (mv:390-397), dW1 = da^T h2
+// (mv:373-383), dWproj = dy^T o (mv:312-319), dWqkv = dqkv^T h1 (mv:233-236), the patch-embed
+// dW = dx^T cols (mv:176-181), each with the bias gradient (column sums of the dY operand) fused.
+//
+// Shape: K = B*N tokens (25,088 at the bench) >> M, N (192..1536).  Both operands are token-major
+// ([K, features] rows), so the product is a reduction over K and its output is small (0.04-1.2 MB):
+// the only parallelism is splitting K.  Design (MI355X):
+//   * tile = BM x 64 outputs with BM up to 192 = the WHOLE narrow operand (the host swaps A and B so
+//     that A is the narrow one, storing C transposed), so the wide operand is streamed exactly once
+//     per token slab and only the narrow one is re-read (from L2: the tiles of one token slab are
+//     consecutive logical blocks, which the XCD remap puts on one XCD);
+//   * one token slab (split) per workgroup, 4-deep LDS-DMA ring of 64-token steps (asm
+//     global_load_lds, counted vmcnt across raw s_barriers, as gemm_bf16_ring_kernel);
+//   * the f32 partial tile is written in MFMA FRAGMENT order (each wave-instruction a contiguous
+//     1 KiB: no LDS staging), and gemm_dw_reduce adds the splits IN SPLIT ORDER and scatters into C
+//     (C += sum): bitwise reproducible, no atomics — also for the fused bias gradient, whose
+//     per-split sums go through the same workspace;
+//   * the split count comes from a small cost model (plan_dw): enough workgroups to stream at the
+//     chip's rate, few enough that the partial tiles (#workgroups x tile bytes) stay a small
+//     fraction of the operand bytes.
+#include <cstdlib>
+
+#include "common.h"
+#include "gemm_dw.h"
+
+namespace vs {
+
+// [64 k][64 rows] bf16 LDS image of an M/N-contiguous operand: the 8-KiB image of OperandBf16<64,
+// KC=false> in gemm.hip (16-B chunk XOR on k, read back transposed by ds_read_tr16_b64).
+__device__ __forceinline__ int dw_swz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+
+// LDS-DMA of one 8-KiB image: 8 pieces of 8 k-rows x 128 B; wave `wid` issues pieces 2wid, 2wid+1.
+// Columns past `cols` re-read the last 8 valid columns, token rows past `k_valid` re-read row
+// k_valid - 1 (finite data; those rows are zeroed in LDS before use, those columns never stored).
+__device__ __forceinline__ void dw_dma(char* img, const bf16_t* __restrict__ p, int64_t ld, int64_t c0, int64_t cols,
+                                       int64_t k0, int k_valid, int wid, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pi = wid * 2 + j;
+    const int k = pi * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ dw_swz(k);
+    const int64_t gc = c0 + c * 8 <= cols - 8 ? c0 + c * 8 : cols - 8;
+    const int kk = k < k_valid ? k : k_valid - 1;
+    glds16_asm(p + (k0 + kk) * ld + gc, img + pi * 1024);
+  }
+}
+
+// fragment of rows [rb, rb+16) (rb within the image), 32-deep k step kk: lane holds row
+// rb + (lane & 15), k = 32 kk + 8 (lane >> 4) + 0..7 (the MFMA 16x16x32 A / B operand layout)
+__device__ __forceinline__ bf16x8 dw_frag(const char* img, int rb, int kk, int lane) {
+  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+  const int col = rb + p4;
+  const int k0 = kk * 32 + 8 * (lane >> 4) + q;
+  const int k1 = k0 + 4;
+  const int off0 = k0 * 128 + (((col >> 3) ^ dw_swz(k0)) << 4) + (col & 7) * 2;
+  const int off1 = k1 * 128 + (((col >> 3) ^ dw_swz(k1)) << 4) + (col & 7) * 2;
+  short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(img + off0));
+  short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(img + off1));
+  typedef __attribute__((ext_vector_type(8))) short short8v;
+  short8v s = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return __builtin_bit_cast(bf16x8, s);
+}
+
+// SUMS: 0 none; 1 row sums of A (the bias gradient when A is the dY operand), written by the
+// nt == 0 tiles; 2 column sums of B (when the host swapped the operands), by the mt == 0 tiles.
+template <int BM, int SUMS>
+__global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                         int64_t M, const bf16_t* __restrict__ B,
+                                                                         int64_t ldb, int64_t N, int64_t K,
+                                                                         DwGrid g, float* __restrict__ part,
+                                                                         float* __restrict__ sums) {
+  constexpr int NA = BM / 64;             // 64-row A images per stage
+  constexpr int IMG = 8192;
+  constexpr int STAGE = (NA + 1) * IMG;   // A images then the B image
+  constexpr int PER = (NA + 1) * 2;       // DMA wave-instructions per stage
+  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
+  __shared__ __attribute__((aligned(16))) char st0[STAGE];
+  __shared__ __attribute__((aligned(16))) char st1[STAGE];
+  __shared__ __attribute__((aligned(16))) char st2[STAGE];
+  __shared__ __attribute__((aligned(16))) char st3[STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);   // one token slab's tiles are consecutive: one XCD
+  const int split = t / tiles, rem = t % tiles, mt = rem / g.tiles_n, nt = rem % g.tiles_n;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * 64;
+  const int nk_all = (int)((K + 63) / 64);
+  const int ks0 = split * g.ksteps, ks1 = ks0 + g.ksteps < nk_all ? ks0 + g.ksteps : nk_all;
+  const int nk = ks1 - ks0;
+
+  f32x4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool sum_on = (SUMS == 1 && nt == 0) || (SUMS == 2 && mt == 0 && wid == 0);
+  float sacc[SUMS == 2 ? FJ : FI];
+#pragma unroll
+  for (int i = 0; i < (SUMS == 2 ? FJ : FI); ++i) sacc[i] = 0.f;
+
+  auto issue = [&](int s, char* stg) {
+    const int64_t k0 = (int64_t)(ks0 + s) * 64;
+    const int kv = K - k0 < 64 ? (int)(K - k0) : 64;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) dw_dma(stg + a * IMG, A, lda, m0 + a * 64, M, k0, kv, wid, lane);
+    dw_dma(stg + NA * IMG, B, ldb, n0, N, k0, kv, wid, lane);
+  };
+  auto compute = [&](const char* stg) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[FI], bfr[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int r = wid * WM + i * 16;  // r and r+15 lie in the same 64-row image (WM % 16 == 0)
+        af[i] = dw_frag(stg + (r >> 6) * IMG, r & 63, kk, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, j * 16, kk, lane);
+      if (sum_on) {
+        if constexpr (SUMS == 1) {
+#pragma unroll
+          for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sacc[i] += (float)af[i][q];
+        } else if constexpr (SUMS == 2) {
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sacc[j] += (float)bfr[j][q];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  // rows k >= k_valid of a partial last step hold re-read data: zero them in every image
+  auto zero_tail = [&](char* stg, int kv) {
+    const int bytes = (64 - kv) * 128;
+    for (int a = 0; a <= NA; ++a)
+      for (int o = tid * 16; o < bytes; o += 256 * 16) *(uint4*)(stg + a * IMG + kv * 128 + o) = make_uint4(0, 0, 0, 0);
+  };
+  auto step = [&](int s, auto sc) {
+    constexpr int S = decltype(sc)::value;
+    char* cur = S == 0 ? st0 : S == 1 ? st1 : S == 2 ? st2 : st3;
+    char* far = S == 0 ? st3 : S == 1 ? st0 : S == 2 ? st1 : st2;  // stage of step s + 3
+    // steps s+1, s+2 may stay in flight
+    if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (s + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's step-s pieces landed; step s-1's stage is free
+    asm volatile("" ::: "memory");
+    const int64_t k0 = (int64_t)(ks0 + s) * 64;
+    if (K - k0 < 64) {  // block-uniform: only the very last token step of the whole reduction
+      zero_tail(cur, (int)(K - k0));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (s + 3 < nk) issue(s + 3, far);
+    compute(cur);
+  };
+  if (nk > 0) issue(0, st0);
+  if (nk > 1) issue(1, st1);
+  if (nk > 2) issue(2, st2);
+  for (int s = 0; s < nk; s += 4) {
+    step(s, IC<0>{});
+    if (s + 1 < nk) step(s + 1, IC<1>{});
+    if (s + 2 < nk) step(s + 2, IC<2>{});
+    if (s + 3 < nk) step(s + 3, IC<3>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // partial tile in fragment order: float4 q = ((wid*FI + i)*FJ + j)*64 + lane
+  float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * 64));
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const f32x4 v = acc[i][j];
+      pt[((wid * FI + i) * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  if (sum_on) {
+    // lane groups g = lane >> 4 hold disjoint k; rows / columns (lane & 15)
+    constexpr int NS = SUMS == 2 ? FJ : FI;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      float v = sacc[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      sacc[i] = v;
+    }
+    if (lane < 16) {
+      if constexpr (SUMS == 1) {
+        float* so = sums + ((int64_t)mt * g.splits + split) * BM;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) so[wid * WM + i * 16 + lane] = sacc[i];
+      } else if constexpr (SUMS == 2) {
+        float* so = sums + ((int64_t)nt * g.splits + split) * 64;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) so[j * 16 + lane] = sacc[j];
+      }
+    }
+  }
+}
+
+// C (+)= sum over splits of the fragment-order partial tiles, in split order.  Blocks [0, tiles *
+// BM/16) reduce tile float4s (one per thread); the blocks after them reduce the bias sums.
+// TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
+template <int BM, bool TRANS>
+__global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ part, const float* __restrict__ sums,
+                                                      DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
+                                                      int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
+                                                      int sum_tiles, int sum_w) {
+  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
+  constexpr int Q = BM * 16;  // float4 per tile
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int64_t blk = blockIdx.x;
+  const int64_t tile_blocks = (int64_t)tiles * (Q / 256);
+  if (blk < tile_blocks) {
+    const int tile = (int)(blk / (Q / 256));
+    const int q = (int)(blk % (Q / 256)) * 256 + threadIdx.x;
+    const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int sp = 0;
+    for (; sp + 8 <= g.splits; sp += 8) {  // 8 independent loads in flight, added in split order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(sp + u) * Q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+      }
+    }
+    for (; sp < g.splits; ++sp) {
+      const float4 v = p[(int64_t)sp * Q];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const int lane = q & 63, f = q >> 6, j = f % FJ, i = (f / FJ) % FI, w = f / (FI * FJ);
+    const int mt = tile / g.tiles_n, nt = tile % g.tiles_n;
+    const int64_t n = (int64_t)nt * 64 + j * 16 + (lane & 15);
+    const int64_t mb = (int64_t)mt * BM + w * WM + i * 16 + (lane >> 4) * 4;
+    const float vv[4] = {s.x, s.y, s.z, s.w};
+    if (n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = mb + r;
+        if (m < M) {
+          float* dst = TRANS ? c + n * ldc + m : c + m * ldc + n;
+          *dst += vv[r];
+        }
+      }
+    }
+    return;
+  }
+  const int64_t e = (blk - tile_blocks) * 256 + threadIdx.x;  // element of the bias vector
+  if (e >= sum_len) return;
+  const int64_t st = e / sum_w, off = e % sum_w;
+  if (st >= sum_tiles) return;
+  const float* p = sums + st * (int64_t)g.splits * sum_w + off;
+  float s = 0.f;
+  for (int sp = 0; sp < g.splits; ++sp) s += p[(int64_t)sp * sum_w];
+  bias_out[e] += s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && v[0] ? atoi(v) : dflt;
+}
+
+// Cost model (microseconds): the workgroups stream their token slab of both operands (L2/HBM ->
+// LDS at ~80 GB/s per CU), then the partial tiles are written and re-read by the reduce (at ~5 TB/s
+// each way), plus the reduce launch.  Splits keep >= 8 token steps each.
+DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
+  DwPlan best = {};
+  best.valid = false;
+  const bool swap = M > N;
+  const int64_t Ma = swap ? N : M, Nb = swap ? M : N;
+  const int64_t nk = (K + 63) / 64;
+  const int force_bm = env_int("VSPIKE_DW_BM", 0);
+  double best_t = 1e30;
+  for (int BM : {64, 128, 192}) {
+    if (force_bm && BM != force_bm) continue;
+    const int64_t tm = (Ma + BM - 1) / BM, tn = (Nb + 63) / 64, tiles = tm * tn;
+    const int slots = BM == 64 ? 512 : 256;
+    int64_t S = slots / tiles;
+    if (S < 1) S = 1;
+    const int64_t smax = nk / 8 > 0 ? nk / 8 : 1;
+    if (S > smax) S = smax;
+    int64_t kps = (nk + S - 1) / S;
+    S = (nk + kps - 1) / kps;
+    const int64_t wgs = tiles * S;
+    const double per_wg = (double)kps * 64.0 * (BM + 64) * 2.0;
+    const double rate = BM == 64 ? 40e3 : 80e3;  // bytes / us per workgroup (2 or 1 per CU)
+    const double rounds = (double)((wgs + slots - 1) / slots);
+    const double part = (double)wgs * BM * 64 * 4.0;
+    const double t = rounds * per_wg / rate + 2.0 * part / 5e6 + 3.0 + (BM - Ma > 0 ? 0.0 : 0.0);
+    // wasted rows of the last A tile cost their share of the stream
+    const double waste = (double)(tm * BM - Ma) / (double)(tm * BM);
+    const double tt = t * (1.0 + 0.5 * waste);
+    if (tt < best_t) {
+      best_t = tt;
+      best.valid = true;
+      best.swap = swap;
+      best.BM = BM;
+      best.g.tiles_m = (int)tm;
+      best.g.tiles_n = (int)tn;
+      best.g.splits = (int)S;
+      best.g.ksteps = (int)kps;
+      best.part_floats = (int64_t)wgs * BM * 64;
+      best.sum_floats = (int64_t)S * (tm * BM > tn * 64 ? tm * BM : tn * 64);
+    }
+  }
+  return best;
+}
+
+size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  const DwPlan p = plan_dw(M, N, K);
+  if (!p.valid) return 0;
+  return (size_t)(p.part_floats + p.sum_floats + 64) * 4;
+}
+
+template <int BM, int SUMS, bool TRANS>
+static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* b, int64_t ldb, int64_t Nb, int64_t K,
+                        const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
+  const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
+  hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part, sums);
+  const int tiles = p.g.tiles_m * p.g.tiles_n;
+  const int64_t tile_blocks = (int64_t)tiles * (BM * 16 / 256);
+  int64_t sum_len = 0, sum_w = 1;
+  int sum_tiles = 0;
+  if (SUMS == 1) {
+    sum_w = BM;
+    sum_tiles = p.g.tiles_m;
+    sum_len = Ma;
+  } else if (SUMS == 2) {
+    sum_w = 64;
+    sum_tiles = p.g.tiles_n;
+    sum_len = Nb;
+  }
+  const int64_t blocks = tile_blocks + (sum_len + 255) / 256;
+  // C is [M][N] of the ORIGINAL product: with TRANS the kernel's (m, n) = (original n, original m)
+  hipLaunchKernelGGL((gemm_dw_reduce<BM, TRANS>), dim3((unsigned)blocks), dim3(256), 0, s, part, sums, p.g, Ma, Nb, c,
+                     ldc, bias, sum_len, sum_tiles, (int)sum_w);
+}
+
+int launch_dw(const vs_gemm_desc* d, hipStream_t s) {
+  const DwPlan p = plan_dw(d->M, d->N, d->K);
+  VS_REQUIRE(p.valid, "vs_gemm: no dW plan");
+  VS_REQUIRE((size_t)d->workspace_bytes >= dw_workspace_bytes(d->M, d->N, d->K), "vs_gemm: dW workspace too small");
+  float* part = (float*)d->workspace;
+  float* sums = part + p.part_floats;
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  float* c = (float*)d->c;
+  float* bias = d->a_rowsum;
+  // swap: A' = B (the narrow operand), B' = A; the bias (row sums of the ORIGINAL A) = column sums of B'
+  const bf16_t* aa = p.swap ? b : a;
+  const bf16_t* bb = p.swap ? a : b;
+  const int64_t la = p.swap ? d->ldb : d->lda, lb = p.swap ? d->lda : d->ldb;
+  const int64_t Ma = p.swap ? d->N : d->M, Nb = p.swap ? d->M : d->N;
+  const int sm = !bias ? 0 : (p.swap ? 2 : 1);
+#define DW_(BM_, S_, T_) launch_dw_t<BM_, S_, T_>(aa, la, Ma, bb, lb, Nb, d->K, p, part, sums, c, d->ldc, bias, s)
+#define DW_BM(BM_)                                  \
+  do {                                              \
+    if (p.swap) {                                   \
+      if (sm == 2) DW_(BM_, 2, true);               \
+      else DW_(BM_, 0, true);                       \
+    } else {                                        \
+      if (sm == 1) DW_(BM_, 1, false);              \
+      else DW_(BM_, 0, false);                      \
+    }                                               \
+  } while (0)
+  if (p.BM == 64) DW_BM(64);
+  else if (p.BM == 128) DW_BM(128);
+  else DW_BM(192);
+#undef DW_BM
+#undef DW_
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+}  // namespace vs
