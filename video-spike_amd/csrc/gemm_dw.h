@@ -15,6 +15,7 @@ struct DwGrid {
 
 struct DwPlan {
   bool valid, swap;  // swap: the kernel runs on (B, A) and stores C transposed
+  bool dma;          // LDS-DMA ring kernel (VSPIKE_DW_MODE=1) instead of register staging
   int BM;            // output rows per tile (64, 128 or 192); 64 columns
   DwGrid g;
   int64_t part_floats, sum_floats;

@@ -209,6 +209,149 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
   }
 }
 
+// The same product with REGISTER-staged operands: per 64-token step each thread loads (NA+1)*2
+// 16-B chunks with global_load_dwordx4 (a few issue cycles each, against ~60-180 for an LDS-DMA
+// piece, which made the DMA ring above issue-bound at ~26 GB/s per CU with one wave per SIMD),
+// two steps in flight in two register sets, written into a double-buffered LDS image one step
+// ahead of the MFMAs (guide T14: issue early, write late).  64 KB of LDS at BM = 192: two
+// workgroups per CU, 8 waves to hide the load latency.  Token rows past K load zeros.
+template <int BM, int SUMS>
+__global__ __launch_bounds__(256, 2) void gemm_dw_reg_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
+                                                             const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
+                                                             int64_t K, DwGrid g, float* __restrict__ part,
+                                                             float* __restrict__ sums) {
+  constexpr int NA = BM / 64;
+  constexpr int IMG = 8192;
+  constexpr int STAGE = (NA + 1) * IMG;
+  constexpr int CPT = (NA + 1) * 2;       // 16-B chunks per thread per step
+  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = t / tiles, rem = t % tiles, mt = rem / g.tiles_n, nt = rem % g.tiles_n;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * 64;
+  const int nk_all = (int)((K + 63) / 64);
+  const int ks0 = split * g.ksteps, ks1 = ks0 + g.ksteps < nk_all ? ks0 + g.ksteps : nk_all;
+  const int nk = ks1 - ks0;
+
+  // chunk c of this thread: image im = c / 2 (im == NA: B), index i = tid + 256 (c & 1):
+  // k = i / 8, 16-B column chunk q = i % 8 (one 128-B segment per 8 lanes)
+  const int kq0 = tid >> 3, q = tid & 7;  // i = tid (+256 -> k + 32)
+  auto load = [&](uint4 (&r)[CPT], int s) {
+    const int64_t k0 = (int64_t)(ks0 + s) * 64;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int im = c >> 1, k = kq0 + 32 * (c & 1);
+      const bf16_t* p = im < NA ? A : B;
+      const int64_t ld = im < NA ? lda : ldb;
+      const int64_t col = (im < NA ? m0 + im * 64 : n0) + q * 8;
+      const int64_t lim = im < NA ? M : N;
+      const bool ok = k0 + k < K && col < lim;
+      r[c] = ok ? *(const uint4*)(p + (k0 + k) * ld + col) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](const uint4 (&r)[CPT], char* stg) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int im = c >> 1, k = kq0 + 32 * (c & 1);
+      *(uint4*)(stg + im * IMG + k * 128 + ((q ^ dw_swz(k)) << 4)) = r[c];
+    }
+  };
+
+  f32x4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool sum_on = (SUMS == 1 && nt == 0) || (SUMS == 2 && mt == 0 && wid == 0);
+  float sacc[SUMS == 2 ? FJ : FI];
+#pragma unroll
+  for (int i = 0; i < (SUMS == 2 ? FJ : FI); ++i) sacc[i] = 0.f;
+
+  auto compute = [&](const char* stg) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[FI], bfr[FJ];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int r = wid * WM + i * 16;
+        af[i] = dw_frag(stg + (r >> 6) * IMG, r & 63, kk, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, j * 16, kk, lane);
+      if (sum_on) {
+        if constexpr (SUMS == 1) {
+#pragma unroll
+          for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int qq = 0; qq < 8; ++qq) sacc[i] += (float)af[i][qq];
+        } else if constexpr (SUMS == 2) {
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+#pragma unroll
+            for (int qq = 0; qq < 8; ++qq) sacc[j] += (float)bfr[j][qq];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  uint4 ra[CPT], rb[CPT];
+  if (nk > 0) load(ra, 0);
+  if (nk > 1) load(rb, 1);
+  if (nk > 0) store(ra, lds);                 // waits for step 0's loads only (compiler-counted)
+  if (nk > 2) load(ra, 2);
+  __syncthreads();
+  // step s computes from lds[s & 1]; meanwhile step s+1 (regs) is stored into the other half and
+  // step s+3 is loaded into the freed register set
+  auto step = [&](int s, uint4 (&cur)[CPT], uint4 (&nxt)[CPT]) {
+    compute(lds + (s & 1) * STAGE);
+    if (s + 1 < nk) store(cur, lds + ((s + 1) & 1) * STAGE);
+    if (s + 3 < nk) load(cur, s + 3);
+    __syncthreads();
+    (void)nxt;
+  };
+  for (int s = 0; s < nk; s += 2) {
+    step(s, rb, ra);
+    if (s + 1 < nk) step(s + 1, ra, rb);
+  }
+
+  float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * 64));
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const f32x4 v = acc[i][j];
+      pt[((wid * FI + i) * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  if (sum_on) {
+    constexpr int NS = SUMS == 2 ? FJ : FI;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      float v = sacc[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      sacc[i] = v;
+    }
+    if (lane < 16) {
+      if constexpr (SUMS == 1) {
+        float* so = sums + ((int64_t)mt * g.splits + split) * BM;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) so[wid * WM + i * 16 + lane] = sacc[i];
+      } else if constexpr (SUMS == 2) {
+        float* so = sums + ((int64_t)nt * g.splits + split) * 64;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) so[j * 16 + lane] = sacc[j];
+      }
+    }
+  }
+}
+
 // C (+)= sum over splits of the fragment-order partial tiles, in split order.  Blocks [0, tiles *
 // BM/16) reduce tile float4s (one per thread); the blocks after them reduce the bias sums.
 // TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
@@ -286,11 +429,12 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   const int64_t Ma = swap ? N : M, Nb = swap ? M : N;
   const int64_t nk = (K + 63) / 64;
   const int force_bm = env_int("VSPIKE_DW_BM", 0);
+  const bool dma = env_int("VSPIKE_DW_MODE", 0) == 1;
   double best_t = 1e30;
   for (int BM : {64, 128, 192}) {
     if (force_bm && BM != force_bm) continue;
     const int64_t tm = (Ma + BM - 1) / BM, tn = (Nb + 63) / 64, tiles = tm * tn;
-    const int slots = BM == 64 ? 512 : 256;
+    const int slots = (BM == 64 || !dma) ? 512 : 256;
     int64_t S = slots / tiles;
     if (S < 1) S = 1;
     const int64_t smax = nk / 8 > 0 ? nk / 8 : 1;
@@ -299,7 +443,7 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
     S = (nk + kps - 1) / kps;
     const int64_t wgs = tiles * S;
     const double per_wg = (double)kps * 64.0 * (BM + 64) * 2.0;
-    const double rate = BM == 64 ? 40e3 : 80e3;  // bytes / us per workgroup (2 or 1 per CU)
+    const double rate = slots == 512 ? 40e3 : 80e3;  // bytes / us per workgroup (2 or 1 per CU)
     const double rounds = (double)((wgs + slots - 1) / slots);
     const double part = (double)wgs * BM * 64 * 4.0;
     const double t = rounds * per_wg / rate + 2.0 * part / 5e6 + 3.0 + (BM - Ma > 0 ? 0.0 : 0.0);
@@ -309,6 +453,7 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
     if (tt < best_t) {
       best_t = tt;
       best.valid = true;
+      best.dma = dma;
       best.swap = swap;
       best.BM = BM;
       best.g.tiles_m = (int)tm;
@@ -332,7 +477,11 @@ template <int BM, int SUMS, bool TRANS>
 static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* b, int64_t ldb, int64_t Nb, int64_t K,
                         const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
   const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
-  hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part, sums);
+  if (p.dma)
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part, sums);
+  else
+    hipLaunchKernelGGL((gemm_dw_reg_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
+                       sums);
   const int tiles = p.g.tiles_m * p.g.tiles_n;
   const int64_t tile_blocks = (int64_t)tiles * (BM * 16 / 256);
   int64_t sum_len = 0, sum_w = 1;
