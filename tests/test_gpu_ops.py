@@ -176,6 +176,28 @@ def test_dw_kernel_every_tile_height(monkeypatch, bm, shape):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("shape", [(16, 64, 301056), (5, 48, 3200), (40, 16, 2048 + 96), (64, 64, 4096)])
+def test_skinny_splitk_kcontig(shape):
+    """The head's Linear(N*D -> 64) forward shape (M = clips, K = N*D): the skinny split-K kernel
+    loading MFMA fragments straight from HBM, partials summed in split order (bias once, C +=)."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=31).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=32, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=33).to(DEV)
+    nb = ops.splitk_workspace_bytes(torch.bfloat16, M, N, K)
+    ws = torch.empty(nb // 4 + 4, device=DEV)
+    outs = []
+    for _ in range(2):
+        c = torch.full((M, N), 0.25, device=DEV)
+        ops.gemm(x, w, c, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=K, ldb=K, ldc=N,
+                 epilogue=L.EPI_ATOMIC | L.EPI_BIAS, bias=bias, workspace=ws)
+        outs.append(c)
+    ref = x.double() @ w.double().t() + bias.double() + 0.25
+    assert rel(outs[0], ref) < 2e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_splitk_workspace_bias_once():
     from vspike import ops, _lib as L
     M, N, K = 96, 128, 20000

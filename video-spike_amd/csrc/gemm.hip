@@ -1267,6 +1267,19 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       !d->b_kcontig && d->split_k <= 0 && use_ws && d->K >= 1 && d->M % 8 == 0 && d->N % 8 == 0 &&
       d->lda % 8 == 0 && d->ldb % 8 == 0 && (size_t)d->workspace_bytes >= dw_workspace_bytes(d->M, d->N, d->K))
     return launch_dw(d, s);
+  // skinny split-K with K-contiguous operands (the head forward): fragments straight from HBM
+  static const int no_skinny = getenv_flag5("VSPIKE_NO_SKINNY");
+  const bool dense_c = d->ldc == d->N && aligned16(d->c) && (!(f & VS_EPI_BIAS) || aligned16(d->bias));
+  if (!no_skinny && use_ws && dense_c && skinny_ok(d) &&
+      (size_t)d->workspace_bytes >= skinny_workspace_bytes(d->M, d->N, d->K)) {
+    int S = 0;
+    VS_CALL(launch_skinny(d, s, &S));
+    const int64_t n4 = d->M * d->N / 4;
+    hipLaunchKernelGGL(gemm_splitk_reduce_wide, dim3((unsigned)n4), dim3(256), 0, s, (const float*)d->workspace, S, d->M,
+                       d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   const GemmPlan plan = plan_gemm(d->dtype, d->M, d->N, d->K, d->split_k, atomic_ok, use_ws ? d->workspace_bytes : 0);
   const GridMap& g = plan.g;
   if (use_ws && g.splits > 1) e.part = (float*)d->workspace;
@@ -1361,6 +1374,8 @@ extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64
   if (dtype == VS_BF16) {  // the dW kernel's partial tiles + bias sums (if this shape is a dW product)
     const size_t dw = dw_workspace_bytes(M, N, K);
     if (dw > b) b = dw;
+    const size_t sk = skinny_workspace_bytes(M, N, K);
+    if (sk > b) b = sk;
   }
   return b;
 }

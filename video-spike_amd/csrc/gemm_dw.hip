@@ -32,14 +32,16 @@ namespace vs {
 // KC=false> in gemm.hip (16-B chunk XOR on k, read back transposed by ds_read_tr16_b64).
 __device__ __forceinline__ int dw_swz(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 
-// LDS-DMA of one 8-KiB image: 8 pieces of 8 k-rows x 128 B; wave `wid` issues pieces 2wid, 2wid+1.
-// Columns past `cols` re-read the last 8 valid columns, token rows past `k_valid` re-read row
-// k_valid - 1 (finite data; those rows are zeroed in LDS before use, those columns never stored).
+// LDS-DMA of one 8-KiB image: 8 pieces of 8 k-rows x 128 B; with NW waves, wave `wid` issues
+// pieces wid * (8 / NW) ...  Columns past `cols` re-read the last 8 valid columns, token rows past
+// `k_valid` re-read row k_valid - 1 (finite data; those rows are zeroed in LDS before use, those
+// columns never stored).
+template <int NW>
 __device__ __forceinline__ void dw_dma(char* img, const bf16_t* __restrict__ p, int64_t ld, int64_t c0, int64_t cols,
                                        int64_t k0, int k_valid, int wid, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pi = wid * 2 + j;
+  for (int j = 0; j < 8 / NW; ++j) {
+    const int pi = wid * (8 / NW) + j;
     const int k = pi * 8 + (lane >> 3);
     const int c = (lane & 7) ^ dw_swz(k);
     const int64_t gc = c0 + c * 8 <= cols - 8 ? c0 + c * 8 : cols - 8;
@@ -66,23 +68,27 @@ __device__ __forceinline__ bf16x8 dw_frag(const char* img, int rb, int kk, int l
 
 // SUMS: 0 none; 1 row sums of A (the bias gradient when A is the dY operand), written by the
 // nt == 0 tiles; 2 column sums of B (when the host swapped the operands), by the mt == 0 tiles.
-template <int BM, int SUMS>
-__global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                                         int64_t M, const bf16_t* __restrict__ B,
-                                                                         int64_t ldb, int64_t N, int64_t K,
-                                                                         DwGrid g, float* __restrict__ part,
-                                                                         float* __restrict__ sums) {
+// NW = 8 waves (two per SIMD: one wave's DMA issue and LDS reads overlap its partner's MFMAs) in a
+// 4 x 2 grid of (BM/4) x 32 wave tiles, or NW = 4 in a 4 x 1 grid of (BM/4) x 64.
+// Partial tiles are stored in tile-fragment order: float4 ((rowfrag * 4 + colfrag) * 64 + lane),
+// rowfrag / colfrag = the 16-row / 16-column block within the BM x 64 tile.
+template <int BM, int SUMS, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
+                                                             const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
+                                                             int64_t K, DwGrid g, float* __restrict__ part,
+                                                             float* __restrict__ sums) {
   constexpr int NA = BM / 64;             // 64-row A images per stage
   constexpr int IMG = 8192;
   constexpr int STAGE = (NA + 1) * IMG;   // A images then the B image
-  constexpr int PER = (NA + 1) * 2;       // DMA wave-instructions per stage
-  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
+  constexpr int PER = (NA + 1) * (8 / NW);  // DMA wave-instructions per stage
+  constexpr int WM = BM / 4, FI = WM / 16, FJ = NW == 8 ? 2 : 4;
   __shared__ __attribute__((aligned(16))) char st0[STAGE];
   __shared__ __attribute__((aligned(16))) char st1[STAGE];
   __shared__ __attribute__((aligned(16))) char st2[STAGE];
   __shared__ __attribute__((aligned(16))) char st3[STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rw = wid & 3, cw = wid >> 2;  // wave tile: rows rw*WM.., columns cw*FJ*16..
   const int tiles = g.tiles_m * g.tiles_n;
   const int t = xcd_remap(blockIdx.x, gridDim.x);   // one token slab's tiles are consecutive: one XCD
   const int split = t / tiles, rem = t % tiles, mt = rem / g.tiles_n, nt = rem % g.tiles_n;
@@ -96,7 +102,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
   for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool sum_on = (SUMS == 1 && nt == 0) || (SUMS == 2 && mt == 0 && wid == 0);
+  const bool sum_on = (SUMS == 1 && nt == 0 && cw == 0) || (SUMS == 2 && mt == 0 && rw == 0);
   float sacc[SUMS == 2 ? FJ : FI];
 #pragma unroll
   for (int i = 0; i < (SUMS == 2 ? FJ : FI); ++i) sacc[i] = 0.f;
@@ -105,8 +111,8 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
     const int64_t k0 = (int64_t)(ks0 + s) * 64;
     const int kv = K - k0 < 64 ? (int)(K - k0) : 64;
 #pragma unroll
-    for (int a = 0; a < NA; ++a) dw_dma(stg + a * IMG, A, lda, m0 + a * 64, M, k0, kv, wid, lane);
-    dw_dma(stg + NA * IMG, B, ldb, n0, N, k0, kv, wid, lane);
+    for (int a = 0; a < NA; ++a) dw_dma<NW>(stg + a * IMG, A, lda, m0 + a * 64, M, k0, kv, wid, lane);
+    dw_dma<NW>(stg + NA * IMG, B, ldb, n0, N, k0, kv, wid, lane);
   };
   auto compute = [&](const char* stg) {
 #pragma unroll
@@ -114,11 +120,11 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
       bf16x8 af[FI], bfr[FJ];
 #pragma unroll
       for (int i = 0; i < FI; ++i) {
-        const int r = wid * WM + i * 16;  // r and r+15 lie in the same 64-row image (WM % 16 == 0)
+        const int r = rw * WM + i * 16;  // r and r+15 lie in the same 64-row image (WM % 16 == 0)
         af[i] = dw_frag(stg + (r >> 6) * IMG, r & 63, kk, lane);
       }
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, j * 16, kk, lane);
+      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, (cw * FJ + j) * 16, kk, lane);
       if (sum_on) {
         if constexpr (SUMS == 1) {
 #pragma unroll
@@ -142,7 +148,7 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
   auto zero_tail = [&](char* stg, int kv) {
     const int bytes = (64 - kv) * 128;
     for (int a = 0; a <= NA; ++a)
-      for (int o = tid * 16; o < bytes; o += 256 * 16) *(uint4*)(stg + a * IMG + kv * 128 + o) = make_uint4(0, 0, 0, 0);
+      for (int o = tid * 16; o < bytes; o += NW * 64 * 16) *(uint4*)(stg + a * IMG + kv * 128 + o) = make_uint4(0, 0, 0, 0);
   };
   auto step = [&](int s, auto sc) {
     constexpr int S = decltype(sc)::value;
@@ -176,14 +182,13 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // partial tile in fragment order: float4 q = ((wid*FI + i)*FJ + j)*64 + lane
   float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * 64));
 #pragma unroll
   for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const f32x4 v = acc[i][j];
-      pt[((wid * FI + i) * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
+      pt[((rw * FI + i) * 4 + cw * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
     }
   if (sum_on) {
     // lane groups g = lane >> 4 hold disjoint k; rows / columns (lane & 15)
@@ -199,11 +204,11 @@ __global__ __launch_bounds__(256, BM == 64 ? 2 : 1) void gemm_dw_kernel(const bf
       if constexpr (SUMS == 1) {
         float* so = sums + ((int64_t)mt * g.splits + split) * BM;
 #pragma unroll
-        for (int i = 0; i < FI; ++i) so[wid * WM + i * 16 + lane] = sacc[i];
+        for (int i = 0; i < FI; ++i) so[rw * WM + i * 16 + lane] = sacc[i];
       } else if constexpr (SUMS == 2) {
         float* so = sums + ((int64_t)nt * g.splits + split) * 64;
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) so[j * 16 + lane] = sacc[j];
+        for (int j = 0; j < FJ; ++j) so[(cw * FJ + j) * 16 + lane] = sacc[j];
       }
     }
   }
@@ -352,42 +357,51 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_reg_kernel(const bf16_t* __res
   }
 }
 
-// C (+)= sum over splits of the fragment-order partial tiles, in split order.  Blocks [0, tiles *
-// BM/16) reduce tile float4s (one per thread); the blocks after them reduce the bias sums.
-// TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
+// C (+)= sum over splits of the fragment-order partial tiles.  A workgroup owns 64 float4 of one
+// tile (one per lane); wave w sums splits w, w+4, ... (all loads of its share issued before the
+// adds), then the four wave sums are added in wave order through LDS — a fixed order that depends
+// only on the split count (bitwise reproducible).  Blocks after the tile blocks reduce the bias
+// sums.  TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
 template <int BM, bool TRANS>
 __global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ part, const float* __restrict__ sums,
                                                       DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
                                                       int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
                                                       int sum_tiles, int sum_w) {
-  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
   constexpr int Q = BM * 16;  // float4 per tile
   const int tiles = g.tiles_m * g.tiles_n;
   const int64_t blk = blockIdx.x;
-  const int64_t tile_blocks = (int64_t)tiles * (Q / 256);
+  const int64_t tile_blocks = (int64_t)tiles * (Q / 64);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (blk < tile_blocks) {
-    const int tile = (int)(blk / (Q / 256));
-    const int q = (int)(blk % (Q / 256)) * 256 + threadIdx.x;
+    __shared__ float4 red[4][64];
+    const int tile = (int)(blk / (Q / 64));
+    const int q = (int)(blk % (Q / 64)) * 64 + lane;
     const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    int sp = 0;
-    for (; sp + 8 <= g.splits; sp += 8) {  // 8 independent loads in flight, added in split order
+    for (int sp0 = w; sp0 < g.splits; sp0 += 4 * 8) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(sp + u) * Q];
+      for (int u = 0; u < 8; ++u) {
+        const int sp = sp0 + 4 * u;
+        v[u] = sp < g.splits ? p[(int64_t)sp * Q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
       }
     }
-    for (; sp < g.splits; ++sp) {
-      const float4 v = p[(int64_t)sp * Q];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    red[w][lane] = s;
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 o = red[k][lane];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
     }
-    const int lane = q & 63, f = q >> 6, j = f % FJ, i = (f / FJ) % FI, w = f / (FI * FJ);
+    const int f = q >> 6, rf = f >> 2, cf = f & 3;
     const int mt = tile / g.tiles_n, nt = tile % g.tiles_n;
-    const int64_t n = (int64_t)nt * 64 + j * 16 + (lane & 15);
-    const int64_t mb = (int64_t)mt * BM + w * WM + i * 16 + (lane >> 4) * 4;
+    const int64_t n = (int64_t)nt * 64 + cf * 16 + (lane & 15);
+    const int64_t mb = (int64_t)mt * BM + rf * 16 + (lane >> 4) * 4;
     const float vv[4] = {s.x, s.y, s.z, s.w};
     if (n < N) {
 #pragma unroll
@@ -412,6 +426,131 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Skinny split-K product with both operands K-contiguous: C[M,N] (+)= A[M,K] B[N,K]^T (+ bias), M <= 64,
+// N <= 64, K huge — the head's Linear(N*D -> 64) forward (src/model/videomae.py:13,29: M = batch,
+// K = 301,056 at the bench, 1.2 M at ViT-Base), HBM-bound on the 19-77 M-element weight.  Each
+// operand element is used by ONE wave, so the MFMA fragments are loaded straight from global memory
+// (16 B per lane: row = lane & 15, k = 8 (lane >> 4) .. +7 — the 16x16x32 operand layout), no LDS:
+// wave w of a workgroup takes 32-deep steps w, w+4, ... of the workgroup's K slice, U steps of loads
+// in flight.  The four wave tiles are added through LDS in wave order and the workgroup's f32 partial
+// [M][N] goes to the split-K workspace, summed in split order by gemm_splitk_reduce_wide (gemm.hip).
+template <int FI, int FJ>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
+                                                          const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
+                                                          int64_t K, int steps_per_split, float* __restrict__ part) {
+  constexpr int U = 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t nsteps = K / 32;
+  const int64_t s0 = (int64_t)blockIdx.x * steps_per_split;
+  const int64_t s1 = s0 + steps_per_split < nsteps ? s0 + steps_per_split : nsteps;
+  const int r = lane & 15, kq = 8 * (lane >> 4);
+  const bf16_t* ap[FI];
+  const bf16_t* bp[FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i) {
+    const int64_t row = i * 16 + r < M ? i * 16 + r : M - 1;  // rows past M: finite, never stored
+    ap[i] = A + row * lda + kq;
+  }
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int64_t row = j * 16 + r < N ? j * 16 + r : N - 1;
+    bp[j] = B + row * ldb + kq;
+  }
+  f32x4 acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t st = s0 + w; st < s1; st += 4 * U) {
+    bf16x8 a[U][FI], b[U][FJ];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = (st + 4 * u < s1 ? st + 4 * u : st) * 32;   // past the slice: re-read, not used
+#pragma unroll
+      for (int i = 0; i < FI; ++i) a[u][i] = *(const bf16x8*)(ap[i] + k);
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) b[u][j] = *(const bf16x8*)(bp[j] + k);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (st + 4 * u < s1) {
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // wave tiles -> LDS -> summed in wave order; C layout 16x16: acc[r4] at row 4 (lane >> 4) + r4, col lane & 15
+  __shared__ float red[4][FI * 16][FJ * 16 + 1];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) red[w][i * 16 + 4 * (lane >> 4) + r4][j * 16 + (lane & 15)] = acc[i][j][r4];
+  __syncthreads();
+  float* pt = part + (int64_t)blockIdx.x * M * N;
+  for (int e = tid; e < M * N; e += 256) {
+    const int m = (int)(e / N), n = (int)(e % N);
+    pt[e] = ((red[0][m][n] + red[1][m][n]) + red[2][m][n]) + red[3][m][n];
+  }
+}
+
+bool skinny_ok(const vs_gemm_desc* d) {
+  const uint32_t f = d->epilogue;
+  return d->dtype == VS_BF16 && d->out_dtype == VS_F32 && d->a_kcontig && d->b_kcontig && d->M >= 1 && d->M <= 64 &&
+         d->N >= 16 && d->N <= 64 && d->N % 16 == 0 && d->K >= 32 && d->K % 32 == 0 && d->lda % 8 == 0 &&
+         d->ldb % 8 == 0 && (f & VS_EPI_ATOMIC) && !(f & ~(uint32_t)(VS_EPI_ATOMIC | VS_EPI_BIAS)) && !d->a_rowsum &&
+         d->split_k <= 0 && d->K / 32 >= 64;
+}
+
+static int skinny_splits(int64_t K, int64_t* steps_per_split) {
+  const int64_t nsteps = K / 32;
+  int64_t S = nsteps / 32;               // >= 8 steps per wave
+  if (S > 1024) S = 1024;
+  if (S < 1) S = 1;
+  const int64_t sps = (nsteps + S - 1) / S;
+  *steps_per_split = sps;
+  return (int)((nsteps + sps - 1) / sps);
+}
+
+size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M < 1 || M > 64 || N > 64 || K % 32 != 0 || K / 32 < 64) return 0;
+  int64_t sps;
+  const int S = skinny_splits(K, &sps);
+  return (size_t)S * (size_t)(M * N) * 4;
+}
+
+int launch_skinny(const vs_gemm_desc* d, hipStream_t s, int* splits_out) {
+  int64_t sps;
+  const int S = skinny_splits(d->K, &sps);
+  VS_REQUIRE((size_t)d->workspace_bytes >= (size_t)S * (size_t)(d->M * d->N) * 4, "vs_gemm: skinny workspace too small");
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  float* part = (float*)d->workspace;
+  const int FI = (int)((d->M + 15) / 16), FJ = (int)(d->N / 16);
+#define SK_(I, J)                                                                                                  \
+  hipLaunchKernelGGL((gemm_skinny_kernel<I, J>), dim3((unsigned)S), dim3(256), 0, s, a, d->lda, d->M, b, d->ldb, d->N, \
+                     d->K, (int)sps, part)
+#define SK_J(I)              \
+  do {                       \
+    if (FJ == 1) SK_(I, 1);  \
+    else if (FJ == 2) SK_(I, 2); \
+    else if (FJ == 3) SK_(I, 3); \
+    else SK_(I, 4);          \
+  } while (0)
+  if (FI == 1) SK_J(1);
+  else if (FI == 2) SK_J(2);
+  else if (FI == 3) SK_J(3);
+  else SK_J(4);
+#undef SK_J
+#undef SK_
+  *splits_out = S;
+  return VS_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 static int env_int(const char* name, int dflt) {
@@ -429,7 +568,7 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   const int64_t Ma = swap ? N : M, Nb = swap ? M : N;
   const int64_t nk = (K + 63) / 64;
   const int force_bm = env_int("VSPIKE_DW_BM", 0);
-  const bool dma = env_int("VSPIKE_DW_MODE", 0) == 1;
+  const bool dma = env_int("VSPIKE_DW_MODE", 1) == 1;   // 1: 8-wave LDS-DMA ring (default), 0: register-staged
   double best_t = 1e30;
   for (int BM : {64, 128, 192}) {
     if (force_bm && BM != force_bm) continue;
@@ -478,12 +617,13 @@ static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* 
                         const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
   const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
   if (p.dma)
-    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part, sums);
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS, 8>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
+                       sums);
   else
     hipLaunchKernelGGL((gemm_dw_reg_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
                        sums);
   const int tiles = p.g.tiles_m * p.g.tiles_n;
-  const int64_t tile_blocks = (int64_t)tiles * (BM * 16 / 256);
+  const int64_t tile_blocks = (int64_t)tiles * (BM * 16 / 64);
   int64_t sum_len = 0, sum_w = 1;
   int sum_tiles = 0;
   if (SUMS == 1) {
