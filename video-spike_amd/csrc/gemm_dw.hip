@@ -363,30 +363,31 @@ __global__ __launch_bounds__(256, 2) void gemm_dw_reg_kernel(const bf16_t* __res
 // only on the split count (bitwise reproducible).  Blocks after the tile blocks reduce the bias
 // sums.  TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
 template <int BM, bool TRANS>
-__global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ part, const float* __restrict__ sums,
-                                                      DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
-                                                      int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
-                                                      int sum_tiles, int sum_w) {
+__global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__ part, const float* __restrict__ sums,
+                                                       DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
+                                                       int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
+                                                       int sum_tiles, int sum_w) {
   constexpr int Q = BM * 16;  // float4 per tile
+  constexpr int NWR = 16;     // waves per block: wave w sums splits w, w + 16, ... (<= 4 loads in flight each)
   const int tiles = g.tiles_m * g.tiles_n;
   const int64_t blk = blockIdx.x;
   const int64_t tile_blocks = (int64_t)tiles * (Q / 64);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (blk < tile_blocks) {
-    __shared__ float4 red[4][64];
+    __shared__ float4 red[NWR][64];
     const int tile = (int)(blk / (Q / 64));
     const int q = (int)(blk % (Q / 64)) * 64 + lane;
     const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp0 = w; sp0 < g.splits; sp0 += 4 * 8) {
-      float4 v[8];
+    for (int sp0 = w; sp0 < g.splits; sp0 += NWR * 4) {
+      float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int sp = sp0 + 4 * u;
+      for (int u = 0; u < 4; ++u) {
+        const int sp = sp0 + NWR * u;
         v[u] = sp < g.splits ? p[(int64_t)sp * Q] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 4; ++u) {
         s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
       }
     }
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ 
     __syncthreads();
     if (w != 0) return;
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < NWR; ++k) {  // fixed wave order
       const float4 o = red[k][lane];
       s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
     }
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce(const float* __restrict__ 
     }
     return;
   }
-  const int64_t e = (blk - tile_blocks) * 256 + threadIdx.x;  // element of the bias vector
+  const int64_t e = (blk - tile_blocks) * 1024 + threadIdx.x;  // element of the bias vector
   if (e >= sum_len) return;
   const int64_t st = e / sum_w, off = e % sum_w;
   if (st >= sum_tiles) return;
@@ -575,6 +576,8 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
     const int64_t tm = (Ma + BM - 1) / BM, tn = (Nb + 63) / 64, tiles = tm * tn;
     const int slots = (BM == 64 || !dma) ? 512 : 256;
     int64_t S = slots / tiles;
+    const int force_s = env_int("VSPIKE_DW_SPLITS", 0);
+    if (force_s > 0) S = force_s;
     if (S < 1) S = 1;
     const int64_t smax = nk / 8 > 0 ? nk / 8 : 1;
     if (S > smax) S = smax;
@@ -635,9 +638,9 @@ static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* 
     sum_tiles = p.g.tiles_n;
     sum_len = Nb;
   }
-  const int64_t blocks = tile_blocks + (sum_len + 255) / 256;
+  const int64_t blocks = tile_blocks + (sum_len + 1023) / 1024;
   // C is [M][N] of the ORIGINAL product: with TRANS the kernel's (m, n) = (original n, original m)
-  hipLaunchKernelGGL((gemm_dw_reduce<BM, TRANS>), dim3((unsigned)blocks), dim3(256), 0, s, part, sums, p.g, Ma, Nb, c,
+  hipLaunchKernelGGL((gemm_dw_reduce<BM, TRANS>), dim3((unsigned)blocks), dim3(1024), 0, s, part, sums, p.g, Ma, Nb, c,
                      ldc, bias, sum_len, sum_tiles, (int)sum_w);
 }
 

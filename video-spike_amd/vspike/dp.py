@@ -43,7 +43,7 @@ class GradExchange:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
-                    dist.broadcast(t.data, src=src, group=group)
+                    dist.broadcast(t.detach(), src=src, group=group)   # versioned write (bf16 shadows recast)
         if hasattr(model, "grad_sink"):
             model.grad_sink = self
             self._sunk = {id(model.enc_flat), id(model.head_flat)} if hasattr(model, "enc_flat") else set()

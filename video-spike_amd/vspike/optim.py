@@ -1,6 +1,8 @@
 """Fused AdamW — torch.optim.AdamW semantics (src/train.py:44-49) in one HIP pass per parameter.
 
-A drop-in `torch.optim.Optimizer`: `param_groups[i]['lr']` is honoured, so torch's OneCycleLR
+A drop-in `torch.optim.Optimizer`.  Parameters with a registered bf16 shadow (LP_SHADOWS) get it
+rewritten in the same pass (2 more bytes per parameter instead of a separate 6-byte cast pass).
+ `param_groups[i]['lr']` is honoured, so torch's OneCycleLR
 (src/train.py:50-57) drives it unchanged.  Hyper-parameters travel in a small device tensor
 (lr, beta1, beta2, eps, wd, step, grad_scale) so the update never syncs the host; `grad_scale`
 folds the data-parallel 1/world average into the same pass.  All parameters' rows are staged in
@@ -9,9 +11,26 @@ one pinned host block and sent with one asynchronous copy per device per step (a
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import ops
+
+# Low-precision shadows of parameters (registered by the plugins, vspike.vit): FusedAdamW writes the
+# bf16 copy of each updated parameter in the same pass (vs_adamw `param_lp`), so the next forward
+# does not re-cast the f32 master weights.  param -> (shadow tensor, stamp dict); stamp["key"] is
+# (data_ptr, _version) of the parameter the shadow was last made from — any autograd-visible in-place
+# write to the parameter bumps _version and makes the forward cast again.
+LP_SHADOWS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def register_lp_shadow(param: torch.Tensor, shadow: torch.Tensor, stamp: dict) -> None:
+    LP_SHADOWS[param] = (shadow, stamp)
+
+
+def lp_key(param: torch.Tensor):
+    return (param.data_ptr(), param._version)
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -50,5 +69,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 g = p.grad
                 if g.dtype != torch.float32 or not g.is_contiguous():
                     g = g.float().contiguous()
-                ops.adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], hyper[k])
+                ent = LP_SHADOWS.get(p)
+                lp = ent[0] if ent is not None and ent[0].device == p.device and ent[0].numel() == p.numel() else None
+                ops.adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], hyper[k], param_lp=lp)
+                if lp is not None:
+                    ent[1]["key"] = lp_key(p)
         return loss

@@ -28,6 +28,7 @@ from . import _lib as L
 from . import ops
 from .layout import BackboneCfg, VitLayout, modern_name
 from .memory import Arena
+from .optim import lp_key, register_lp_shadow
 
 # Side-stream joins of the block backward.  A join at every block end costs a ~24 us cross-queue
 # stall per block (the main stream waits on the dWqkv product, which the side stream finishes last).
@@ -190,7 +191,7 @@ class VideoMAE(nn.Module):
         st = super().__getstate__() if hasattr(super(), "__getstate__") else self.__dict__.copy()
         st = dict(st)
         st["_pos_cache"] = {}
-        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains"):
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains", "_lp"):
             st.pop(k, None)
         st["grad_sink"] = None
         return st
@@ -226,10 +227,36 @@ class VideoMAE(nn.Module):
 
     def _caches(self):
         d = self.__dict__
-        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains"):
+        for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains", "_lp"):
             if k not in d:
                 d[k] = {}
         return d["_fwd_cache"], d["_bwd_cache"], d["_gs_cache"]
+
+    def _lp_shadows(self, dev):
+        """Persistent bf16 shadows of the two flat parameter buffers on `dev` (one per device, shared
+        by every cached forward arena), registered with FusedAdamW so the optimizer step rewrites
+        them.  NB: an optimizer step between a forward and ITS backward would change the weights the
+        backward uses (the reference's loop never does that: base.py:144-159)."""
+        self._caches()
+        sh = self.__dict__["_lp"]
+        key = str(dev)
+        if key not in sh:
+            dt = self.compute_dtype
+            ent = {}
+            for name, p in (("enc", self.enc_flat), ("head", self.head_flat)):
+                t = torch.empty(p.numel(), dtype=dt, device=dev)
+                stamp = {}
+                register_lp_shadow(p, t, stamp)
+                ent[name] = (t, stamp)
+            sh[key] = ent
+        return sh[key]
+
+    def invalidate_lp(self):
+        """Force the next forward to re-cast the bf16 shadows (after writing parameters through
+        `.data`, which torch does not version)."""
+        for ent in self.__dict__.get("_lp", {}).values():
+            for _, stamp in ent.values():
+                stamp.clear()
 
     def _chain(self, dev):
         """This model's vs_bwd_chain on `dev`: the side stream and deferred-join state of its
@@ -268,16 +295,16 @@ class VideoMAE(nn.Module):
             ar.add(f"X{j}", (M, D), torch.float32)
         if lp:
             ar.add("x_lp", (B, N * D), dt)
-            ar.add("enc_lp", (enc32.numel(),), dt)
-            ar.add("head_lp", (head32.numel(),), dt)
         ar.add("z", (B, self.layout.enc_out), torch.float32)
         # split-K over the N*D = 301,056-long reduction; partials summed in order (deterministic)
         hws = ops.splitk_workspace_bytes(dt, B, self.layout.enc_out, N * D)
         if hws:
             ar.add("head_ws", (hws // 4 + 4,), torch.float32)
         act = ar.allocate(dev)
-        enc_lp = act["enc_lp"] if lp else enc32
-        head_lp = act["head_lp"] if lp else head32
+        if lp:
+            enc_lp, head_lp = self._lp_shadows(dev)["enc"][0], self._lp_shadows(dev)["head"][0]
+        else:
+            enc_lp, head_lp = enc32, head32
         x = act["x0"]
         structs = []
         for i in range(Lyr):
@@ -302,8 +329,13 @@ class VideoMAE(nn.Module):
         ent = self._fwd_buffers(B, dev, save_encoder)
         act, enc_lp, head_lp = ent["act"], ent["enc_lp"], ent["head_lp"]
         if dt != torch.float32:
-            ops.cast(enc32, enc_lp)
-            ops.cast(head32, head_lp)
+            # bf16 shadows: FusedAdamW rewrites them with each update (vs_adamw param_lp); cast only
+            # when the master weights changed some other way (load, init, a user's in-place write)
+            sh = self._lp_shadows(dev)
+            for p, (shadow, stamp) in ((self.enc_flat, sh["enc"]), (self.head_flat, sh["head"])):
+                if stamp.get("key") != lp_key(p):
+                    ops.cast(p.detach(), shadow)
+                    stamp["key"] = lp_key(p)
 
         ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
         ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
