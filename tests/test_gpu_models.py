@@ -276,3 +276,51 @@ def test_deferred_side_stream_joins_give_identical_grads(mode):
     finally:
         V._DEFER = old
     assert (grads[0] - grads[mode]).norm().item() <= 1e-5 * grads[0].norm().item()
+
+
+def test_bf16_shadows_written_by_fused_adamw():
+    """FusedAdamW rewrites the bf16 weight shadows in its update pass (vs_adamw param_lp): after
+    each step they equal the rounded master weights, and an autograd-visible in-place write to a
+    parameter makes the next forward re-cast."""
+    from vspike import FusedAdamW, poisson_nll_mean
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n, dtype="bf16")
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=0.01)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    for _ in range(2):
+        poisson_nll_mean(m(px), y).backward()
+        opt.step()
+        opt.zero_grad()
+        sh = m._lp_shadows(torch.device(DEV))
+        assert torch.equal(sh["enc"][0], m.enc_flat.detach().to(torch.bfloat16))
+        assert torch.equal(sh["head"][0], m.head_flat.detach().to(torch.bfloat16))
+    with torch.no_grad():
+        m.head_flat.mul_(0.5)
+    out = m(px)
+    assert torch.equal(sh["head"][0], m.head_flat.detach().to(torch.bfloat16))
+    m2 = _vit_model(cfg, 64, n, dtype="bf16")
+    with torch.no_grad():
+        m2.enc_flat.copy_(m.enc_flat)
+        m2.head_flat.copy_(m.head_flat)
+    assert torch.equal(out, m2(px))
+
+
+def test_bf16_backward_bitwise_reproducible():
+    """Every reduction of the bf16 train step sums in a fixed order (split-K dW partials and bias
+    sums, the head dZ split-K, LayerNorm dgamma/dbeta partial rows, the loss): two backward passes
+    from the same state give bit-identical gradients (hidden 192: the vectorised LayerNorm path)."""
+    from vspike import poisson_nll_mean
+    cfg = cpu_ref.ViTCfg(image_size=112, num_frames=8, hidden_size=192, num_hidden_layers=2,
+                         num_attention_heads=3, intermediate_size=768)
+    B, n = 2, 16
+    m = _vit_model(cfg, 64, n, dtype="bf16")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    grads = []
+    for _ in range(3):
+        m.zero_grad(set_to_none=True)
+        poisson_nll_mean(m(px), y).backward()
+        grads.append((m.enc_flat.grad.clone(), m.head_flat.grad.clone()))
+    for g in grads[1:]:
+        assert torch.equal(g[0], grads[0][0]) and torch.equal(g[1], grads[0][1])

@@ -325,15 +325,15 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
   }
 }
 
-// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][cols + c].  Grid (column blocks of 64,
-// 16 row groups): each thread sums nblk/64 partial rows with 8 loads in flight, the 4 row groups
-// of a block meet in LDS, and the 16 blocks of a column add with one f32 atomic each.  (One block
-// per 64 columns summing all rows serially took 32 us for D = 192.)
-__global__ __launch_bounds__(256) void ln_partsum_kernel(const float* __restrict__ part, int nblk, int cols,
-                                                         float* __restrict__ dg, float* __restrict__ db) {
-  __shared__ float red[4][64];
+// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][cols + c].  One block of 16 waves per 64
+// columns: wave w sums partial rows w, w+16, ... with 8 loads in flight, the 16 wave sums meet in
+// LDS in wave order: a fixed order (bitwise reproducible; the previous 16-block version finished
+// with one f32 atomic per block and column, in arrival order).
+__global__ __launch_bounds__(1024) void ln_partsum_kernel(const float* __restrict__ part, int nblk, int cols,
+                                                          float* __restrict__ dg, float* __restrict__ db) {
+  __shared__ float red[16][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = 2 * cols;
-  const int grp = blockIdx.y * 4 + (threadIdx.x >> 6), ngrp = gridDim.y * 4;
+  const int grp = threadIdx.x >> 6, ngrp = 16;
   float acc = 0.f;
   if (c < w) {
     int b = grp;
@@ -346,12 +346,14 @@ __global__ __launch_bounds__(256) void ln_partsum_kernel(const float* __restrict
     }
     for (; b < nblk; b += ngrp) acc += part[(int64_t)b * w + c];
   }
-  red[threadIdx.x >> 6][threadIdx.x & 63] = acc;
+  red[grp][threadIdx.x & 63] = acc;
   __syncthreads();
   if (threadIdx.x < 64 && c < w) {
-    const float v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
-    if (c < cols) unsafeAtomicAdd(dg + c, v);
-    else unsafeAtomicAdd(db + c - cols, v);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][threadIdx.x];
+    if (c < cols) dg[c] += v;
+    else db[c - cols] += v;
   }
 }
 
@@ -467,7 +469,7 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
     if (lpr == 16) BV_(16); else if (lpr == 32) BV_(32); else BV_(64);
 #undef BV_
     if (part)
-      hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 64), 16), dim3(256), 0, s, part, (int)grid,
+      hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 64)), dim3(1024), 0, s, part, (int)grid,
                          (int)cols, dgamma, dbeta);
     VS_LAUNCH_CHECK();
     return VS_OK;

@@ -19,14 +19,23 @@ from . import ops
 
 # Low-precision shadows of parameters (registered by the plugins, vspike.vit): FusedAdamW writes the
 # bf16 copy of each updated parameter in the same pass (vs_adamw `param_lp`), so the next forward
-# does not re-cast the f32 master weights.  param -> (shadow tensor, stamp dict); stamp["key"] is
-# (data_ptr, _version) of the parameter the shadow was last made from — any autograd-visible in-place
-# write to the parameter bumps _version and makes the forward cast again.
-LP_SHADOWS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# does not re-cast the f32 master weights.  id(param) -> (weakref(param), shadow tensor, stamp dict);
+# stamp["key"] is (data_ptr, _version) of the parameter the shadow was last made from — any
+# autograd-visible in-place write to the parameter bumps _version and makes the forward cast again.
+# (Keyed by id: a WeakKeyDictionary compares tensor keys with ==, which is elementwise.)
+LP_SHADOWS: dict = {}
 
 
 def register_lp_shadow(param: torch.Tensor, shadow: torch.Tensor, stamp: dict) -> None:
-    LP_SHADOWS[param] = (shadow, stamp)
+    pid = id(param)
+    LP_SHADOWS[pid] = (weakref.ref(param, lambda _r, pid=pid: LP_SHADOWS.pop(pid, None)), shadow, stamp)
+
+
+def lp_shadow(param: torch.Tensor):
+    ent = LP_SHADOWS.get(id(param))
+    if ent is None or ent[0]() is not param:
+        return None
+    return ent[1], ent[2]
 
 
 def lp_key(param: torch.Tensor):
@@ -69,7 +78,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 g = p.grad
                 if g.dtype != torch.float32 or not g.is_contiguous():
                     g = g.float().contiguous()
-                ent = LP_SHADOWS.get(p)
+                ent = lp_shadow(p)
                 lp = ent[0] if ent is not None and ent[0].device == p.device and ent[0].numel() == p.numel() else None
                 ops.adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], hyper[k], param_lp=lp)
                 if lp is not None:

@@ -397,6 +397,12 @@ class VideoMAE(nn.Module):
                     ar.add(k, (M, D), dt)
                 ar.add("dz_lp", (B, lay.enc_out), dt)
             ar.add("attn_ws", (ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64,), torch.float32)
+            # head dZ = dr dec_w over K = 100 * neurons: split-K partials summed in a fixed order
+            ar.add("dz_ws", (max(ops.splitk_workspace_bytes(torch.float32, B, lay.enc_out, lay.out_dim), 16) // 4 + 64,),
+                   torch.float32)
+            pws = ops.splitk_workspace_bytes(dt, D, cfg.patch_dim, M)
+            if pws:
+                ar.add("patch_ws", (pws // 4 + 64,), torch.float32)
             ar.add("ln_ws", (ops.layernorm_bwd_workspace_bytes(B * N, D) // 4 + 64,), torch.float32)
             gws = max(ops.splitk_workspace_bytes(dt, m, n, M) for m, n in ((D, F), (F, D), (D, D), (3 * D, D)))
             ar.add("gemm_ws", (gws // 4 + 64,), torch.float32)
@@ -408,7 +414,8 @@ class VideoMAE(nn.Module):
         z = act["z"]
         dz = g["dz"]
         dz.zero_()
-        ops.linear_dx(dr, lh.view(head32, "dec_w"), dz, accumulate=True)     # K = 100*neurons: split-K
+        ops.linear_dx(dr, lh.view(head32, "dec_w"), dz, accumulate=True,     # K = 100*neurons: split-K,
+                      workspace=g["dz_ws"])                                  # fixed-order partial sums
         if lp:
             dz_lp = g["dz_lp"]
             ops.cast(dz, dz_lp)
@@ -476,9 +483,8 @@ class VideoMAE(nn.Module):
         if prev is not None:
             self._ready(self.enc_flat, *lay.layer_ranges[prev])
         # patch embedding: dW = dx0^T cols, db = colsum(dx0); the position table is fixed
-        if lp:
-            ops.linear_dw(dx_lp, act["cols"], Ge("patch_w"))
-            ops.colsum(dx, Ge("patch_b"))                    # from the f32 gradient, not its bf16 copy
+        if lp:   # bias gradient fused as row sums of dx^T (fixed-order, like every block's dW)
+            ops.linear_dw(dx_lp, act["cols"], Ge("patch_w"), db=Ge("patch_b"), workspace=g.get("patch_ws"))
         else:
             ops.linear_dw(dx, act["cols"], Ge("patch_w"), db=Ge("patch_b"))
         self._ready(self.enc_flat, 0, lay.layer_ranges[0][0] if lay.layer_ranges else self.enc_flat.numel())
