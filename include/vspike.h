@@ -62,7 +62,9 @@ int vs_struct_size(int which);
 #define VS_EPI_POS       0x010u  /* + pos[(m % pos_rows)*N + n] (f32)                          */
 #define VS_EPI_GELU_BWD  0x020u  /* v *= gelu_erf'(aux_in(m,n))                                */
 #define VS_EPI_RELU_BWD  0x040u  /* v = aux_in(m,n) > 0 ? v : 0                                */
-#define VS_EPI_ATOMIC    0x080u  /* C(m,n) += v by f32 atomics (split-K); C must be f32       */
+#define VS_EPI_ATOMIC    0x080u  /* C(m,n) += v (split-K); C must be f32.  With a workspace the  */
+                                 /* splits are summed in a fixed order (no atomics); with RELU  */
+                                 /* (skinny path only) C = relu(C + v)                          */
 #define VS_EPI_ACCUM     0x100u  /* C(m,n) += v (plain read-modify-write); C must be f32      */
 
 typedef struct vs_gemm_desc {

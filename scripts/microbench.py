@@ -109,6 +109,23 @@ def main():
         report("attn fwd", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps), M * 4 * D * 2, f)
         report("attn bwd (delta+dkdv+dq)", timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps),
                M * 8 * D * 2, 2.5 * f)
+    if a.only in ("", "linear"):
+        # Linear plugin first layer at the real linear_video geometry (K = 120*128*128), f32, B = 4
+        Bn, K, Nout = 4, 120 * 128 * 128, 256
+        xf = torch.randn(Bn, K, device=dev)
+        wf = torch.randn(Nout, K, device=dev) * K ** -0.5
+        bf_ = torch.zeros(Nout, device=dev)
+        yf = torch.zeros(Bn, Nout, device=dev)
+        nb = ops.splitk_workspace_bytes(torch.float32, Bn, Nout, K)
+        wsf = torch.empty(nb // 4 + 4, device=dev)
+        report("linear_video L0 fwd (skinny f32)", timeit(lambda: ops.gemm(
+            xf, wf, yf, M=Bn, N=Nout, K=K, a_kcontig=True, b_kcontig=True, lda=K, ldb=K, ldc=Nout,
+            epilogue=L.EPI_ATOMIC | L.EPI_BIAS, bias=bf_, workspace=wsf), a.reps), (Bn + Nout) * K * 4, 2 * Bn * Nout * K)
+        dyf = torch.randn(Bn, Nout, device=dev)
+        dwf = torch.empty(Nout, K, device=dev)
+        dbf = torch.zeros(Nout, device=dev)
+        report("linear_video L0 dW (f32 stores)", timeit(lambda: ops.linear_dw(dyf, xf, dwf, db=dbf, accumulate=False),
+                                                        a.reps), (Bn + Nout) * K * 4 + Bn * K * 4, 2 * Bn * Nout * K)
     if a.only in ("", "ln"):
         x = r(M, D, dt=torch.float32)
         g, b = r(D, dt=torch.float32) + 1, r(D, dt=torch.float32)

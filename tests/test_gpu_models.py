@@ -324,3 +324,42 @@ def test_bf16_backward_bitwise_reproducible():
         grads.append((m.enc_flat.grad.clone(), m.head_flat.grad.clone()))
     for g in grads[1:]:
         assert torch.equal(g[0], grads[0][0]) and torch.equal(g[1], grads[0][1])
+
+
+def test_linear_video_real_first_layer():
+    """§8(f) row 4: the Linear plugin at the real `linear_video` geometry (config/model/
+    linear_video.yaml: 120 frames x 128 x 128 -> K = 1,966,080, a 503 M-parameter first layer),
+    B = 2 clips: forward (skinny split-K) and every gradient against an fp64 reference of the same
+    math (src/model/linear.py:10-56) on the device.  Tolerances: the fp32 north star (1e-4 of
+    max|ref| on log-rates, 1e-3 of the norm on gradients)."""
+    from vspike import Linear, poisson_nll_mean
+    n = 16
+    conf = {"model_class": "Linear",
+            "encoder": {"input_dim": 120 * 128 * 128, "hidden_dims": [256, 128], "output_dim": 64, "layer_num": 2},
+            "decoder": {"input_dim": 64, "hidden_dims": [128, 256], "output_dim": 100 * n, "layer_num": 2}}
+    torch.manual_seed(5)
+    m = Linear(conf).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    video = torch.randint(0, 256, (2, 120, 1, 128, 128), device=DEV, generator=g).float()
+    y = torch.poisson(torch.full((2, 100, n), 0.3, device=DEV), generator=g)
+    out = m(video)
+    loss = poisson_nll_mean(out, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    # fp64 reference of linear.py:10-15 (ReLU between hidden layers only)
+    ps = {k: p.detach().double().requires_grad_() for k, p in m.named_parameters()}
+    h = video.flatten(1).double()
+    for stack in ("encoder", "decoder"):
+        idx = sorted(int(k.split(".")[2]) for k in ps if k.startswith(stack) and k.endswith(".weight"))
+        for j, i in enumerate(idx):
+            h = h @ ps[f"{stack}.layers.{i}.weight"].t() + ps[f"{stack}.layers.{i}.bias"]
+            if j < len(idx) - 1:
+                h = torch.relu(h)
+    ref = h.reshape(2, 100, n)
+    rl = (torch.exp(ref) - y.double() * ref).mean()
+    rl.backward()
+    assert float((out.double() - ref).abs().max() / ref.abs().max()) < 1e-4
+    assert abs(loss.item() - rl.item()) < 1e-5 * abs(rl.item())
+    for k, p in m.named_parameters():
+        err = float((p.grad.double() - ps[k].grad).norm() / ps[k].grad.norm())
+        assert err < 1e-3, (k, err)

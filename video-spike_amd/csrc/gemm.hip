@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
 // adds the 256 partial sums (deterministic: the order depends only on `splits`).
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_wide(const float* __restrict__ part, int splits, int64_t M,
                                                                int64_t N, float* __restrict__ c, int64_t ldc,
-                                                               const float* __restrict__ bias) {
+                                                               const float* __restrict__ bias, int relu = 0) {
   __shared__ float4 red[256];
   const int64_t MN = M * N;
   const int64_t e4 = (int64_t)blockIdx.x * 4;
@@ -1103,6 +1103,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_wide(const float* __re
     float4* dst = (float4*)(c + m * ldc + n);
     float4 o = *dst;
     o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+    if (relu) {  // VS_EPI_ATOMIC | VS_EPI_RELU on the skinny path: C = relu(C + sum)
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
     *dst = o;
   }
 }
@@ -1240,8 +1243,8 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   VS_REQUIRE(!(f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) || d->aux_in, "vs_gemm: *_BWD needs aux_in");
   VS_REQUIRE(!(f & VS_EPI_GELU) || d->aux_out, "vs_gemm: GELU needs aux_out");
   VS_REQUIRE(!(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM)) || d->out_dtype == VS_F32, "vs_gemm: ATOMIC/ACCUM need f32 C");
-  VS_REQUIRE(!((f & VS_EPI_ATOMIC) && (f & ~(VS_EPI_ATOMIC | VS_EPI_BIAS))),
-             "vs_gemm: ATOMIC combines with BIAS only");
+  VS_REQUIRE(!((f & VS_EPI_ATOMIC) && (f & ~(VS_EPI_ATOMIC | VS_EPI_BIAS | VS_EPI_RELU))),
+             "vs_gemm: ATOMIC combines with BIAS (and RELU on the skinny split-K path) only");
   VS_REQUIRE(d->split_k <= 1 || (f & VS_EPI_ATOMIC), "vs_gemm: split_k > 1 needs VS_EPI_ATOMIC");
 
   EpiParams e;
@@ -1270,13 +1273,16 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   // skinny split-K with K-contiguous operands (the head forward): fragments straight from HBM
   static const int no_skinny = getenv_flag5("VSPIKE_NO_SKINNY");
   const bool dense_c = d->ldc == d->N && aligned16(d->c) && (!(f & VS_EPI_BIAS) || aligned16(d->bias));
-  if (!no_skinny && use_ws && dense_c && skinny_ok(d) &&
-      (size_t)d->workspace_bytes >= skinny_workspace_bytes(d->M, d->N, d->K)) {
+  const bool skinny = !no_skinny && use_ws && dense_c && skinny_ok(d) &&
+                      (size_t)d->workspace_bytes >= skinny_workspace_bytes(d->dtype, d->M, d->N, d->K);
+  VS_REQUIRE(skinny || !((f & VS_EPI_ATOMIC) && (f & VS_EPI_RELU)),
+             "vs_gemm: ATOMIC|RELU needs the skinny split-K path (M <= 64, N <= 256, K-contiguous, workspace)");
+  if (skinny) {
     int S = 0;
     VS_CALL(launch_skinny(d, s, &S));
     const int64_t n4 = d->M * d->N / 4;
     hipLaunchKernelGGL(gemm_splitk_reduce_wide, dim3((unsigned)n4), dim3(256), 0, s, (const float*)d->workspace, S, d->M,
-                       d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr);
+                       d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, (f & VS_EPI_RELU) ? 1 : 0);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
@@ -1374,9 +1380,9 @@ extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64
   if (dtype == VS_BF16) {  // the dW kernel's partial tiles + bias sums (if this shape is a dW product)
     const size_t dw = dw_workspace_bytes(M, N, K);
     if (dw > b) b = dw;
-    const size_t sk = skinny_workspace_bytes(M, N, K);
-    if (sk > b) b = sk;
   }
+  const size_t sk = skinny_workspace_bytes(dtype, M, N, K);   // skinny split-K (head / Linear layer 0)
+  if (sk > b) b = sk;
   return b;
 }
 

@@ -25,9 +25,9 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
 size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int launch_dw(const vs_gemm_desc* d, hipStream_t s);
 
-// skinny split-K (M, N <= 64, both operands K-contiguous): partials [splits][M][N] in the workspace
+// skinny split-K (M <= 64, N <= 256, both operands K-contiguous, bf16 or f32): partials [splits][M][N] in the workspace
 bool skinny_ok(const vs_gemm_desc* d);
-size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K);
+size_t skinny_workspace_bytes(int32_t dtype, int64_t M, int64_t N, int64_t K);
 int launch_skinny(const vs_gemm_desc* d, hipStream_t s, int* splits_out);
 
 }  // namespace vs

@@ -22,6 +22,7 @@
 //     chip's rate, few enough that the partial tiles (#workgroups x tile bytes) stay a small
 //     fraction of the operand bytes.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "gemm_dw.h"
@@ -435,26 +436,35 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Skinny split-K product with both operands K-contiguous: C[M,N] (+)= A[M,K] B[N,K]^T (+ bias), M <= 64,
-// N <= 64, K huge — the head's Linear(N*D -> 64) forward (src/model/videomae.py:13,29: M = batch,
-// K = 301,056 at the bench, 1.2 M at ViT-Base), HBM-bound on the 19-77 M-element weight.  Each
-// operand element is used by ONE wave, so the MFMA fragments are loaded straight from global memory
-// (16 B per lane: row = lane & 15, k = 8 (lane >> 4) .. +7 — the 16x16x32 operand layout), no LDS:
-// wave w of a workgroup takes 32-deep steps w, w+4, ... of the workgroup's K slice, U steps of loads
-// in flight.  The four wave tiles are added through LDS in wave order and the workgroup's f32 partial
+// Skinny split-K product with both operands K-contiguous: C[M,N] (+)= A[M,K] B[N,K]^T (+ bias),
+// M <= 64, N <= 256, K huge — the head's Linear(N*D -> 64) forward (src/model/videomae.py:13,29:
+// M = batch, K = 301,056 at the bench, 1.2 M at ViT-Base) and the Linear plugin's first layer
+// (src/model/linear.py:26: K = 120*128*128 = 1,966,080, a 503 M-parameter f32 weight), both
+// HBM-bound on the weight.  Each operand element is used by ONE wave, so the MFMA fragments are
+// loaded straight from global memory, no LDS: per 16-B load a lane holds
+//   bf16: 8 consecutive k of row (lane & 15) at k0 + 8 (lane >> 4)  (the 16x16x32 operand layout);
+//   f32:  4 consecutive k at k0 + 4 (lane >> 4), consumed by 4 exact-f32 16x16x4 MFMAs, MFMA j
+//         taking element j (a fixed permutation of the k order inside each 16-deep step, the same
+//         for A and B: it changes only the f32 summation order).
+// Wave w of a workgroup takes steps w, w+4, ... of the workgroup's K slice with U steps of loads in
+// flight; the four wave tiles are added through LDS in wave order and the workgroup's f32 partial
 // [M][N] goes to the split-K workspace, summed in split order by gemm_splitk_reduce_wide (gemm.hip).
-template <int FI, int FJ>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
-                                                          const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
+template <typename T, int FI, int FJ>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const T* __restrict__ A, int64_t lda, int64_t M,
+                                                          const T* __restrict__ B, int64_t ldb, int64_t N,
                                                           int64_t K, int steps_per_split, float* __restrict__ part) {
-  constexpr int U = 4;
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int KS = BF ? 32 : 16;               // k per step
+  constexpr int U = FJ <= 4 ? 4 : 2;             // steps of loads in flight per wave
+  typedef __attribute__((ext_vector_type(4))) float f32v4;
+  typedef typename std::conditional<BF, bf16x8, f32v4>::type Frag;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t nsteps = K / 32;
+  const int64_t nsteps = K / KS;
   const int64_t s0 = (int64_t)blockIdx.x * steps_per_split;
   const int64_t s1 = s0 + steps_per_split < nsteps ? s0 + steps_per_split : nsteps;
-  const int r = lane & 15, kq = 8 * (lane >> 4);
-  const bf16_t* ap[FI];
-  const bf16_t* bp[FJ];
+  const int r = lane & 15, kq = (BF ? 8 : 4) * (lane >> 4);
+  const T* ap[FI];
+  const T* bp[FJ];
 #pragma unroll
   for (int i = 0; i < FI; ++i) {
     const int64_t row = i * 16 + r < M ? i * 16 + r : M - 1;  // rows past M: finite, never stored
@@ -471,14 +481,14 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int64_t st = s0 + w; st < s1; st += 4 * U) {
-    bf16x8 a[U][FI], b[U][FJ];
+    Frag a[U][FI], b[U][FJ];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t k = (st + 4 * u < s1 ? st + 4 * u : st) * 32;   // past the slice: re-read, not used
+      const int64_t k = (st + 4 * u < s1 ? st + 4 * u : st) * KS;   // past the slice: re-read, not used
 #pragma unroll
-      for (int i = 0; i < FI; ++i) a[u][i] = *(const bf16x8*)(ap[i] + k);
+      for (int i = 0; i < FI; ++i) a[u][i] = *(const Frag*)(ap[i] + k);
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) b[u][j] = *(const bf16x8*)(bp[j] + k);
+      for (int j = 0; j < FJ; ++j) b[u][j] = *(const Frag*)(bp[j] + k);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -486,7 +496,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
         for (int i = 0; i < FI; ++i)
 #pragma unroll
-          for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FJ; ++j) {
+            if constexpr (BF) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][i][e], b[u][j][e], acc[i][j], 0, 0, 0);
+            }
+          }
       }
     }
   }
@@ -506,16 +524,21 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
   }
 }
 
+static int skinny_ks(int dtype) { return dtype == VS_BF16 ? 32 : 16; }
+
 bool skinny_ok(const vs_gemm_desc* d) {
   const uint32_t f = d->epilogue;
-  return d->dtype == VS_BF16 && d->out_dtype == VS_F32 && d->a_kcontig && d->b_kcontig && d->M >= 1 && d->M <= 64 &&
-         d->N >= 16 && d->N <= 64 && d->N % 16 == 0 && d->K >= 32 && d->K % 32 == 0 && d->lda % 8 == 0 &&
-         d->ldb % 8 == 0 && (f & VS_EPI_ATOMIC) && !(f & ~(uint32_t)(VS_EPI_ATOMIC | VS_EPI_BIAS)) && !d->a_rowsum &&
-         d->split_k <= 0 && d->K / 32 >= 64;
+  const int ks = skinny_ks(d->dtype);
+  const int vec = d->dtype == VS_BF16 ? 8 : 4;
+  const int max_fj = d->M <= 16 ? 16 : 4;     // LDS / register budget: FI * FJ <= 16
+  return (d->dtype == VS_BF16 || d->dtype == VS_F32) && d->out_dtype == VS_F32 && d->a_kcontig && d->b_kcontig &&
+         d->M >= 1 && d->M <= 64 && d->N >= 16 && d->N <= 16 * max_fj && d->N % 16 == 0 && d->K % ks == 0 &&
+         d->lda % vec == 0 && d->ldb % vec == 0 && (f & VS_EPI_ATOMIC) &&
+         !(f & ~(uint32_t)(VS_EPI_ATOMIC | VS_EPI_BIAS)) && !d->a_rowsum && d->split_k <= 0 && d->K / ks >= 64;
 }
 
-static int skinny_splits(int64_t K, int64_t* steps_per_split) {
-  const int64_t nsteps = K / 32;
+static int skinny_splits(int64_t K, int ks, int64_t* steps_per_split) {
+  const int64_t nsteps = K / ks;
   int64_t S = nsteps / 32;               // >= 8 steps per wave
   if (S > 1024) S = 1024;
   if (S < 1) S = 1;
@@ -524,37 +547,56 @@ static int skinny_splits(int64_t K, int64_t* steps_per_split) {
   return (int)((nsteps + sps - 1) / sps);
 }
 
-size_t skinny_workspace_bytes(int64_t M, int64_t N, int64_t K) {
-  if (M < 1 || M > 64 || N > 64 || K % 32 != 0 || K / 32 < 64) return 0;
+size_t skinny_workspace_bytes(int32_t dtype, int64_t M, int64_t N, int64_t K) {
+  const int ks = skinny_ks(dtype);
+  if (M < 1 || M > 64 || N > 256 || K % ks != 0 || K / ks < 64) return 0;
   int64_t sps;
-  const int S = skinny_splits(K, &sps);
+  const int S = skinny_splits(K, ks, &sps);
   return (size_t)S * (size_t)(M * N) * 4;
+}
+
+template <typename T>
+static void launch_skinny_t(const vs_gemm_desc* d, int FI, int FJ, int S, int64_t sps, float* part, hipStream_t s) {
+  const T* a = (const T*)d->a;
+  const T* b = (const T*)d->b;
+#define SK_(I, J)                                                                                                   \
+  hipLaunchKernelGGL((gemm_skinny_kernel<T, I, J>), dim3((unsigned)S), dim3(256), 0, s, a, d->lda, d->M, b, d->ldb, \
+                     d->N, d->K, (int)sps, part)
+  if (FI == 1) {
+    switch (FJ) {
+      case 1: SK_(1, 1); break;
+      case 2: SK_(1, 2); break;
+      case 3: SK_(1, 3); break;
+      case 4: SK_(1, 4); break;
+      case 8: SK_(1, 8); break;
+      default: SK_(1, 16); break;   // N <= 256: columns past N re-read row N-1 and are not stored
+    }
+  } else {
+    const int fj = FJ <= 1 ? 1 : FJ <= 2 ? 2 : FJ <= 3 ? 3 : 4;
+#define SK_J(I)                      \
+  do {                               \
+    if (fj == 1) SK_(I, 1);          \
+    else if (fj == 2) SK_(I, 2);     \
+    else if (fj == 3) SK_(I, 3);     \
+    else SK_(I, 4);                  \
+  } while (0)
+    if (FI == 2) SK_J(2);
+    else if (FI == 3) SK_J(3);
+    else SK_J(4);
+#undef SK_J
+  }
+#undef SK_
 }
 
 int launch_skinny(const vs_gemm_desc* d, hipStream_t s, int* splits_out) {
   int64_t sps;
-  const int S = skinny_splits(d->K, &sps);
+  const int S = skinny_splits(d->K, skinny_ks(d->dtype), &sps);
   VS_REQUIRE((size_t)d->workspace_bytes >= (size_t)S * (size_t)(d->M * d->N) * 4, "vs_gemm: skinny workspace too small");
-  const bf16_t* a = (const bf16_t*)d->a;
-  const bf16_t* b = (const bf16_t*)d->b;
-  float* part = (float*)d->workspace;
-  const int FI = (int)((d->M + 15) / 16), FJ = (int)(d->N / 16);
-#define SK_(I, J)                                                                                                  \
-  hipLaunchKernelGGL((gemm_skinny_kernel<I, J>), dim3((unsigned)S), dim3(256), 0, s, a, d->lda, d->M, b, d->ldb, d->N, \
-                     d->K, (int)sps, part)
-#define SK_J(I)              \
-  do {                       \
-    if (FJ == 1) SK_(I, 1);  \
-    else if (FJ == 2) SK_(I, 2); \
-    else if (FJ == 3) SK_(I, 3); \
-    else SK_(I, 4);          \
-  } while (0)
-  if (FI == 1) SK_J(1);
-  else if (FI == 2) SK_J(2);
-  else if (FI == 3) SK_J(3);
-  else SK_J(4);
-#undef SK_J
-#undef SK_
+  const int FI = (int)((d->M + 15) / 16);
+  int FJ = (int)(d->N / 16);
+  if (FI == 1 && FJ > 4) FJ = FJ <= 8 ? 8 : 16;
+  if (d->dtype == VS_BF16) launch_skinny_t<bf16_t>(d, FI, FJ, S, sps, (float*)d->workspace, s);
+  else launch_skinny_t<float>(d, FI, FJ, S, sps, (float*)d->workspace, s);
   *splits_out = S;
   return VS_OK;
 }

@@ -6,7 +6,9 @@ loads unchanged.  The forward is ONE autograd node over the whole 6-layer MLP: e
 as an f32 MFMA GEMM with bias+ReLU fused in the epilogue, and the backward fuses each ReLU mask
 into the dX GEMM that produces the masked gradient (VS_EPI_RELU_BWD).  The first layer's
 K = frames*128*128 reduction (1,966,080 for the real `linear_video` config, a 503 M-parameter
-weight) streams through split-K f32 atomics.
+weight) runs on the skinny split-K kernel (fragments streamed straight from HBM, fixed-order
+partial sums, bias + ReLU in the reduce); its weight gradient (K = batch) is written with plain
+stores.
 """
 from __future__ import annotations
 
@@ -95,8 +97,24 @@ class _MLPFn(torch.autograd.Function):
         outs = []
         h = x
         for w, b, r in zip(ws, bs, relu):
-            y = torch.empty(h.shape[0], w.shape[0], dtype=torch.float32, device=h.device)
-            ops.linear(h, w.detach(), y, bias=b.detach(), epilogue=L.EPI_RELU if r else 0)
+            M, K = h.shape
+            N = w.shape[0]
+            # the skinny split-K path of vs_gemm (gemm_dw.hip skinny_ok): M <= 16 and N <= 256 (or
+            # M, N <= 64), K % 16 == 0
+            skinny = K >= 16384 and K % 16 == 0 and N % 16 == 0 and ((M <= 16 and N <= 256) or (M <= 64 and N <= 64))
+            nb = ops.splitk_workspace_bytes(torch.float32, M, N, K) if skinny else 0
+            if nb:
+                # long reduction (the first layer: K = frames*H*W, 1,966,080 for linear_video): skinny
+                # split-K streaming the weight at the HBM rate, splits summed in a fixed order; bias
+                # (and ReLU) applied by the split reduce
+                y = torch.zeros(M, N, dtype=torch.float32, device=h.device)
+                wsp = torch.empty(nb // 4 + 4, dtype=torch.float32, device=h.device)
+                ops.gemm(h, w.detach(), y, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=h.stride(0),
+                         ldb=w.stride(0), ldc=N, epilogue=L.EPI_ATOMIC | L.EPI_BIAS | (L.EPI_RELU if r else 0),
+                         bias=b.detach(), workspace=wsp)
+            else:
+                y = torch.empty(M, N, dtype=torch.float32, device=h.device)
+                ops.linear(h, w.detach(), y, bias=b.detach(), epilogue=L.EPI_RELU if r else 0)
             outs.append(y)
             h = y
         ctx.save_for_backward(x, *outs, *[w.detach() for w in ws])
@@ -116,9 +134,11 @@ class _MLPFn(torch.autograd.Function):
         dy = g.contiguous().to(torch.float32)
         for i in reversed(range(n)):
             inp = x if i == 0 else outs[i - 1]
-            dw = torch.zeros_like(ws[i])
+            # K = batch: one split, plain stores (f32 atomics on the 503 M-element first-layer
+            # gradient would run at ~1.3 TB/s instead of the store rate); db fused as row sums
+            dw = torch.empty_like(ws[i])
             db = torch.zeros(ws[i].shape[0], dtype=torch.float32, device=dy.device)
-            ops.linear_dw(dy, inp, dw, db=db)
+            ops.linear_dw(dy, inp, dw, db=db, accumulate=False)
             grads[2 * i], grads[2 * i + 1] = dw, db
             if i > 0 or ctx.need_x:
                 dx = torch.empty(dy.shape[0], ws[i].shape[1], dtype=torch.float32, device=dy.device)
