@@ -113,6 +113,8 @@ def _single_process_grads(layers, dtype):
     ("exchange", 2, "fp32", 1e-5),
     ("exchange", 4, "bf16", 1e-4),        # 4 layers: consecutive deferred joins (VS_BWD_DEFER_LAST)
     ("ddp", 2, "fp32", 1e-5),
+    ("ddp", 4, "bf16", 1e-4),
+    ("ddp_attach", 2, "fp32", 1e-5),
     ("ddp_attach", 4, "bf16", 1e-4),
 ])
 def test_two_ranks_equal_single_process_batch(mode, layers, dtype, tol):

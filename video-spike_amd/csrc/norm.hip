@@ -325,15 +325,15 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
   }
 }
 
-// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][cols + c].  One block of 16 waves per 64
-// columns: wave w sums partial rows w, w+16, ... with 8 loads in flight, the 16 wave sums meet in
-// LDS in wave order: a fixed order (bitwise reproducible; the previous 16-block version finished
-// with one f32 atomic per block and column, in arrival order).
+// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][cols + c].  A block of 1024 threads owns
+// 16 columns: thread t sums partial rows g, g+64, ... (g = t / 16: 64 row groups, 8 loads in
+// flight), the 64 group sums meet in LDS and are added in group order: a fixed order (bitwise
+// reproducible; the previous version finished with one f32 atomic per block and column).
 __global__ __launch_bounds__(1024) void ln_partsum_kernel(const float* __restrict__ part, int nblk, int cols,
                                                           float* __restrict__ dg, float* __restrict__ db) {
-  __shared__ float red[16][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = 2 * cols;
-  const int grp = threadIdx.x >> 6, ngrp = 16;
+  __shared__ float red[64][17];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4, ngrp = 64;
+  const int c = blockIdx.x * 16 + cl, w = 2 * cols;
   float acc = 0.f;
   if (c < w) {
     int b = grp;
@@ -346,12 +346,11 @@ __global__ __launch_bounds__(1024) void ln_partsum_kernel(const float* __restric
     }
     for (; b < nblk; b += ngrp) acc += part[(int64_t)b * w + c];
   }
-  red[grp][threadIdx.x & 63] = acc;
+  red[grp][cl] = acc;
   __syncthreads();
-  if (threadIdx.x < 64 && c < w) {
+  if (threadIdx.x < 16 && c < w) {
     float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v += red[k][threadIdx.x];
+    for (int k = 0; k < 64; ++k) v += red[k][cl];
     if (c < cols) dg[c] += v;
     else db[c - cols] += v;
   }
@@ -469,7 +468,7 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
     if (lpr == 16) BV_(16); else if (lpr == 32) BV_(32); else BV_(64);
 #undef BV_
     if (part)
-      hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 64)), dim3(1024), 0, s, part, (int)grid,
+      hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 16)), dim3(1024), 0, s, part, (int)grid,
                          (int)cols, dgamma, dbeta);
     VS_LAUNCH_CHECK();
     return VS_OK;
