@@ -534,7 +534,8 @@ bool skinny_ok(const vs_gemm_desc* d) {
   return (d->dtype == VS_BF16 || d->dtype == VS_F32) && d->out_dtype == VS_F32 && d->a_kcontig && d->b_kcontig &&
          d->M >= 1 && d->M <= 64 && d->N >= 16 && d->N <= 16 * max_fj && d->N % 16 == 0 && d->K % ks == 0 &&
          d->lda % vec == 0 && d->ldb % vec == 0 && (f & VS_EPI_ATOMIC) &&
-         !(f & ~(uint32_t)(VS_EPI_ATOMIC | VS_EPI_BIAS)) && !d->a_rowsum && d->split_k <= 0 && d->K / ks >= 64;
+         !(f & ~(uint32_t)(VS_EPI_ATOMIC | VS_EPI_BIAS | VS_EPI_RELU)) && !d->a_rowsum && d->split_k <= 0 &&
+         d->K / ks >= 64;
 }
 
 static int skinny_splits(int64_t K, int ks, int64_t* steps_per_split) {

@@ -47,6 +47,14 @@ class _FwdState(dict):
     an instance is alive (VideoMAE._fwd_buffers holds a weak reference)."""
 
 
+def _dev_key(dev) -> str:
+    """Canonical per-device cache key ('cuda' and 'cuda:0' are the same device)."""
+    d = torch.device(dev)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return str(d)
+
+
 def _cfg_get(config, key, default=None):
     try:
         return config[key] if key in config else default
@@ -182,7 +190,7 @@ class VideoMAE(nn.Module):
         return _VideoMAEFn.apply(pixels, self.enc_flat, self.head_flat, self)
 
     def _pos_table(self, device):
-        key = str(device)
+        key = _dev_key(device)
         if key not in self._pos_cache:
             self._pos_cache[key] = ops.sinusoid_table(self.backbone.num_tokens, self.backbone.hidden_size, device)
         return self._pos_cache[key]
@@ -239,7 +247,7 @@ class VideoMAE(nn.Module):
         backward uses (the reference's loop never does that: base.py:144-159)."""
         self._caches()
         sh = self.__dict__["_lp"]
-        key = str(dev)
+        key = _dev_key(dev)
         if key not in sh:
             dt = self.compute_dtype
             ent = {}
@@ -264,7 +272,7 @@ class VideoMAE(nn.Module):
         shared too)."""
         self._caches()
         chains = self.__dict__["_chains"]
-        key = str(dev)
+        key = _dev_key(dev)
         if key not in chains:
             with torch.cuda.device(dev):
                 chains[key] = L.BwdChain()
@@ -278,7 +286,7 @@ class VideoMAE(nn.Module):
         fwd_cache, _, _ = self._caches()
         enc32, head32 = self.enc_flat.detach(), self.head_flat.detach()
         sig = (enc32.data_ptr(), head32.data_ptr())
-        key = (B, str(dev), save_encoder, self.compute_dtype)
+        key = (B, _dev_key(dev), save_encoder, self.compute_dtype)
         ent = fwd_cache.get(key)
         if ent is not None and ent["sig"] == sig and (ent["owner"] is None or ent["owner"]() is None):
             return ent
@@ -383,7 +391,7 @@ class VideoMAE(nn.Module):
 
         lp = dt != torch.float32
         _, bwd_cache, gs_cache = self._caches()
-        bkey = (B, str(dev), dt)
+        bkey = (B, _dev_key(dev), dt)
         g = bwd_cache.get(bkey)
         if g is None:
             # backward scratch: only used inside this call, in stream order, so one set per shape
