@@ -40,14 +40,19 @@ def _needs(obj: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
-    os.makedirs(BUILD_DIR, exist_ok=True)
+def build(force: bool = False, verbose: bool = True, jobs: int = 8, variant: str = "", defines=()) -> str:
+    """Compile + link.  `variant` builds a diagnostic copy (objects under _build/<variant>/, library
+    _build/libvspike_<variant>.so) with extra `-D` defines, e.g. ("wt", ["VS_WT_STORES"])."""
+    obj_dir = os.path.join(BUILD_DIR, variant) if variant else BUILD_DIR
+    lib_path = os.path.join(BUILD_DIR, f"libvspike_{variant}.so") if variant else LIB_PATH
+    os.makedirs(obj_dir, exist_ok=True)
     hipcc = _hipcc()
+    dflags = [f"-D{d}" for d in defines]
     srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip"))) + sorted(glob.glob(os.path.join(SRC_DIR, "*.cpp")))
     headers = sorted(glob.glob(os.path.join(SRC_DIR, "*.h"))) + [os.path.join(INCLUDE, "vspike.h")]
     objs, todo = [], []
     for s in srcs:
-        o = os.path.join(BUILD_DIR, os.path.splitext(os.path.basename(s))[0] + ".o")
+        o = os.path.join(obj_dir, os.path.splitext(os.path.basename(s))[0] + ".o")
         objs.append(o)
         if force or _needs(o, [s] + headers):
             todo.append((s, o))
@@ -57,7 +62,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
         if s.endswith(".cpp"):     # host-only code (shard reader): plain C++
             cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-I", INCLUDE, "-c", s, "-o", o]
         else:
-            cmd = [hipcc, *_flags(), "-c", s, "-o", o]
+            cmd = [hipcc, *_flags(), *dflags, "-c", s, "-o", o]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed for {os.path.basename(s)}:\n{r.stderr[-6000:]}")
@@ -68,14 +73,14 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
             for s in ex.map(compile_one, todo):
                 if verbose:
                     print(f"[vspike.build] compiled {os.path.basename(s)}", file=sys.stderr)
-    if force or todo or _needs(LIB_PATH, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs, "-lpthread"]
+    if force or todo or _needs(lib_path, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
         if verbose:
-            print(f"[vspike.build] linked {LIB_PATH}", file=sys.stderr)
-    return LIB_PATH
+            print(f"[vspike.build] linked {lib_path}", file=sys.stderr)
+    return lib_path
 
 
 if __name__ == "__main__":
