@@ -1,7 +1,6 @@
 #!/bin/bash
 # Build libvspike.so plus diagnostic variants in-tree; fails loudly.
 #   libvspike_stamp.so : per-block cycle stamps (VS_STAMP) in attention + GEMM
-#   libvspike_wt.so    : epilogue outputs stored write-through (VS_WT_STORES, `sc1`)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 python - <<'PY'
@@ -9,6 +8,5 @@ import sys; sys.path.insert(0, 'video-spike_amd')
 from vspike import build
 build.build()
 build.build(variant="stamp", defines=["VS_STAMP"])
-build.build(variant="wt", defines=["VS_WT_STORES"])
 PY
 echo "built: $(ls video-spike_amd/vspike/_build/*.so | tr '\n' ' ')"

@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   for (int pss = 0; pss < 4; ++pss) {
     const int r = pss * 8 + (lane >> 3), ch = lane & 7;
     const uint4 v = *(const uint4*)(so + r * 128 + ((ch ^ (r & 7)) << 4));
-    if (q0w + r < N) st16_out(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8, v);
+    if (q0w + r < N) *(uint4*)(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8) = v;
   }
   VS_STAMP_AT(true);
 #ifdef VS_STAMP
@@ -899,9 +899,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        st8_out(krow + d, pack4(dkacc[dt][4 * g] * scale, dkacc[dt][4 * g + 1] * scale,
-                                dkacc[dt][4 * g + 2] * scale, dkacc[dt][4 * g + 3] * scale));
-        st8_out(vrow + d, pack4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]));
+        *(uint2*)(krow + d) = pack4(dkacc[dt][4 * g] * scale, dkacc[dt][4 * g + 1] * scale,
+                                    dkacc[dt][4 * g + 2] * scale, dkacc[dt][4 * g + 3] * scale);
+        *(uint2*)(vrow + d) = pack4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
       }
   }
 }
@@ -1045,8 +1045,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        st8_out(qrow + d, pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
-                                dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale));
+        *(uint2*)(qrow + d) = pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
+                                    dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale);
       }
   }
 }

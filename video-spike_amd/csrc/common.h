@@ -120,31 +120,6 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
 }
 
-// 16-B vector store of an epilogue output.  With VS_WT_STORES it is written through to memory
-// (`global_store_dwordx4 ... sc1`: the line leaves the XCD's L2 instead of staying dirty), so the
-// output streams to HBM while the kernel runs instead of being written back at the kernel boundary
-// (MI355X_MICROARCH.md 'boundary': + B / 6 TB/s when the predecessor leaves B bytes dirty).  A
-// vector store (never a scalar one); invisible to hipcc's waitcnt pass, which is fine for outputs
-// the kernel never reads back (the end of the kernel drains every outstanding store).
-__device__ __forceinline__ void st16_out(void* p, uint4 v) {
-#ifdef VS_WT_STORES
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 w = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-#else
-  *(uint4*)p = v;
-#endif
-}
-__device__ __forceinline__ void st8_out(void* p, uint2 v) {
-#ifdef VS_WT_STORES
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 w = {v.x, v.y};
-  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-#else
-  *(uint2*)p = v;
-#endif
-}
-
 // compile-time integer tag (unrolled loops over LDS stages)
 template <int I>
 using IC = std::integral_constant<int, I>;

@@ -109,12 +109,10 @@ __device__ __forceinline__ void st8(void* p, int64_t i, int bf, const float (&v)
     u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
     u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
     u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    st16_out((bf16_t*)p + i, u);
+    *(uint4*)((bf16_t*)p + i) = u;
   } else {
-    st16_out((float*)p + i, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                                       __float_as_uint(v[3])));
-    st16_out((float*)p + i + 4, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]),
-                                           __float_as_uint(v[7])));
+    *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)((float*)p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
 }
 

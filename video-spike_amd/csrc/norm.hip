@@ -154,14 +154,12 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ void st4(float* p, float4 v) {
-  st16_out(p, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
-}
+__device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
 __device__ __forceinline__ void st4(bf16_t* p, float4 v) {
   uint2 u;
   u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
   u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
-  st8_out(p, u);
+  *(uint2*)p = u;
 }
 
 template <typename TO, int LPR, int VEC>
@@ -281,7 +279,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
       o.y = rs * (d[j].y - m1 - xv[j].y * m2) + r[j].y;
       o.z = rs * (d[j].z - m1 - xv[j].z * m2) + r[j].z;
       o.w = rs * (d[j].w - m1 - xv[j].w * m2) + r[j].w;
-      st4(dx + row * lddx + c, o);
+      *(float4*)(dx + row * lddx + c) = o;
       if (dx_lp) st4(dx_lp + row * lddx + c, o);
     }
 #pragma unroll
