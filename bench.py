@@ -12,10 +12,12 @@ Prints ONE JSON line (rank 0):
   * `value` = clips/s over EXACTLY `--steps` train steps, timers off, barrier + synchronize on
     both sides, max over ranks;
   * `roofline`: a SEPARATE instrumented pass (`--profile-steps`, after the timed region) brackets
-    every launch of every kernel class with hipEvents on its own launch stream (libvspike timers)
-    and sums the classes' algorithmic bytes / flops; the dominant class is the one with the most
-    kernel time per step, reported against its bound (HBM bytes for GEMMs, LayerNorm, AdamW;
-    MFMA flops for attention), with every class listed under `all`;
+    every launch with hipEvents on its own launch stream (libvspike timers: one per kernel class,
+    and one per Linear product of the ViT block — fwd / dX / dW of qkv, proj, fc1, fc2) and sums
+    their algorithmic bytes / flops; the dominant entry is the one with the most kernel time per
+    step, reported against its bound (HBM bytes for GEMMs, LayerNorm, AdamW; MFMA flops for
+    attention), with every entry listed under `all`; `pmc` cross-checks attention with the
+    committed rocprofv3 MFMA-busy counters;
   * `cpu_baseline`: the CPU fp32 oracle (oracle/cpu_ref.py, a torch-CPU restatement of the same
     step) on the host cores, per BASELINE.md's plan (median of 5 after a warm-up, fwd and fwd+bwd,
     B=1 and B=4), bounded in time; `parity` compares its B=4 loss with the HIP path's on the same
@@ -40,6 +42,9 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0       # HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s is the measured copy rate
+# timer classes whose launches map one-to-one onto kernels that the committed PMC traffic summary
+# (scripts/traffic_summary.py) groups; the per-product GEMM timers share kernel templates
+TRAFFIC_CLASSES = ("attn_fwd", "attn_bwd", "ln_fwd", "ln_bwd", "adamw")
 
 
 def parse():
@@ -114,18 +119,42 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
     return out, loss4
 
 
-def _traffic_lookup(kind):
-    """HBM bytes per launch of a kernel class from the newest committed PMC summary
+def _traffic_lookup(kind, launches_per_step):
+    """HBM bytes per timed call of a kernel class from the newest committed PMC summary
     (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950
     correction), with the file it came from; None when no summary covers that class."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            return round(d["ops"][kind]["traffic_bytes"], 0), os.path.relpath(f, ROOT)
+            op = d["ops"][kind]
+            if "bytes_per_step" in op:
+                return round(op["bytes_per_step"] / launches_per_step, 0), os.path.relpath(f, ROOT)
+            return round(op["traffic_bytes"], 0), os.path.relpath(f, ROOT)
         except (KeyError, ValueError, OSError):
             continue
     return None, None
+
+
+def _pmc_lookup(kind):
+    """MFMA-busy fraction of an attention kernel from the newest committed PMC summary
+    (scripts/pmc_attn.sh passes -> scripts/pmc_json.py: SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8), the executed-MFMA cross-check of the hipEvent roofline."""
+    kern = {"attn_fwd": "attn_fwd_bf16_kernel", "attn_bwd": "attn_bwd_bf16_kernel"}.get(kind)
+    if kern is None:
+        return None
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_attn.json")))):
+        try:
+            d = json.load(open(f))
+            for name, e in d["kernels"].items():
+                if name.endswith(kern) and "mfma_busy_frac" in e:
+                    return {"mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
+                            "note": "executed MFMA cycles (the backward's dQ pass recomputes S and dP: 7 products "
+                                    "executed for the 5 credited)" if kind == "attn_bwd" else "executed MFMA cycles "
+                                    "(incl. the row-sum MFMAs)"}
+        except (KeyError, ValueError, OSError):
+            continue
+    return None
 
 
 def main():
@@ -228,12 +257,12 @@ def main():
     if roof_all:
         dom = max(roof_all, key=lambda k: roof_all[k]["ms_per_step"])
         r = roof_all[dom]
-        traffic, tsrc = _traffic_lookup(dom)
+        traffic, tsrc = _traffic_lookup(dom, r["launches_per_step"]) if dom in TRAFFIC_CLASSES else (None, None)
         roofline = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
                     "frac": r["frac"], "traffic": traffic, "traffic_source": tsrc,
                     "avg_launch_ms": round(r["avg_launch_us"] / 1e3, 4), "work_per_launch": r["work_per_launch"],
                     "timing": f"hipEvents per launch on the launch stream, {args.profile_steps} instrumented steps",
-                    "all": roof_all}
+                    "pmc": _pmc_lookup(dom), "all": roof_all}
     # algorithmic train FLOPs per clip (BASELINE.md convention: train = 3 x forward)
     D, F, K = bb.hidden_size, bb.intermediate_size, bb.patch_dim
     fwd_clip = Lyr * (2 * N * D * 3 * D + 2 * N * D * D + 4 * N * D * F + 4 * N * N * D) + 2 * N * K * D \

@@ -304,7 +304,21 @@ const char* vs_shard_last_error(void);
 #define VS_TIMER_LN_BWD   5   /* vs_layernorm_bwd (+ its partial-sum reduction) */
 #define VS_TIMER_ADAMW    6   /* vs_adamw */
 #define VS_TIMER_MISC     7   /* vs_cast, vs_colsum, vs_patch_im2col, vs_poisson_nll(_bwd) */
-#define VS_TIMER_COUNT    8
+/* per-product tags of the ViT block executor (vs_vit_layer_fwd / _bwd): its vs_gemm calls are
+   charged to these instead of VS_TIMER_GEMM / VS_TIMER_GEMM_DW, so every product has its own timer */
+#define VS_TIMER_FWD_QKV   8   /* qkv = h1 Wqkv^T + b          (mv:233-236) */
+#define VS_TIMER_FWD_PROJ  9   /* y = x + o Wp^T + bp           (mv:312-319) */
+#define VS_TIMER_FWD_FC1  10   /* a = gelu(h2 W1^T + b1)        (mv:373-383) */
+#define VS_TIMER_FWD_FC2  11   /* x' = y + a W2^T + b2          (mv:390-397) */
+#define VS_TIMER_DX_FC2   12   /* da = (dx' W2) * gelu'(pre) */
+#define VS_TIMER_DX_FC1   13   /* dh2 = da W1 */
+#define VS_TIMER_DX_PROJ  14   /* do = dy Wp */
+#define VS_TIMER_DX_QKV   15   /* dh1 = dqkv Wqkv */
+#define VS_TIMER_DW_FC2   16   /* dW2 += dx'^T a (+ db2) */
+#define VS_TIMER_DW_FC1   17   /* dW1 += da^T h2 (+ db1) */
+#define VS_TIMER_DW_PROJ  18   /* dWp += dy^T o (+ dbp) */
+#define VS_TIMER_DW_QKV   19   /* dWqkv += dqkv^T h1 (+ dbqkv) */
+#define VS_TIMER_COUNT    20
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
 int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */

@@ -363,3 +363,33 @@ def test_linear_video_real_first_layer():
     for k, p in m.named_parameters():
         err = float((p.grad.double() - ps[k].grad).norm() / ps[k].grad.norm())
         assert err < 1e-3, (k, err)
+
+
+def test_kernel_timers_per_product():
+    """bench.py's roofline reads the libvspike timers: with every timer on, one bf16 train step of
+    an L-layer encoder charges exactly L launches to each ViT-block product timer (fwd / dX / dW of
+    qkv, proj, fc1, fc2), L to each attention timer, none of the block's GEMMs to the generic GEMM
+    classes beyond the patch-embed and head products, and positive algorithmic bytes to each."""
+    from vspike import _lib as L, ops, poisson_nll_mean
+    cfg = cpu_ref.ViTCfg(image_size=112, num_frames=8, hidden_size=192, num_hidden_layers=3,
+                         num_attention_heads=3, intermediate_size=768)
+    m = _vit_model(cfg, 64, 16, dtype="bf16")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 2)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (2, 100, 16))).to(DEV)
+    poisson_nll_mean(m(px), y).backward()        # warm caches outside the timed pass
+    torch.cuda.synchronize()
+    ops.timing_enable((1 << len(L.TIMER_NAMES)) - 1)
+    try:
+        m.zero_grad(set_to_none=True)
+        poisson_nll_mean(m(px), y).backward()
+        torch.cuda.synchronize()
+        got = {name: ops.timing_collect(t, with_bytes=True) for t, name in enumerate(L.TIMER_NAMES)}
+    finally:
+        ops.timing_enable(0)
+    for name in L.TIMER_NAMES[8:] + ("attn_fwd", "attn_bwd", "ln_fwd", "ln_bwd"):
+        n, ms, nbytes = got[name]
+        want = 2 * cfg.num_hidden_layers if name.startswith("ln_") else cfg.num_hidden_layers
+        assert n == want, (name, n)
+        assert ms > 0 and nbytes > 0, (name, ms, nbytes)
+    # outside the block: patch-embed fwd + head (fwd, dX) in "gemm", patch dW + head dW in "gemm_dw"
+    assert 0 < got["gemm"][0] <= 6 and 0 < got["gemm_dw"][0] <= 4, (got["gemm"], got["gemm_dw"])

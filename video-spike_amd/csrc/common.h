@@ -50,6 +50,14 @@ struct ScopedTimer {
   ScopedTimer(int t, hipStream_t s, double algorithmic_bytes = 0.0);
   ~ScopedTimer();
 };
+// The timer a nested vs_gemm call is charged to, set by the block executor around each product
+// (-1: the call's own class).  Thread-local: executors on different threads do not interfere.
+extern thread_local int g_timer_tag;
+struct TimerTag {
+  int prev;
+  explicit TimerTag(int t) : prev(g_timer_tag) { g_timer_tag = t; }
+  ~TimerTag() { g_timer_tag = prev; }
+};
 
 // ---- device conversions -------------------------------------------------------------------
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }

@@ -1260,7 +1260,8 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   e.part = nullptr;
 
   hipStream_t s = (hipStream_t)stream;
-  ScopedTimer timer((f & VS_EPI_ATOMIC) ? VS_TIMER_GEMM_DW : VS_TIMER_GEMM, s, gemm_algorithmic_bytes(d));
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : (f & VS_EPI_ATOMIC) ? VS_TIMER_GEMM_DW : VS_TIMER_GEMM, s,
+                    gemm_algorithmic_bytes(d));
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
   const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
   // token-reduction weight gradients (dW = dY^T X, both operands token-major): the dedicated

@@ -8,6 +8,7 @@
 namespace vs {
 
 static thread_local char g_err[512] = "";
+thread_local int g_timer_tag = -1;
 
 void set_error(const char* msg) {
   strncpy(g_err, msg, sizeof(g_err) - 1);

@@ -79,6 +79,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   VS_CALL(vs_layernorm_fwd(T, M, D, L->x_in, D, L->ln1_g, L->ln1_b, L->ln_eps, L->h1, D, L->mean1, L->rstd1, stream));
   {
     vs_gemm_desc g = gdesc(T, T, true, true, M, 3 * D, D, L->h1, D, L->w_qkv, D, L->qkv, 3 * D, VS_EPI_BIAS);
+    TimerTag tag(VS_TIMER_FWD_QKV);
     g.bias = L->b_qkv;
     VS_CALL(vs_gemm(&g, stream));
   }
@@ -87,6 +88,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     vs_gemm_desc g = gdesc(T, VS_F32, true, true, M, D, D, L->attn_o, D, L->w_proj, D, L->y, D,
                            VS_EPI_BIAS | VS_EPI_RESIDUAL);
     g.bias = L->b_proj;
+    TimerTag tag(VS_TIMER_FWD_PROJ);
     g.residual = L->x_in;
     g.ld_residual = D;
     VS_CALL(vs_gemm(&g, stream));
@@ -94,6 +96,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
   {
     vs_gemm_desc g = gdesc(T, T, true, true, M, F, D, L->h2, D, L->w_fc1, D, L->a_act, F, VS_EPI_BIAS | VS_EPI_GELU);
+    TimerTag tag(VS_TIMER_FWD_FC1);
     g.bias = L->b_fc1;
     g.aux_out = L->a_pre;
     g.ld_aux_out = F;
@@ -103,6 +106,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     vs_gemm_desc g = gdesc(T, VS_F32, true, true, M, D, F, L->a_act, F, L->w_fc2, F, L->x_out, D,
                            VS_EPI_BIAS | VS_EPI_RESIDUAL);
     g.bias = L->b_fc2;
+    TimerTag tag(VS_TIMER_FWD_FC2);
     g.residual = L->y;
     g.ld_residual = D;
     VS_CALL(vs_gemm(&g, stream));
@@ -145,6 +149,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(fork(0));  // dx' (and the block's saved activations) ready
   {  // [side] dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
+    TimerTag tag(VS_TIMER_DW_FC2);
     g.a_rowsum = G->b_fc2;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
@@ -154,6 +159,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(wait_prev(1));  // d_a is read by the previous block's dW1
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
     vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
+    TimerTag tag(VS_TIMER_DX_FC2);
     g.aux_in = L->a_pre;
     g.ld_aux_in = F;
     VS_CALL(vs_gemm(&g, stream));
@@ -161,6 +167,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(fork(1));  // da ready
   {  // [side] dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
+    TimerTag tag(VS_TIMER_DW_FC1);
     g.a_rowsum = G->b_fc1;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
@@ -169,6 +176,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   {  // dh2 = da W1
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
+    TimerTag tag(VS_TIMER_DX_FC1);
     VS_CALL(vs_gemm(&g, stream));
   }
   // dy = dx' + LN2'(dh2)
@@ -179,6 +187,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(fork(2));  // dy ready
   {  // [side] dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, D, M, gy, D, L->attn_o, D, G->w_proj, D, VS_EPI_ATOMIC);
+    TimerTag tag(VS_TIMER_DW_PROJ);
     g.a_rowsum = G->b_proj;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
@@ -187,6 +196,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   {  // do = dy Wp
     vs_gemm_desc g = gdesc(T, T, true, false, M, D, D, gy, D, L->w_proj, D, G->d_o, D, 0);
+    TimerTag tag(VS_TIMER_DX_PROJ);
     VS_CALL(vs_gemm(&g, stream));
   }
   VS_CALL(wait_prev(3));  // d_qkv is read by the previous block's dWqkv
@@ -195,6 +205,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(fork(3));  // dqkv ready
   {  // [side] dWqkv[3D,D] += dqkv^T h1;  d(q,k,v bias) += colsum(dqkv) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, 3 * D, D, M, G->d_qkv, 3 * D, L->h1, D, G->w_qkv, D, VS_EPI_ATOMIC);
+    TimerTag tag(VS_TIMER_DW_QKV);
     g.a_rowsum = G->b_qkv;
     g.workspace = G->gemm_ws;
     g.workspace_bytes = G->gemm_ws_bytes;
@@ -206,6 +217,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   {  // dh1 = dqkv Wqkv
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
+    TimerTag tag(VS_TIMER_DX_QKV);
     VS_CALL(vs_gemm(&g, stream));
   }
   // dx = dy + LN1'(dh1)

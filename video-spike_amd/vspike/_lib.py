@@ -19,7 +19,10 @@ EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 BWD_DEFER_JOIN = 0x1
 BWD_DEFER_LAST = 0x2
 TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM, TIMER_GEMM_DW, TIMER_LN_FWD, TIMER_LN_BWD, TIMER_ADAMW, TIMER_MISC = range(8)
-TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "adamw", "misc")
+TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "adamw", "misc",
+               # the block executor's products (vspike.h VS_TIMER_FWD_QKV ..): fwd, dX, dW of each Linear
+               "fwd_qkv", "fwd_proj", "fwd_fc1", "fwd_fc2", "dx_fc2", "dx_fc1", "dx_proj", "dx_qkv",
+               "dw_fc2", "dw_fc1", "dw_proj", "dw_qkv")
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_size_t)
