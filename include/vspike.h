@@ -112,6 +112,17 @@ int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, 
                      int64_t ldx, const float* mean, const float* rstd, const float* gamma,
                      const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
                      float* dgamma, float* dbeta, void* workspace, void* stream);
+/* The dX product of a Linear fed straight into the backward of the LayerNorm before it (the ViT
+ * block's dh2 = da W1 -> LN2' and dh1 = dqkv Wqkv -> LN1', mv:416-417 + mv:373-383 / mv:233-236):
+ *   dh = A B (d: the GEMM, epilogue 0, d->c = an [M, N] f32 scratch used only off the fused path);
+ *   dx = dres + LN'(dh; x, mean, rstd, gamma);  dx_lp = bf16(dx) (optional);
+ *   dgamma, dbeta += the LN weight gradients (fixed-order partial rows through `workspace`, sized by
+ *   vs_layernorm_bwd_workspace_bytes).
+ * bf16 with N in {64, 128, 192} and M >= 8192 runs fused (dh never leaves the chip); otherwise it is
+ * vs_gemm into d->c followed by vs_layernorm_bwd. */
+int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const float* mean, const float* rstd,
+                   const float* gamma, const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
+                   float* dgamma, float* dbeta, void* workspace, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Non-causal multi-head attention, head dim 64 (mv:243-258; SDPA variant mv:286-294):
@@ -264,6 +275,11 @@ typedef struct vs_vit_layer_grad {
  * (each model / thread creates its own).  Destroying a chain does not wait for its side stream. */
 #define VS_BWD_DEFER_JOIN 0x1
 #define VS_BWD_DEFER_LAST 0x2
+/* VS_BWD_FUSE_LN: run dh2 -> LN2' and dh1 -> LN1' as vs_gemm_ln_bwd (one launch each, dh never
+ * leaves the chip).  Off by default: with the side-stream dW products it measured 6.02 vs 5.93
+ * ms/step (the fused kernel holds 128 KB of LDS per CU, so the 128-KB dW workgroups cannot share
+ * its CUs; serialised, the fusion wins: 6.28 vs 6.36, scripts/r02_run19.sh). */
+#define VS_BWD_FUSE_LN    0x4
 
 int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream);
 int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* G, void* stream);

@@ -98,6 +98,13 @@ def main():
                M * 2 * D * e2, 2 * M * D * D)
         rep("dWqkv [576,192] (+db)", lambda: timeit(lambda: ops.linear_dw(qkv, x, dW["qkv"], db=db["qkv"]), a.reps),
                M * 4 * D * e2, 2 * M * D * 3 * D)
+    if a.only in ("", "copy"):
+        # the chip's practical streaming rates on the same byte counts (torch's own kernels)
+        src = torch.empty(M, F, dtype=bf, device=dev).normal_()
+        dst = torch.empty_like(src)
+        big = torch.empty(2 * M, F, dtype=bf, device=dev)
+        report("copy 38.5 MB -> 38.5 MB (torch)", timeit(lambda: dst.copy_(src), a.reps), 2 * M * F * 2, 0)
+        report("fill 77 MB (torch zero_)", timeit(lambda: big.zero_(), a.reps), 2 * M * F * 2, 0)
     if a.only in ("", "attn"):
         qkv = r(M, 3 * D, dt=bf) * 3
         o = torch.empty(M, D, dtype=bf, device=dev)

@@ -132,6 +132,131 @@ def test_gemm_panel_path_many_items(bkc, shape):
         assert rel(g.float(), (x.float() @ w.float().t()) * gg) < 1.5e-2
 
 
+@pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 192), (25088, 192, 576), (8200, 64, 128),
+                                   (12345, 128, 64), (40000, 192, 128)])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
+def test_gemm_row_slab_path(bkc, shape, epi):
+    """N <= 192 bf16 products at M >= 8192 run on the row-slab kernel (one balanced row range per
+    workgroup, all N columns): the ViT block's proj / fc2 (+ bias + f32 residual) and the dX
+    products (plain, f32 or bf16 out).  Ragged M (slabs of 16..17 rows), M > 32,768 (two 64-row
+    tiles per workgroup), both W layouts.  Reference: fp64 on the same bf16 inputs; tolerance 1e-5
+    of max|ref| for f32 outputs (f32 accumulation), 8e-3 for bf16 outputs (one rounding)."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=21).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=22, scale=0.1).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=23).to(DEV)
+    res = _rand(M, N, seed=24).to(DEV)
+    ref = x.double() @ w.double().t()
+    out_bf16 = epi == "none" and K == 192
+    c = torch.empty(M, N, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=DEV)
+    flags, kw = 0, {}
+    if epi != "none":
+        flags |= L.EPI_BIAS
+        kw["bias"] = bias
+        ref = ref + bias.double()
+    if epi == "bias_res":
+        flags |= L.EPI_RESIDUAL
+        kw.update(residual=res, ld_residual=N)
+        ref = ref + res.double()
+    if bkc:
+        ops.gemm(x, w, c, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=K, ldb=K, ldc=N, epilogue=flags, **kw)
+    else:
+        wt = w.t().contiguous()
+        ops.gemm(x, wt, c, M=M, N=N, K=K, a_kcontig=True, b_kcontig=False, lda=K, ldb=N, ldc=N, epilogue=flags, **kw)
+    torch.cuda.synchronize()
+    assert rel(c.float(), ref) < (8e-3 if out_bf16 else 1e-5)
+
+
+@pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("shape", [(25088, 576, 192), (25088, 768, 192), (12345, 256, 128), (40000, 768, 64),
+                                   (8192, 320, 192)])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none"])
+def test_gemm_wide_row_slab_path(bkc, shape, epi):
+    """K <= 192, N > 192 bf16 products at M >= 8192 run on the wide row-slab kernel (balanced row
+    ranges, 64-column chunks, prefetched W chunk and GELU' operand): qkv (+ bias), fc1 (+ bias +
+    GELU, pre-activation written too) and the GELU' dX product; ragged M, two tiles per workgroup
+    (M > 32,768), N not a multiple of 128.  Reference fp64 on the same bf16 inputs; bf16 outputs
+    within 8e-3 of max|ref| (one rounding; GELU' 1.5e-2: the saved pre-activation is bf16)."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=31).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=32, scale=0.1).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=33).to(DEV)
+    b_dev, ldb = (w, K) if bkc else (w.t().contiguous(), N)
+    ref = x.double() @ w.double().t()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    kw = dict(M=M, N=N, K=K, a_kcontig=True, b_kcontig=bkc, lda=K, ldb=ldb, ldc=N)
+    if epi == "bias":
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS, bias=bias, **kw)
+        ref = ref + bias.double()
+        tol = 8e-3
+    elif epi == "none":
+        ops.gemm(x, b_dev, out, **kw)
+        tol = 8e-3
+    elif epi == "gelu":
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU, bias=bias, aux_out=pre, ld_aux_out=N, **kw)
+        ref = ref + bias.double()
+        assert rel(pre.float(), ref) < 8e-3
+        ref = torch.nn.functional.gelu(ref)
+        tol = 8e-3
+    else:
+        pre = _rand(M, N, seed=34).to(torch.bfloat16).to(DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=N, **kw)
+        xp = pre.double().requires_grad_()
+        gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        ref = ref * gg
+        tol = 1.5e-2
+    torch.cuda.synchronize()
+    assert rel(out.float(), ref) < tol
+
+
+@pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 576), (12345, 128, 64), (40000, 64, 128),
+                                   (300, 192, 256)])
+@pytest.mark.parametrize("dres,lp", [(True, True), (False, False)])
+def test_gemm_ln_bwd_fused(shape, dres, lp):
+    """vs_gemm_ln_bwd: the block's dh = dY W product with the LayerNorm backward in its epilogue
+    (fused for bf16, N <= 192, M >= 8192: ragged slabs, two tiles per workgroup at M > 32,768; the
+    small case runs the unfused GEMM + vs_layernorm_bwd).  Reference: fp64 autograd of
+    LayerNorm(eps 1e-12) on dh = dY W computed from the same bf16 inputs.  dx within 1e-4 of
+    max|ref| (f32 arithmetic), dgamma/dbeta 1e-4 of their max (the 16-lane row sums reorder), the
+    bf16 copy within 8e-3; the fused call is bitwise reproducible."""
+    from vspike import ops
+    M, D, Nout = shape
+    dy = _rand(M, Nout, seed=41).to(torch.bfloat16).to(DEV)
+    w = _rand(Nout, D, seed=42, scale=0.05).to(torch.bfloat16).to(DEV)
+    x = (_rand(M, D, seed=43) * 2 + 0.5).to(DEV)
+    gamma = (_rand(D, seed=44) * 0.3 + 1).to(DEV)
+    r = _rand(M, D, seed=45).to(DEV) if dres else None
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-12)
+    dx = torch.empty(M, D, device=DEV)
+    dx_lp = torch.empty(M, D, dtype=torch.bfloat16, device=DEV) if lp else None
+    dg0, db0 = _rand(D, seed=46).to(DEV), _rand(D, seed=47).to(DEV)
+    dg, db = dg0.clone(), db0.clone()
+    ops.linear_dx_ln_bwd(dy, w, x, mean, rstd, gamma, dx, dg, db, dres=r, dx_lp=dx_lp)
+    torch.cuda.synchronize()
+    xd = x.double().cpu().requires_grad_()
+    gd = gamma.double().cpu().requires_grad_()
+    bd = torch.zeros(D, dtype=torch.float64, requires_grad=True)
+    y = torch.nn.functional.layer_norm(xd, (D,), gd, bd, eps=1e-12)
+    dh = dy.double().cpu() @ w.double().cpu()
+    gx, gg, gb = torch.autograd.grad(y, (xd, gd, bd), dh)
+    if dres:
+        gx = gx + r.double().cpu()
+    assert rel(dx, gx) < 1e-4
+    assert rel(dg - dg0, gg) < 1e-4 and rel(db - db0, gb) < 1e-4
+    if lp:
+        assert rel(dx_lp.float(), gx) < 8e-3
+    dx2 = torch.empty_like(dx)
+    dg2, db2 = dg0.clone(), db0.clone()
+    ops.linear_dx_ln_bwd(dy, w, x, mean, rstd, gamma, dx2, dg2, db2, dres=r, dx_lp=dx_lp)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("ws", [None, False])       # split-K partials + reduce launch, or f32 atomics
 @pytest.mark.parametrize("shape", [(64, 192, 25088), (192, 768, 25088), (104, 40, 5000), (768, 192, 25088),

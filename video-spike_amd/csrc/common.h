@@ -53,6 +53,8 @@ struct ScopedTimer {
 // The timer a nested vs_gemm call is charged to, set by the block executor around each product
 // (-1: the call's own class).  Thread-local: executors on different threads do not interfere.
 extern thread_local int g_timer_tag;
+// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][cols + c] in a fixed order (norm.hip)
+void launch_ln_partsum(const float* part, int nblk, int cols, float* dgamma, float* dbeta, hipStream_t s);
 struct TimerTag {
   int prev;
   explicit TimerTag(int t) : prev(g_timer_tag) { g_timer_tag = t; }

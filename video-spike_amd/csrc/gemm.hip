@@ -774,6 +774,368 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_panel_kernel(const bf16_t* _
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16 row-slab kernel for N <= 192 (the ViT block's D-wide outputs: proj + residual, fc2 +
+// residual, and the dX products do, dh2, dh1).  With 128 x 64 tiles these shapes make 588 tiles
+// for 512 resident slots (2 per CU): two rounds, the second a quarter full.  Here the grid is
+// exactly min(512, M/16) workgroups and workgroup g owns the contiguous rows [g M / G, (g+1) M / G)
+// (49 at the bench) and ALL N columns, so every CU carries the same work in one round:
+//   * one 64-row tile covers the slab (rows past the slab re-read its last row, never stored, so
+//     no HBM byte is fetched twice); the W operand (N x 64 per k-step, L2-resident) is re-read by
+//     every workgroup from L2;
+//   * 2-stage LDS-DMA ring over 64-deep k-steps (asm DMA, counted vmcnt + raw barrier, as the ring
+//     kernel): step t+1 is in flight while step t computes; 2 workgroups per CU (64 KB each);
+//   * 4 waves in 2 x 2, wave tile 32 x (N / 2);
+//   * epilogue: the f32 tile is staged through the ring's LDS, each thread takes 2 NT 8-column
+//     groups, every bias / residual load of the thread issued before its first store.
+// Slabs longer than 64 rows (M > 32,768) are processed as consecutive 64-row tiles.
+// ----------------------------------------------------------------------------------------------
+// LayerNorm backward fused into the slab kernel's epilogue (vs_gemm_ln_bwd): the product is dh,
+// the gradient w.r.t. the LN output; every workgroup owns whole rows, so the row reductions of
+// LN' run on the staged tile and dh never reaches HBM.
+struct LnBwdParams {
+  const float* x;      // LN input rows
+  int64_t ldx;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* dres;   // residual gradient added to dx (or null)
+  int64_t ldr;
+  float* dx;
+  int64_t lddx;
+  bf16_t* dx_lp;       // optional bf16 copy of dx (next GEMM operand)
+  float* part;         // [gridDim.x][2][N] dgamma / dbeta partial rows (ln_partsum adds them)
+};
+
+template <int NT, bool BKC, uint32_t EF, bool LNB = false>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
+                                                                EpiParams e, LnBwdParams ln) {
+  using OA = OperandBf16<64, true>;
+  using OB = OperandBf16<64, BKC>;
+  constexpr int N = 64 * NT, TM = 2, TN = NT * 2, WN = N / 2;
+  constexpr int STAGE = OA::BYTES + NT * OB::BYTES;
+  constexpr int PER = OA::PPW + NT * OB::PPW;  // DMA wave-instructions per k-step
+  constexpr int LDT = N + 4;
+  static_assert(64 * LDT * 4 <= 2 * STAGE, "epilogue staging fits the ring");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int64_t G = gridDim.x;
+  const int64_t r_begin = (int64_t)blockIdx.x * e.M / G, r_end = ((int64_t)blockIdx.x + 1) * e.M / G;
+  const int nk = (int)(K / 64);
+  // LN': 16 lanes per row (lane gl owns columns 4 (gl + 16 j), j < NT), 16 rows per pass
+  const int gl = tid & 15, rsub = tid >> 4;
+  float4 pg[NT], pb[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    pg[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  for (int64_t m0 = r_begin; m0 < r_end; m0 += 64) {
+    const int64_t m_end = m0 + 64 < r_end ? m0 + 64 : r_end;
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto issue = [&](int t, char* st) {
+      const int64_t k0 = (int64_t)t * 64;
+      OA::template dma<true>(st, A, lda, m0, m_end, k0, wid, lane);   // rows >= m_end re-read row m_end - 1
+#pragma unroll
+      for (int j = 0; j < NT; ++j) OB::template dma<true>(st + OA::BYTES + j * OB::BYTES, B, ldb, j * 64, N, k0, wid, lane);
+    };
+    auto compute = [&](const char* sa) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * 32 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wc * WN + j * 16;
+          bfr[j] = OB::frag(sa + OA::BYTES + (col >> 6) * OB::BYTES, col & 63, kk, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    auto step = [&](int t, auto sc) {
+      constexpr int S = decltype(sc)::value;
+      char* cur = smem + S * STAGE;
+      char* nxt = smem + (1 - S) * STAGE;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of step t landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                      // every wave's; step t-1's stage is free
+      asm volatile("" ::: "memory");
+      if (t + 1 < nk) issue(t + 1, nxt);
+      compute(cur);
+    };
+    __syncthreads();  // a previous tile's epilogue reads of the staging area are done
+    issue(0, smem);
+    for (int t = 0; t < nk; t += 2) {
+      step(t, IC<0>{});
+      if (t + 1 < nk) step(t + 1, IC<1>{});
+    }
+    (void)PER;
+    // epilogue: stage the f32 tile (alpha applied) over the ring, then 8-column groups per thread
+    __syncthreads();  // every wave's last MFMA operand reads are done
+    float* stg = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stg[(wr * 32 + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
+    __syncthreads();
+    if constexpr (LNB) {
+      // dx = rstd (g dh - mean(g dh) - xh mean(g dh xh)) + dres, xh = (x - mu) rstd (ln_bwd_vec_kernel)
+      constexpr float inv = 1.f / (float)N;
+      float4 xv[4][NT], rv[4][NT];
+      float mu[4], rs[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {  // every operand load of the 4 passes issued first
+        int64_t m = m0 + p * 16 + rsub;
+        m = m < m_end ? m : m_end - 1;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int c = 4 * (gl + 16 * j);
+          xv[p][j] = *(const float4*)(ln.x + m * ln.ldx + c);
+          rv[p][j] = ln.dres ? *(const float4*)(ln.dres + m * ln.ldr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        mu[p] = ln.mean[m];
+        rs[p] = ln.rstd[m];
+      }
+      float4 gam[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) gam[j] = *(const float4*)(ln.gamma + 4 * (gl + 16 * j));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int rr = p * 16 + rsub;
+        const int64_t m = m0 + rr;
+        const bool valid = m < m_end;
+        float4 d[NT];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          d[j] = *(const float4*)(stg + rr * LDT + 4 * (gl + 16 * j));
+#define VS_LNB(C)                                    \
+  {                                                  \
+    const float xh = (xv[p][j].C - mu[p]) * rs[p];   \
+    const float gy = d[j].C * gam[j].C;              \
+    if (valid) {                                     \
+      pg[j].C += d[j].C * xh;                        \
+      pb[j].C += d[j].C;                             \
+    }                                                \
+    xv[p][j].C = xh;                                 \
+    d[j].C = gy;                                     \
+    s1 += gy;                                        \
+    s2 += gy * xh;                                   \
+  }
+          VS_LNB(x) VS_LNB(y) VS_LNB(z) VS_LNB(w)
+#undef VS_LNB
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        const float m1 = s1 * inv, m2 = s2 * inv;
+        if (valid) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            const int c = 4 * (gl + 16 * j);
+            float4 o;
+            o.x = rs[p] * (d[j].x - m1 - xv[p][j].x * m2) + rv[p][j].x;
+            o.y = rs[p] * (d[j].y - m1 - xv[p][j].y * m2) + rv[p][j].y;
+            o.z = rs[p] * (d[j].z - m1 - xv[p][j].z * m2) + rv[p][j].z;
+            o.w = rs[p] * (d[j].w - m1 - xv[p][j].w * m2) + rv[p][j].w;
+            *(float4*)(ln.dx + m * ln.lddx + c) = o;
+            if (ln.dx_lp) {
+              uint2 u;
+              u.x = (uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16);
+              u.y = (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16);
+              *(uint2*)(ln.dx_lp + m * ln.lddx + c) = u;
+            }
+          }
+        }
+      }
+      continue;
+    }
+    constexpr int CPR = N / 8, ITEMS = 64 * CPR / 256;
+    static_assert(64 * CPR % 256 == 0, "whole items per thread");
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const int idx = tid + 256 * it, rr = idx / CPR, cg = idx % CPR;
+      const int64_t m = m0 + rr;
+      if (m < m_end) {
+        const float* src = stg + rr * LDT + cg * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_eight<EF>(e, m, (int64_t)cg * 8, v, false);
+      }
+    }
+  }
+  if constexpr (LNB) {
+    // dgamma / dbeta partial row of this workgroup: the 4 row groups of a wave (lanes of equal gl),
+    // then the 4 waves in wave order through LDS (fixed order: bitwise reproducible)
+    float* red = (float*)smem;  // [2][4][N]
+    __syncthreads();            // the last tile's staging reads are done
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+#define VS_RED(V)                               \
+  {                                             \
+    _Pragma("unroll") for (int o = 16; o < 64; o <<= 1) { \
+      V.x += __shfl_xor(V.x, o, 64);            \
+      V.y += __shfl_xor(V.y, o, 64);            \
+      V.z += __shfl_xor(V.z, o, 64);            \
+      V.w += __shfl_xor(V.w, o, 64);            \
+    }                                           \
+  }
+      VS_RED(pg[j]) VS_RED(pb[j])
+#undef VS_RED
+      if (lane < 16) {
+        *(float4*)&red[(0 * 4 + wid) * N + 4 * (gl + 16 * j)] = pg[j];
+        *(float4*)&red[(1 * 4 + wid) * N + 4 * (gl + 16 * j)] = pb[j];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < N; c += 256) {
+      const float a = (red[0 * N + c] + red[1 * N + c]) + (red[2 * N + c] + red[3 * N + c]);
+      const float b = (red[4 * N + c] + red[5 * N + c]) + (red[6 * N + c] + red[7 * N + c]);
+      ln.part[(int64_t)blockIdx.x * 2 * N + c] = a;
+      ln.part[(int64_t)blockIdx.x * 2 * N + N + c] = b;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// bf16 wide row-slab kernel for K <= 192 and N > 192 (the ViT block's qkv, fc1 + GELU and the
+// GELU' dX product: outputs 3-4x the size of the input, so they are bound by their stores).  Same
+// balanced row ownership as the slab kernel (workgroup g owns rows [g M / G, (g+1) M / G), one
+// 64-row tile), walking the N columns in 64-wide chunks:
+//   * A: each wave keeps its 32 rows x K as MFMA fragments in registers, loaded once;
+//   * W chunk c+1 (64 x K, L2-resident) is register-staged: loads in flight under chunk c's MFMAs,
+//     written into the one LDS image between two barriers (guide T14);
+//   * the GELU' operand of chunk c+1 is loaded under chunk c too, so the epilogue never waits on
+//     HBM; epilogue stores are compiler-visible, so no wait ever drains them;
+//   * epilogue per wave from a wave-private LDS staging tile (32 x 32 f32), 16-B accesses.
+// 2 workgroups per CU (4 waves each).
+// ----------------------------------------------------------------------------------------------
+template <int KT, bool BKC, uint32_t EF>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_wslab_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                 const bf16_t* __restrict__ B, int64_t ldb,
+                                                                 EpiParams e) {
+  using OB = OperandBf16<64, BKC>;
+  constexpr int KS = 2 * KT;   // 32-deep MFMA k-steps
+  constexpr int LDS_T = 68;    // staging row stride (floats)
+  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0;
+  __shared__ __attribute__((aligned(16))) char wimg[KT * OB::BYTES];
+  __shared__ __attribute__((aligned(16))) float stage[4][16 * LDS_T];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t G = gridDim.x;
+  const int64_t r_begin = (int64_t)blockIdx.x * e.M / G, r_end = ((int64_t)blockIdx.x + 1) * e.M / G;
+  const int nch = (int)(e.N / 64);
+  float* st = stage[wid];
+  // wave w: rows 16w .. 16w+15 of the tile, all 64 columns of a chunk (whole 128-B output rows);
+  // epilogue: lane -> rows erow, erow + 8, 8-column group ecg
+  const int erow = lane >> 3, ecg = lane & 7;
+
+  for (int64_t m0 = r_begin; m0 < r_end; m0 += 64) {
+    const int64_t m_end = m0 + 64 < r_end ? m0 + 64 : r_end;
+    bf16x8 af[KS];
+    {
+      int64_t r = m0 + wid * 16 + (lane & 15);
+      r = r < m_end ? r : m_end - 1;  // rows past the slab: its last row again (never stored)
+      const bf16_t* p = A + r * lda + 8 * (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) af[ks] = *(const bf16x8*)(p + 32 * ks);
+    }
+    uint4 wreg[KT][OB::CHUNKS];
+    auto load_w = [&](int c) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) OB::load(wreg[t], B, ldb, (int64_t)c * 64, e.N, t * 64, KT * 64, tid);
+    };
+    // GELU' operand of this lane's two epilogue rows of chunk c (rows past the slab: clamped), in
+    // two named register sets (the chunk loop is unrolled by 2) so no copy waits on a load
+    uint4 auxA[2], auxB[2];
+    auto load_aux = [&](int c, uint4 (&dst)[2]) {
+      if constexpr (GBWD) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          int64_t m = m0 + wid * 16 + erow + 8 * k;
+          m = m < m_end ? m : m_end - 1;
+          dst[k] = *(const uint4*)((const bf16_t*)e.aux_in + m * e.ld_aux_in + (int64_t)c * 64 + ecg * 8);
+        }
+      }
+    };
+    auto chunk = [&](int c, uint4 (&cur)[2], uint4 (&nxt)[2]) {
+      __syncthreads();  // every wave is done reading chunk c-1's W image
+#pragma unroll
+      for (int t = 0; t < KT; ++t) OB::store(wimg + t * OB::BYTES, wreg[t], tid);
+      __syncthreads();  // chunk c's W image complete
+      if (c + 1 < nch) {
+        load_w(c + 1);  // in flight under this chunk's MFMAs and epilogue
+        load_aux(c + 1, nxt);
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = OB::frag(wimg + (ks >> 1) * OB::BYTES, j * 16, ks & 1, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], bfr[j], acc[j], 0, 0, 0);
+      }
+      // wave-private staging: the previous chunk's epilogue reads of `st` come earlier in this
+      // wave's program order, and LDS executes one wave's operations in order
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[((lane >> 4) * 4 + r) * LDS_T + j * 16 + (lane & 15)] = acc[j][r] * e.alpha;
+      const int64_t n = (int64_t)c * 64 + ecg * 8;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int rr = erow + 8 * k;
+        const int64_t m = m0 + wid * 16 + rr;
+        const float* src = st + rr * LDS_T + ecg * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if (m < m_end) {
+          if constexpr (GBWD) {
+            const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[2 * q] *= gelu_fast_grad(__uint_as_float(w[q] << 16));
+              v[2 * q + 1] *= gelu_fast_grad(__uint_as_float(w[q] & 0xffff0000u));
+            }
+            st8(e.c, m * e.ldc + n, e.out_bf16, v);
+          } else {
+            epi_eight<EF>(e, m, n, v, false);
+          }
+        }
+      }
+    };
+    __syncthreads();  // the previous tile's readers of wimg are done
+    load_w(0);
+    load_aux(0, auxA);
+    for (int c = 0; c < nch; c += 2) {
+      chunk(c, auxA, auxB);
+      if (c + 1 < nch) chunk(c + 1, auxB, auxA);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
 // f32 kernel (exact: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
 // ----------------------------------------------------------------------------------------------
 template <bool KC>
@@ -946,6 +1308,46 @@ static void launch_bf16_panel_ef(const vs_gemm_desc* d, unsigned grid, int64_t i
     hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, true, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
   else
     hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, false, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
+}
+
+template <int NT, uint32_t EF, bool LNB = false>
+static void launch_bf16_slab_ef(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s,
+                                const LnBwdParams& ln = LnBwdParams{}) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, true, EF, LNB>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb,
+                       d->K, e, ln);
+  else
+    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, false, EF, LNB>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb,
+                       d->K, e, ln);
+}
+template <int NT>
+static void launch_bf16_slab(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s) {
+  switch (e.flags) {
+    case 0: launch_bf16_slab_ef<NT, 0u>(d, grid, e, s); break;
+    case VS_EPI_BIAS: launch_bf16_slab_ef<NT, (uint32_t)VS_EPI_BIAS>(d, grid, e, s); break;
+    default: launch_bf16_slab_ef<NT, (uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL)>(d, grid, e, s); break;
+  }
+}
+
+template <int KT, uint32_t EF>
+static void launch_bf16_wslab_ef(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_wslab_kernel<KT, true, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_wslab_kernel<KT, false, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
+}
+template <int KT>
+static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s) {
+  switch (e.flags) {
+    case 0: launch_bf16_wslab_ef<KT, 0u>(d, grid, e, s); break;
+    case VS_EPI_BIAS: launch_bf16_wslab_ef<KT, (uint32_t)VS_EPI_BIAS>(d, grid, e, s); break;
+    case VS_EPI_BIAS | VS_EPI_GELU: launch_bf16_wslab_ef<KT, (uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, grid, e, s); break;
+    default: launch_bf16_wslab_ef<KT, (uint32_t)VS_EPI_GELU_BWD>(d, grid, e, s); break;
+  }
 }
 
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
@@ -1287,6 +1689,36 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
+  // row-slab path: N <= 192 outputs of a large-M, K-contiguous-A product, no split / reduction
+  static const int no_slab = getenv_flag5("VSPIKE_NO_SLAB");
+  if (!no_slab && d->dtype == VS_BF16 && d->a_kcontig && (d->N == 64 || d->N == 128 || d->N == 192) &&
+      d->K % 64 == 0 && d->K >= 64 && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
+      (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_RESIDUAL))) {
+    const int64_t G = d->M / 16 < 512 ? d->M / 16 : 512;
+    if (d->N == 64) launch_bf16_slab<1>(d, (unsigned)G, e, s);
+    else if (d->N == 128) launch_bf16_slab<2>(d, (unsigned)G, e, s);
+    else launch_bf16_slab<3>(d, (unsigned)G, e, s);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
+  // wide row-slab path: K <= 192, N > 192 (qkv, fc1 + GELU, the GELU' dX product)
+  static const int no_wslab = getenv_flag5("VSPIKE_NO_WSLAB");
+  // Measured (scripts/microbench.py, bench shapes): faster than the panel kernel for the GELU'
+  // product (39.7 -> 36.8 us), slower than the whole-K tile kernel for the store-bound forward
+  // products (qkv 19.0 -> 22.2, fc1 + GELU 37.9 -> 41.2 us), which therefore stay on it unless
+  // VSPIKE_WSLAB=1 forces this path for every eligible epilogue.
+  static const int all_wslab = getenv_flag5("VSPIKE_WSLAB");
+  if (!no_wslab && d->dtype == VS_BF16 && d->a_kcontig && d->N % 64 == 0 && d->N > 192 &&
+      (d->K == 64 || d->K == 128 || d->K == 192) && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
+      (f == VS_EPI_GELU_BWD || (all_wslab && (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU))))) {
+    static const int gw = getenv("VSPIKE_WSLAB_G") ? atoi(getenv("VSPIKE_WSLAB_G")) : 512;  // A/B knob
+    const int64_t G = d->M / 16 < gw ? d->M / 16 : gw;
+    if (d->K == 64) launch_bf16_wslab<1>(d, (unsigned)G, e, s);
+    else if (d->K == 128) launch_bf16_wslab<2>(d, (unsigned)G, e, s);
+    else launch_bf16_wslab<3>(d, (unsigned)G, e, s);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
   const GemmPlan plan = plan_gemm(d->dtype, d->M, d->N, d->K, d->split_k, atomic_ok, use_ws ? d->workspace_bytes : 0);
   const GridMap& g = plan.g;
   if (use_ws && g.splits > 1) e.part = (float*)d->workspace;
@@ -1369,6 +1801,46 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, vec ? 64 : 256)), dim3(256), 0, s, e.part, g.splits,
                        d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const float* mean,
+                              const float* rstd, const float* gamma, const float* dres, int64_t lddres, float* dx,
+                              int64_t lddx, void* dx_lp, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  using namespace vs;
+  VS_REQUIRE(d && x && mean && rstd && gamma && dx && dgamma && dbeta, "vs_gemm_ln_bwd: null pointer");
+  VS_REQUIRE(d->epilogue == 0 && d->split_k <= 1 && !d->a_rowsum, "vs_gemm_ln_bwd: the product takes no epilogue");
+  if (d->M == 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t M = d->M, N = d->N;
+  static const int no_fuse = getenv_flag5("VSPIKE_NO_LN_FUSE");
+  const bool fused = !no_fuse && d->dtype == VS_BF16 && d->a_kcontig && (N == 64 || N == 128 || N == 192) &&
+                     d->K % 64 == 0 && d->K >= 64 && M >= 8192 && workspace &&
+                     aligned16(d->a) && aligned16(d->b) && d->lda % 8 == 0 && d->ldb % 8 == 0 && d->lda >= d->K &&
+                     (d->b_kcontig ? d->ldb >= d->K : d->ldb >= N) && aligned16(x) && ldx % 4 == 0 && aligned16(dx) &&
+                     lddx % 4 == 0 && aligned16(gamma) && (!dres || (aligned16(dres) && lddres % 4 == 0)) &&
+                     (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0);
+  if (!fused) {
+    VS_REQUIRE(d->c && d->out_dtype == VS_F32, "vs_gemm_ln_bwd: the unfused path needs an f32 scratch d->c");
+    VS_CALL(vs_gemm(d, stream));
+    return vs_layernorm_bwd(M, N, (const float*)d->c, d->ldc, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp,
+                            dgamma, dbeta, workspace, stream);
+  }
+  const double ea = esize(d->dtype);
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
+                    (double)(M + N) * (double)d->K * ea + (double)M * (double)N * (12.0 + (dres ? 4.0 : 0.0) +
+                    (dx_lp ? 2.0 : 0.0)) + (double)M * 8.0 + (double)N * 20.0);
+  EpiParams e = {};
+  e.M = M; e.N = N; e.alpha = d->alpha; e.vec_ok = 1;
+  LnBwdParams ln;
+  ln.x = x; ln.ldx = ldx; ln.mean = mean; ln.rstd = rstd; ln.gamma = gamma; ln.dres = dres; ln.ldr = lddres;
+  ln.dx = dx; ln.lddx = lddx; ln.dx_lp = (bf16_t*)dx_lp; ln.part = (float*)workspace;
+  const int64_t G = M / 16 < 512 ? M / 16 : 512;  // <= the 1024 partial rows of the LN workspace
+  if (N == 64) launch_bf16_slab_ef<1, 0u, true>(d, (unsigned)G, e, s, ln);
+  else if (N == 128) launch_bf16_slab_ef<2, 0u, true>(d, (unsigned)G, e, s, ln);
+  else launch_bf16_slab_ef<3, 0u, true>(d, (unsigned)G, e, s, ln);
+  launch_ln_partsum((const float*)workspace, (int)G, (int)N, dgamma, dbeta, s);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -440,6 +440,13 @@ extern "C" int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, con
   return VS_OK;
 }
 
+namespace vs {
+void launch_ln_partsum(const float* part, int nblk, int cols, float* dgamma, float* dbeta, hipStream_t s) {
+  hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 16)), dim3(1024), 0, s, part, nblk, cols, dgamma,
+                     dbeta);
+}
+}  // namespace vs
+
 extern "C" size_t vs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t cols) {
   (void)rows;
   return (size_t)kLnBwdBlocks * 2 * (size_t)(cols > 0 ? cols : 0) * sizeof(float);

@@ -174,15 +174,20 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     VS_CALL(vs_gemm(&g, side));
     VS_CALL(mark(1));
   }
-  {  // dh2 = da W1
+  // dh2 = da W1;  dy = dx' + LN2'(dh2)  (VS_BWD_FUSE_LN: one launch, dh2 stays on the chip)
+  VS_CALL(wait_prev(2));  // dy / dy_lp are read by the previous block's dWp
+  {
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
     TimerTag tag(VS_TIMER_DX_FC1);
-    VS_CALL(vs_gemm(&g, stream));
+    if (G->flags & VS_BWD_FUSE_LN) {
+      VS_CALL(vs_gemm_ln_bwd(&g, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
+                             lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
+    } else {
+      VS_CALL(vs_gemm(&g, stream));
+      VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
+                               lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
+    }
   }
-  // dy = dx' + LN2'(dh2)
-  VS_CALL(wait_prev(2));  // dy / dy_lp are read by the previous block's dWp
-  VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
-                           lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
   // ---- attention: y = x + o Wp^T + bp
   VS_CALL(fork(2));  // dy ready
   {  // [side] dWp[D,D] += dy^T o;  dbp += colsum(dy) fused
@@ -215,15 +220,20 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     if (e != hipSuccess) return (int)e;
     VS_CALL(mark(3));
   }
-  {  // dh1 = dqkv Wqkv
+  // dh1 = dqkv Wqkv;  dx = dy + LN1'(dh1)  (one launch, as above)
+  VS_CALL(wait_prev(0));  // dx_in is the previous block's dx_out, read by its dW2
+  {
     vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
     TimerTag tag(VS_TIMER_DX_QKV);
-    VS_CALL(vs_gemm(&g, stream));
+    if (G->flags & VS_BWD_FUSE_LN) {
+      VS_CALL(vs_gemm_ln_bwd(&g, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
+                             lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
+    } else {
+      VS_CALL(vs_gemm(&g, stream));
+      VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
+                               lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
+    }
   }
-  // dx = dy + LN1'(dh1)
-  VS_CALL(wait_prev(0));  // dx_in is the previous block's dx_out, read by its dW2
-  VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
-                           lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
   if (!ch) return VS_OK;
   if (G->flags & VS_BWD_DEFER_JOIN) {
     ch->pending = 0xF;  // the next block waits on ce[] before each overwrite

@@ -18,6 +18,7 @@ EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 BWD_DEFER_JOIN = 0x1
 BWD_DEFER_LAST = 0x2
+BWD_FUSE_LN = 0x4
 TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM, TIMER_GEMM_DW, TIMER_LN_FWD, TIMER_LN_BWD, TIMER_ADAMW, TIMER_MISC = range(8)
 TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "adamw", "misc",
                # the block executor's products (vspike.h VS_TIMER_FWD_QKV ..): fwd, dX, dW of each Linear
@@ -79,6 +80,8 @@ PROTOTYPES = {
                                            c_i64, ctypes.POINTER(c_f32), ctypes.POINTER(c_f32), c_p, c_p]),
     "vs_layernorm_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
                                         c_i64, c_p, c_p, c_p, c_p, c_p]),
+    "vs_gemm_ln_bwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
+                                      c_p, c_p, c_p, c_p, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),
     "vs_attn_bwd_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "vs_attn_bwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,

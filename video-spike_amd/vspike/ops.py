@@ -111,6 +111,32 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=
     return dx
 
 
+def linear_dx_ln_bwd(dy, w, x, mean, rstd, gamma, dx, dgamma, dbeta, *, dres=None, dx_lp=None, scratch=None,
+                     workspace=None):
+    """dx = dres + LN'(dy @ w; x, mean, rstd, gamma), dgamma/dbeta accumulate (vs_gemm_ln_bwd): the
+    dX product of a Linear fused with the backward of the LayerNorm that feeds it.  dy [M, Nout]
+    (bf16 or f32), w [Nout, D]; `scratch` ([M, D] f32) is only written off the fused path."""
+    require_device(dy, w, x, dx)
+    M, Nout = dy.shape
+    D = w.shape[1]
+    if scratch is None:
+        scratch = torch.empty(M, D, dtype=torch.float32, device=x.device)
+    if workspace is None:
+        workspace = torch.empty(layernorm_bwd_workspace_bytes(M, D) // 4 + 4, dtype=torch.float32, device=x.device)
+    d = L.GemmDesc()
+    d.dtype = L.dtype_code(dy.dtype)
+    d.out_dtype = L.dtype_code(torch.float32)
+    d.a_kcontig, d.b_kcontig = 1, 0
+    d.M, d.N, d.K = M, D, Nout
+    d.a, d.lda, d.b, d.ldb, d.c, d.ldc = dy.data_ptr(), dy.stride(0), w.data_ptr(), w.stride(0), scratch.data_ptr(), D
+    d.alpha = 1.0
+    check(lib().vs_gemm_ln_bwd(ctypes.byref(d), x.data_ptr(), x.stride(0), mean.data_ptr(), rstd.data_ptr(),
+                               gamma.data_ptr(), ptr(dres), dres.stride(0) if dres is not None else 0, dx.data_ptr(),
+                               dx.stride(0), ptr(dx_lp), dgamma.data_ptr(), dbeta.data_ptr(), workspace.data_ptr(),
+                               stream()), "vs_gemm_ln_bwd")
+    return dx
+
+
 def attn_fwd(qkv, o, lse, B, N, H, scale=0.125):
     require_device(qkv, o, lse)
     check(lib().vs_attn_fwd(L.dtype_code(qkv.dtype), B, N, H, 64, qkv.data_ptr(), qkv.stride(0), o.data_ptr(),

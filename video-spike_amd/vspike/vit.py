@@ -37,6 +37,10 @@ from .optim import lp_key, register_lp_shadow
 # (VS_BWD_DEFER_LAST, the default) keeps the other three joined: 6.33 vs 6.41 ms/step for
 # join-every-block (VSPIKE_DEFER=0), same box, 3 round-robin runs of 30 steps (scripts/ab_env.sh).
 _DEFER = {"0": 0, "1": 1, "last": 2}.get(os.environ.get("VSPIKE_DEFER", "last"), 2)
+# VSPIKE_SIDE=0: no side stream (every dW product in order on the main stream), for A/B runs
+_SIDE = os.environ.get("VSPIKE_SIDE", "1") != "0"
+# VSPIKE_LN_FUSE=1: fuse the dX products with the LayerNorm backwards (VS_BWD_FUSE_LN, see vspike.h)
+_LN_FUSE = os.environ.get("VSPIKE_LN_FUSE", "0") == "1"
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -465,10 +469,11 @@ class VideoMAE(nn.Module):
                 gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
                 gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
                 gs.ln_ws = g["ln_ws"].data_ptr()
-                gs.chain = self._chain(dev).handle
+                gs.chain = self._chain(dev).handle if _SIDE else None
                 gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
                 # opt-in: every block but the last one defers its side-stream join to the next
-                gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER else 0)
+                gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER and _SIDE else 0)
+                gs.flags |= L.BWD_FUSE_LN if _LN_FUSE else 0
                 grads[i] = (gs, nxt)
                 cur = nxt
             gs_cache[gkey] = grads
