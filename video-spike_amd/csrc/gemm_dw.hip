@@ -73,7 +73,7 @@ __device__ __forceinline__ bf16x8 dw_frag(const char* img, int rb, int kk, int l
 // 4 x 2 grid of (BM/4) x 32 wave tiles, or NW = 4 in a 4 x 1 grid of (BM/4) x 64.
 // Partial tiles are stored in tile-fragment order: float4 ((rowfrag * 4 + colfrag) * 64 + lane),
 // rowfrag / colfrag = the 16-row / 16-column block within the BM x 64 tile.
-template <int BM, int SUMS, int NW>
+template <int BM, int SUMS, int NW, int NSTG = 4>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
                                                              const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
                                                              int64_t K, DwGrid g, float* __restrict__ part,
@@ -83,10 +83,11 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
   constexpr int STAGE = (NA + 1) * IMG;   // A images then the B image
   constexpr int PER = (NA + 1) * (8 / NW);  // DMA wave-instructions per stage
   constexpr int WM = BM / 4, FI = WM / 16, FJ = NW == 8 ? 2 : 4;
+  static_assert(NSTG == 3 || NSTG == 4, "3- or 4-stage ring");
   __shared__ __attribute__((aligned(16))) char st0[STAGE];
   __shared__ __attribute__((aligned(16))) char st1[STAGE];
   __shared__ __attribute__((aligned(16))) char st2[STAGE];
-  __shared__ __attribute__((aligned(16))) char st3[STAGE];
+  __shared__ __attribute__((aligned(16))) char st3[NSTG == 4 ? STAGE : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rw = wid & 3, cw = wid >> 2;  // wave tile: rows rw*WM.., columns cw*FJ*16..
@@ -154,9 +155,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
   auto step = [&](int s, auto sc) {
     constexpr int S = decltype(sc)::value;
     char* cur = S == 0 ? st0 : S == 1 ? st1 : S == 2 ? st2 : st3;
-    char* far = S == 0 ? st3 : S == 1 ? st0 : S == 2 ? st1 : st2;  // stage of step s + 3
-    // steps s+1, s+2 may stay in flight
-    if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    // stage of step s + NSTG - 1 (the one step s - 1 used)
+    char* far = NSTG == 4 ? (S == 0 ? st3 : S == 1 ? st0 : S == 2 ? st1 : st2) : (S == 0 ? st2 : S == 1 ? st0 : st1);
+    // steps s+1 .. s+NSTG-2 may stay in flight
+    if (NSTG == 4 && s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
     else if (s + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -169,17 +171,17 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
-    if (s + 3 < nk) issue(s + 3, far);
+    if (s + NSTG - 1 < nk) issue(s + NSTG - 1, far);
     compute(cur);
   };
   if (nk > 0) issue(0, st0);
   if (nk > 1) issue(1, st1);
-  if (nk > 2) issue(2, st2);
-  for (int s = 0; s < nk; s += 4) {
+  if (NSTG == 4 && nk > 2) issue(2, st2);
+  for (int s = 0; s < nk; s += NSTG) {
     step(s, IC<0>{});
     if (s + 1 < nk) step(s + 1, IC<1>{});
     if (s + 2 < nk) step(s + 2, IC<2>{});
-    if (s + 3 < nk) step(s + 3, IC<3>{});
+    if (NSTG == 4 && s + 3 < nk) step(s + 3, IC<3>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -670,7 +672,11 @@ template <int BM, int SUMS, bool TRANS>
 static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* b, int64_t ldb, int64_t Nb, int64_t K,
                         const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
   const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
-  if (p.dma)
+  static const int stages = env_int("VSPIKE_DW_STAGES", 4);
+  if (p.dma && stages == 3)
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS, 8, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
+                       part, sums);
+  else if (p.dma)
     hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS, 8>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
                        sums);
   else
