@@ -15,6 +15,7 @@
 // f32 (parity) path — exact-f32 VALU kernels: 4 lanes per query/key row, K/V (or Q/dO) tiles in
 //   LDS, expf/logf in f32.  Used for the 1e-4-relative parity mode.
 #include <math.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
