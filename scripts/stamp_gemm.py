@@ -1,5 +1,5 @@
-"""Phase timeline of the whole-K GEMM (qkv shape) from a -DVS_STAMP build.
-usage: VSPIKE_LIB=.../libvspike_stamp.so python scripts/stamp_gemm.py"""
+"""Phase timeline of the whole-K GEMM (qkv shape; N=768 EPI=gelu: fc1) from a -DVS_STAMP build.
+usage: VSPIKE_LIB=.../libvspike_stamp.so [N=768 EPI=gelu] python scripts/stamp_gemm.py"""
 import ctypes
 import os
 import sys
@@ -20,8 +20,13 @@ def main():
     w = (torch.randn(N, K, device="cuda") * 0.5).to(torch.bfloat16)
     b = torch.randn(N, device="cuda")
     y = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    gelu = os.environ.get("EPI") == "gelu"   # fc1 + GELU (pre-activation written too)
     for _ in range(5):
-        ops.linear(x, w, y, bias=b)
+        if gelu:
+            ops.linear(x, w, y, bias=b, epilogue=L.EPI_GELU, aux_out=pre, ld_aux_out=N)
+        else:
+            ops.linear(x, w, y, bias=b)
     torch.cuda.synchronize()
     nblk = (M // 128) * ((N + 63) // 64)
     nw = nblk * 4
