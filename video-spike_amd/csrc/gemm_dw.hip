@@ -437,6 +437,60 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
   bias_out[e] += s;
 }
 
+// The same reduction for few splits (S <= 8: the ViT-Base products, whose many output tiles leave
+// one or two splits): one float4 of a tile per thread in 256-thread blocks, the splits added in
+// split order (the 16-wave layout above left 15 of 16 waves idle there and ran latency-bound,
+// 363 us for a 9.4 MB dW at S = 1).  TRANS stores the 4 consecutive m of a lane as one float4.
+template <int BM, bool TRANS>
+__global__ __launch_bounds__(256) void gemm_dw_reduce_few(const float* __restrict__ part, const float* __restrict__ sums,
+                                                          DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
+                                                          int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
+                                                          int sum_tiles, int sum_w) {
+  constexpr int Q = BM * 16;  // float4 per tile
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tile_items = (int64_t)tiles * Q;
+  if (item < tile_items) {
+    const int tile = (int)(item / Q), q = (int)(item % Q), lane = q & 63;
+    const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
+    float4 sum = p[0];
+    for (int sp = 1; sp < g.splits; ++sp) {
+      const float4 o = p[(int64_t)sp * Q];
+      sum.x += o.x; sum.y += o.y; sum.z += o.z; sum.w += o.w;
+    }
+    const int f = q >> 6, rf = f >> 2, cf = f & 3;
+    const int mt = tile / g.tiles_n, nt = tile % g.tiles_n;
+    const int64_t n = (int64_t)nt * 64 + cf * 16 + (lane & 15);
+    const int64_t mb = (int64_t)mt * BM + rf * 16 + (lane >> 4) * 4;
+    if (n >= N) return;
+    const float vv[4] = {sum.x, sum.y, sum.z, sum.w};
+    if (TRANS && mb + 4 <= M && ldc % 4 == 0) {
+      float4* dst = (float4*)(c + n * ldc + mb);
+      float4 o = *dst;
+      o.x += vv[0]; o.y += vv[1]; o.z += vv[2]; o.w += vv[3];
+      *dst = o;
+      return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t m = mb + r;
+      if (m < M) {
+        float* dst = TRANS ? c + n * ldc + m : c + m * ldc + n;
+        *dst += vv[r];
+      }
+    }
+    return;
+  }
+  const int64_t e = item - tile_items;  // element of the bias vector
+  if (e >= sum_len) return;
+  const int64_t st = e / sum_w, off = e % sum_w;
+  if (st >= sum_tiles) return;
+  const float* ps = sums + st * (int64_t)g.splits * sum_w + off;
+  float acc = 0.f;
+  for (int sp = 0; sp < g.splits; ++sp) acc += ps[(int64_t)sp * sum_w];
+  bias_out[e] += acc;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Skinny split-K product with both operands K-contiguous: C[M,N] (+)= A[M,K] B[N,K]^T (+ bias),
 // M <= 64, N <= 256, K huge — the head's Linear(N*D -> 64) forward (src/model/videomae.py:13,29:
@@ -695,8 +749,14 @@ static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* 
     sum_tiles = p.g.tiles_n;
     sum_len = Nb;
   }
-  const int64_t blocks = tile_blocks + (sum_len + 1023) / 1024;
   // C is [M][N] of the ORIGINAL product: with TRANS the kernel's (m, n) = (original n, original m)
+  if (p.g.splits <= 8) {
+    const int64_t items = (int64_t)tiles * (BM * 16) + sum_len;
+    hipLaunchKernelGGL((gemm_dw_reduce_few<BM, TRANS>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, part,
+                       sums, p.g, Ma, Nb, c, ldc, bias, sum_len, sum_tiles, (int)sum_w);
+    return;
+  }
+  const int64_t blocks = tile_blocks + (sum_len + 1023) / 1024;
   hipLaunchKernelGGL((gemm_dw_reduce<BM, TRANS>), dim3((unsigned)blocks), dim3(1024), 0, s, part, sums, p.g, Ma, Nb, c,
                      ldc, bias, sum_len, sum_tiles, (int)sum_w);
 }
