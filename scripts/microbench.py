@@ -98,6 +98,26 @@ def main():
                M * 2 * D * e2, 2 * M * D * D)
         rep("dWqkv [576,192] (+db)", lambda: timeit(lambda: ops.linear_dw(qkv, x, dW["qkv"], db=db["qkv"]), a.reps),
                M * 4 * D * e2, 2 * M * D * 3 * D)
+    if a.only == "base":
+        # ViT-Base (C3) block products: D = 768, F = 3072, M = B x 1568
+        Db, Fb = 768, 3072
+        x, h = r(M, Db), r(M, Fb)
+        wq, wp, w1, w2 = r(3 * Db, Db), r(Db, Db), r(Fb, Db), r(Db, Fb)
+        bq, bd, b1 = r(3 * Db, dt=torch.float32), r(Db, dt=torch.float32), r(Fb, dt=torch.float32)
+        qkv, a_, pre, o32 = r(M, 3 * Db), r(M, Fb), r(M, Fb), torch.empty(M, Db, device=dev)
+        res = r(M, Db, dt=torch.float32)
+        for name, fn, nb, fl in (
+                ("base fwd qkv", lambda: ops.linear(x, wq, qkv, bias=bq), M * Db * 2 + M * 3 * Db * 2, 2 * M * Db * 3 * Db),
+                ("base fwd proj +res", lambda: ops.linear(x, wp, o32, bias=bd, epilogue=L.EPI_RESIDUAL, residual=res,
+                                                          ld_residual=Db), M * Db * 10, 2 * M * Db * Db),
+                ("base fwd fc1 +GELU", lambda: ops.linear(x, w1, a_, bias=b1, epilogue=L.EPI_GELU, aux_out=pre,
+                                                          ld_aux_out=Fb), M * Db * 2 + 2 * M * Fb * 2, 2 * M * Db * Fb),
+                ("base fwd fc2 +res", lambda: ops.linear(h, w2, o32, bias=bd, epilogue=L.EPI_RESIDUAL, residual=res,
+                                                         ld_residual=Db), M * Fb * 2 + M * Db * 8, 2 * M * Db * Fb),
+                ("base dx da*gelu'", lambda: ops.linear_dx(x, w2, a_, epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=Fb),
+                 M * Db * 2 + 2 * M * Fb * 2, 2 * M * Db * Fb),
+                ("base dx dh2 (f32)", lambda: ops.linear_dx(h, w1, o32), M * Fb * 2 + M * Db * 4, 2 * M * Db * Fb)):
+            report(name, timeit(fn, a.reps), nb, fl)
     if a.only in ("", "copy"):
         # the chip's practical streaming rates on the same byte counts (torch's own kernels)
         src = torch.empty(M, F, dtype=bf, device=dev).normal_()

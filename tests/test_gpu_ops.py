@@ -213,6 +213,55 @@ def test_gemm_wide_row_slab_path(bkc, shape, epi):
     assert rel(out.float(), ref) < tol
 
 
+@pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("shape,epi", [((25088, 3072, 768), "gelu"), ((25088, 768, 3072), "bias_res"),
+                                       ((4100, 512, 512), "bias"), ((8192, 2304, 768), "none"),
+                                       ((6000, 768, 1536), "gelu_bwd")])
+def test_gemm_big_tile_path(bkc, shape, epi):
+    """K >= 512, N >= 512 bf16 products (ViT-Base's D = 768 / F = 3072 block) run on the 256 x 128
+    8-wave big-tile kernel: every epilogue the block uses, both W layouts, ragged M (M % 256 != 0).
+    Reference fp64 on the same bf16 inputs: f32 outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (GELU'
+    1.5e-2, against a bf16 pre-activation)."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=51).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=52, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=53).to(DEV)
+    b_dev, ldb = (w, K) if bkc else (w.t().contiguous(), N)
+    kw = dict(M=M, N=N, K=K, a_kcontig=True, b_kcontig=bkc, lda=K, ldb=ldb, ldc=N)
+    ref = x.double() @ w.double().t()
+    if epi == "bias_res":
+        res = _rand(M, N, seed=54).to(DEV)
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_RESIDUAL, bias=bias, residual=res, ld_residual=N, **kw)
+        ref, tol = ref + bias.double() + res.double(), 1e-5
+    elif epi == "bias":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS, bias=bias, **kw)
+        ref, tol = ref + bias.double(), 8e-3
+    elif epi == "none":
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm(x, b_dev, out, **kw)
+        tol = 1e-5
+    elif epi == "gelu":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU, bias=bias, aux_out=pre, ld_aux_out=N, **kw)
+        ref = ref + bias.double()
+        torch.cuda.synchronize()
+        assert rel(pre.float(), ref) < 8e-3
+        ref, tol = torch.nn.functional.gelu(ref), 8e-3
+    else:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        pre = _rand(M, N, seed=55).to(torch.bfloat16).to(DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=N, **kw)
+        xp = pre.double().requires_grad_()
+        gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        ref, tol = ref * gg, 1.5e-2
+    torch.cuda.synchronize()
+    assert rel(out.float(), ref) < tol
+
+
 @pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 576), (12345, 128, 64), (40000, 64, 128),
                                    (300, 192, 256)])
 @pytest.mark.parametrize("dres,lp", [(True, True), (False, False)])

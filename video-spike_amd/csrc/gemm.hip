@@ -365,6 +365,31 @@ struct OperandBf16 {
       else glds16(src, lds + pi * 1024);
     }
   }
+  // the same fill issued by NW waves (8-wave kernels)
+  template <int NW>
+  __device__ __forceinline__ static void dma_nw(char* lds, const bf16_t* __restrict__ p, int64_t ld, int64_t r0,
+                                                int64_t rows, int64_t k0, int wid, int lane) {
+    static_assert(PIECES % NW == 0, "whole pieces per wave");
+#pragma unroll
+    for (int j = 0; j < PIECES / NW; ++j) {
+      const int pi = wid * (PIECES / NW) + j;
+      const bf16_t* src;
+      if constexpr (KC) {
+        const int r = pi * 8 + (lane >> 3), c = (lane & 7) ^ swz_kc(r);
+        const int64_t gr = r0 + r < rows ? r0 + r : rows - 1;
+        src = p + gr * ld + k0 + c * 8;
+      } else if constexpr (R == 128) {
+        const int k = pi * 4 + (lane >> 4), c = (lane & 15) ^ swz_mc<R>(k);
+        const int64_t gc = r0 + c * 8 <= rows - 8 ? r0 + c * 8 : rows - 8;
+        src = p + (k0 + k) * ld + gc;
+      } else {
+        const int k = pi * 8 + (lane >> 3), c = (lane & 7) ^ swz_mc<R>(k);
+        const int64_t gc = r0 + c * 8 <= rows - 8 ? r0 + c * 8 : rows - 8;
+        src = p + (k0 + k) * ld + gc;
+      }
+      glds16_asm(src, lds + pi * 1024);
+    }
+  }
   // fragment of rows [rb, rb+16) for the 32-deep k step kk (0/1): lane holds rows rb+(lane&15),
   // k = 32kk + 8(lane>>4) + 0..7.
   __device__ __forceinline__ static bf16x8 frag(const char* lds, int rb, int kk, int lane) {
@@ -1136,6 +1161,104 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wslab_kernel(const bf16_t* _
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16 big-tile kernel for the MFMA-heavy products (K >= 512, N >= 512: ViT-Base's D = 768 /
+// F = 3072 projections and their dX, 2-4 TFLOP/s-scale work per launch): 256 x 128 output tile per
+// workgroup of 8 waves (4 x 2, 64 x 64 per wave: 16 accumulator tiles, 32 MFMAs per 64-deep k-step
+// against 16 fragment reads), 2-stage LDS-DMA ring of 48-KB stages (asm DMA, vmcnt(0) + raw barrier;
+// step t+1 in flight under step t's MFMAs; guide §5 "glds vs register staging": at ~1 block per CU
+// this ties a register pipeline), one workgroup per CU; the per-tile kernels above (128 x 64, 4
+// waves) re-read 4x more operand bytes per MFMA and ran these shapes at 0.1-0.2 of the MFMA roof.
+// Epilogue: the f32 tile staged through the ring in two 128-row halves, 8-column groups per thread.
+// ----------------------------------------------------------------------------------------------
+template <bool BKC, uint32_t EF>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                               const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
+                                                               GridMap g, EpiParams e) {
+  using OA = OperandBf16<256, true>;
+  using OB = OperandBf16<128, BKC>;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;  // 48 KB
+  constexpr int LDT = 128 + 4;
+  constexpr int SMEM = CMax<2 * STAGE, 128 * LDT * 4>::v;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  int nt, mt, split;
+  map_block(g, nt, mt, split);
+  (void)split;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int64_t m0 = (int64_t)mt * 256, n0 = (int64_t)nt * 128;
+  const int nk = (int)(K / 64);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int t, char* st) {
+    const int64_t k0 = (int64_t)t * 64;
+    OA::template dma_nw<8>(st, A, lda, m0, e.M, k0, wid, lane);
+    OB::template dma_nw<8>(st + OA::BYTES, B, ldb, n0, e.N, k0, wid, lane);
+  };
+  auto compute = [&](const char* sa) {
+    const char* sb = sa + OA::BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = OA::frag(sa, wr * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = OB::frag(sb, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto step = [&](int t, auto sc) {
+    constexpr int S = decltype(sc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of step t landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                       // every wave's; step t-1's stage is free
+    asm volatile("" ::: "memory");
+    if (t + 1 < nk) issue(t + 1, smem + (1 - S) * STAGE);
+    compute(smem + S * STAGE);
+  };
+  issue(0, smem);
+  for (int t = 0; t < nk; t += 2) {
+    step(t, IC<0>{});
+    if (t + 1 < nk) step(t + 1, IC<1>{});
+  }
+  float* stg = (float*)smem;
+  constexpr int CPR = 128 / 8;  // 8-column groups per row: 32 rows per pass of 512 threads
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    __syncthreads();  // every wave's last operand reads / the previous half's epilogue reads are done
+    if ((wr >> 1) == part) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[((wr & 1) * 64 + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * 64 + j * 16 + (lane & 15)] =
+                acc[i][j][r] * e.alpha;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rr = p * 32 + tid / CPR, cg = tid % CPR;
+      const int64_t m = m0 + part * 128 + rr, n = n0 + cg * 8;
+      if (m < e.M) {
+        const float* src = stg + rr * LDT + cg * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_eight<EF>(e, m, n, v, false);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
 // f32 kernel (exact: v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain)
 // ----------------------------------------------------------------------------------------------
 template <bool KC>
@@ -1350,6 +1473,17 @@ static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiPar
   }
 }
 
+template <uint32_t EF>
+static void launch_bf16_big_ef(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e,
+                               hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_big_kernel<true, EF>), dim3(nblk), dim3(512), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_big_kernel<false, EF>), dim3(nblk), dim3(512), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
+}
+
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
 #define VS_EPI_SWITCH(F, CALL)                                                             \
   switch (F) {                                                                             \
@@ -1360,6 +1494,12 @@ static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiPar
     case VS_EPI_GELU_BWD: CALL((uint32_t)VS_EPI_GELU_BWD); break;                          \
     default: CALL(kEpiRuntime); break;                                                     \
   }
+
+static void launch_bf16_big(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
+#define L_(EF) launch_bf16_big_ef<EF>(d, nblk, g, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
+}
 
 template <int BM, int BN>
 static void launch_bf16(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
@@ -1698,6 +1838,20 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     if (d->N == 64) launch_bf16_slab<1>(d, (unsigned)G, e, s);
     else if (d->N == 128) launch_bf16_slab<2>(d, (unsigned)G, e, s);
     else launch_bf16_slab<3>(d, (unsigned)G, e, s);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
+  // big-tile path: MFMA-heavy products (K >= 512, N >= 512, N % 128 == 0: the ViT-Base block)
+  static const int no_big = getenv_flag5("VSPIKE_NO_BIG");
+  if (!no_big && d->dtype == VS_BF16 && d->a_kcontig && d->M >= 4096 && d->N >= 512 && d->N % 128 == 0 &&
+      d->K >= 512 && d->K % 64 == 0 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
+      !(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM))) {
+    GridMap g;
+    g.tiles_m = (int)cdiv(d->M, 256);
+    g.tiles_n = (int)(d->N / 128);
+    g.splits = 1;
+    g.k_per_split = d->K;
+    launch_bf16_big(d, (unsigned)((int64_t)g.tiles_m * g.tiles_n), g, e, s);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
