@@ -106,6 +106,9 @@ def main():
         bq, bd, b1 = r(3 * Db, dt=torch.float32), r(Db, dt=torch.float32), r(Fb, dt=torch.float32)
         qkv, a_, pre, o32 = r(M, 3 * Db), r(M, Fb), r(M, Fb), torch.empty(M, Db, device=dev)
         res = r(M, Db, dt=torch.float32)
+        dWb = {k: torch.zeros(*s, device=dev) for k, s in (("qkv", (3 * Db, Db)), ("p", (Db, Db)), ("1", (Fb, Db)),
+                                                           ("2", (Db, Fb)))}
+        dbb = {k: torch.zeros(s, device=dev) for k, s in (("qkv", 3 * Db), ("p", Db), ("1", Fb), ("2", Db))}
         for name, fn, nb, fl in (
                 ("base fwd qkv", lambda: ops.linear(x, wq, qkv, bias=bq), M * Db * 2 + M * 3 * Db * 2, 2 * M * Db * 3 * Db),
                 ("base fwd proj +res", lambda: ops.linear(x, wp, o32, bias=bd, epilogue=L.EPI_RESIDUAL, residual=res,
@@ -116,7 +119,14 @@ def main():
                                                          ld_residual=Db), M * Fb * 2 + M * Db * 8, 2 * M * Db * Fb),
                 ("base dx da*gelu'", lambda: ops.linear_dx(x, w2, a_, epilogue=L.EPI_GELU_BWD, aux_in=pre, ld_aux_in=Fb),
                  M * Db * 2 + 2 * M * Fb * 2, 2 * M * Db * Fb),
-                ("base dx dh2 (f32)", lambda: ops.linear_dx(h, w1, o32), M * Fb * 2 + M * Db * 4, 2 * M * Db * Fb)):
+                ("base dx dh2 (f32)", lambda: ops.linear_dx(h, w1, o32), M * Fb * 2 + M * Db * 4, 2 * M * Db * Fb),
+                ("base dWqkv [2304,768]", lambda: ops.linear_dw(qkv, x, dWb["qkv"], db=dbb["qkv"]), M * 4 * Db * 2,
+                 2 * M * Db * 3 * Db),
+                ("base dWp [768,768]", lambda: ops.linear_dw(x, x, dWb["p"], db=dbb["p"]), M * 2 * Db * 2, 2 * M * Db * Db),
+                ("base dW1 [3072,768]", lambda: ops.linear_dw(a_, x, dWb["1"], db=dbb["1"]), M * (Db + Fb) * 2,
+                 2 * M * Db * Fb),
+                ("base dW2 [768,3072]", lambda: ops.linear_dw(x, a_, dWb["2"], db=dbb["2"]), M * (Db + Fb) * 2,
+                 2 * M * Db * Fb)):
             report(name, timeit(fn, a.reps), nb, fl)
     if a.only in ("", "copy"):
         # the chip's practical streaming rates on the same byte counts (torch's own kernels)

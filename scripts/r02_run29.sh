@@ -1,12 +1,16 @@
 #!/bin/bash
+# dW product sweep: ring/register modes, tile heights, split counts (isolated microbench), plus a
+# rocprof split of kernel vs reduce time at the default plan.
 export TMPDIR=/tmp
-set -e
+M="python scripts/microbench.py --only gemm:dW --reps 50"
 scripts/gpu_steps.sh \
-  "t_big|300|python -u -m pytest tests/test_gpu_ops.py -q -x -k 'big_tile or gemm_layouts or epilogues' --timeout 200 --timeout-method thread -p no:cacheprovider" \
-  "mb_big|200|python scripts/microbench.py --only base --reps 10" \
-  "mb_old|200|VSPIKE_NO_BIG=1 python scripts/microbench.py --only base --reps 10" \
-  "t_models|400|python -u -m pytest tests/test_gpu_models.py tests/test_gpu_parity_bench.py -q -x --timeout 200 --timeout-method thread -p no:cacheprovider" \
-  "c3|300|python bench.py --model vmae_video --neurons 512 --lr 5e-8 --no-cpu-baseline --steps 20 --warmup 5 --profile-steps 3" \
-  "c2|120|python bench.py --no-cpu-baseline --profile-steps 0"
-for f in c3 c2; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/$f.log | head -1) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log | head -1)"; done
-cat gpurun_out/mb_big.log gpurun_out/mb_old.log | grep base
+  "dw_def|90|$M" \
+  "dw_reg|90|VSPIKE_DW_MODE=0 $M" \
+  "dw_s8|90|VSPIKE_DW_SPLITS=8 $M" \
+  "dw_s12|90|VSPIKE_DW_SPLITS=12 $M" \
+  "dw_s42|90|VSPIKE_DW_SPLITS=42 $M" \
+  "dw_bm64|90|VSPIKE_DW_BM=64 $M" \
+  "dw_bm128|90|VSPIKE_DW_BM=128 $M" \
+  "dw_prof|120|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/dw_prof -o run -- python3 scripts/microbench.py --only gemm:dW --reps 50" || exit $?
+for f in dw_def dw_reg dw_s8 dw_s12 dw_s42 dw_bm64 dw_bm128; do echo "== $f"; grep "^dW" gpurun_out/$f.log; done
+f=$(find gpurun_out/dw_prof -name '*kernel_stats.csv' | head -1); python3 scripts/kstats.py "$f" 1 12

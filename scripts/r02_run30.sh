@@ -1,12 +1,14 @@
 #!/bin/bash
-# GPU checkpoint at HEAD: full GPU tests, smoke, default bench, rocprof kernel stats, PMC passes.
+# dW kernel v2 (BN in {64,128}, step-invariant DMA offsets, split-order reduce): tests + sweep.
 export TMPDIR=/tmp
-set -e
+M="python scripts/microbench.py --only gemm:dW --reps 50"
 scripts/gpu_steps.sh \
-  "tests|700|python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider" \
-  "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "bench|300|python bench.py" \
-  "prof|240|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline"
-scripts/pmc_traffic.sh r02_v3
-ONLY=attn scripts/pmc_attn.sh gpurun_out/pmc_attn
-ONLY=gemm:dW scripts/pmc_attn.sh gpurun_out/pmc_dw
+  "dw_tests|300|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k 'dw or splitk'" \
+  "dw_def|90|$M" \
+  "dw_bn64|90|VSPIKE_DW_BN=64 $M" \
+  "dw_bn128|90|VSPIKE_DW_BN=128 $M" \
+  "dw_bn128_s16|90|VSPIKE_DW_BN=128 VSPIKE_DW_SPLITS=16 $M" \
+  "dw_bn128_s24|90|VSPIKE_DW_BN=128 VSPIKE_DW_SPLITS=24 $M" \
+  "dw_prof|120|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/dw_prof -o run -- python3 scripts/microbench.py --only gemm:dW --reps 50" || exit $?
+for f in dw_def dw_bn64 dw_bn128 dw_bn128_s16 dw_bn128_s24; do echo "== $f"; grep "^dW" gpurun_out/$f.log; done
+f=$(find gpurun_out/dw_prof -name '*kernel_stats.csv' | head -1); python3 scripts/kstats.py "$f" 1 12

@@ -327,14 +327,16 @@ def test_gemm_splitk_atomic_accumulates(dtype, ws, shape):
         assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("bm", [64, 128, 192])
 @pytest.mark.parametrize("shape", [(192, 768, 3136 + 40), (576, 192, 1568), (200, 72, 999)])
-def test_dw_kernel_every_tile_height(monkeypatch, bm, shape):
-    """The token-reduction dW kernel (gemm_dw.hip) at every tile height, with ragged tiles, a
+def test_dw_kernel_every_tile_height(monkeypatch, bm, bn, shape):
+    """The token-reduction dW kernel (gemm_dw.hip) at every tile shape, with ragged tiles, a
     partial last token step, swapped operands (M > N: C stored transposed, bias = column sums of
     the swapped B) and the fixed-order split reduce: bit-identical reruns."""
     from vspike import ops
     monkeypatch.setenv("VSPIKE_DW_BM", str(bm))
+    monkeypatch.setenv("VSPIKE_DW_BN", str(bn))
     M, N, K = shape
     dy = _rand(K, M, seed=18).to(torch.bfloat16).to(DEV)
     x = _rand(K, N, seed=19).to(torch.bfloat16).to(DEV)

@@ -15,8 +15,8 @@ struct DwGrid {
 
 struct DwPlan {
   bool valid, swap;  // swap: the kernel runs on (B, A) and stores C transposed
-  bool dma;          // LDS-DMA ring kernel (VSPIKE_DW_MODE=1) instead of register staging
-  int BM;            // output rows per tile (64, 128 or 192); 64 columns
+  int BM, BN;        // output tile: BM (64, 128, 192) rows of the narrow operand x BN (64, 128) columns
+  int stages;        // LDS-DMA ring depth (3 or 4)
   DwGrid g;
   int64_t part_floats, sum_floats;
 };

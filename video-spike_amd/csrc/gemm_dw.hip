@@ -8,19 +8,21 @@
 // Shape: K = B*N tokens (25,088 at the bench) >> M, N (192..1536).  Both operands are token-major
 // ([K, features] rows), so the product is a reduction over K and its output is small (0.04-1.2 MB):
 // the only parallelism is splitting K.  Design (MI355X):
-//   * tile = BM x 64 outputs with BM up to 192 = the WHOLE narrow operand (the host swaps A and B so
-//     that A is the narrow one, storing C transposed), so the wide operand is streamed exactly once
-//     per token slab and only the narrow one is re-read (from L2: the tiles of one token slab are
-//     consecutive logical blocks, which the XCD remap puts on one XCD);
-//   * one token slab (split) per workgroup, 4-deep LDS-DMA ring of 64-token steps (asm
-//     global_load_lds, counted vmcnt across raw s_barriers, as gemm_bf16_ring_kernel);
+//   * tile = BM x BN outputs, BM up to 192 = the WHOLE narrow operand (the host swaps A and B so
+//     that A is the narrow one, storing C transposed), BN = 64 or 128 columns of the wide one, so the
+//     wide operand is streamed exactly once per token slab and only the narrow one is re-read (from
+//     L2: the tiles of one token slab are consecutive logical blocks, which the XCD remap puts on
+//     one XCD).  BN = 128 halves the narrow re-reads and doubles the MFMAs per LDS-DMA byte;
+//   * one token slab (split) per workgroup, 3- or 4-deep LDS-DMA ring of 64-token steps (asm
+//     global_load_lds with step-invariant per-lane offsets from one SGPR base per operand, counted
+//     vmcnt across raw s_barriers, as gemm_bf16_ring_kernel);
 //   * the f32 partial tile is written in MFMA FRAGMENT order (each wave-instruction a contiguous
 //     1 KiB: no LDS staging), and gemm_dw_reduce adds the splits IN SPLIT ORDER and scatters into C
 //     (C += sum): bitwise reproducible, no atomics — also for the fused bias gradient, whose
 //     per-split sums go through the same workspace;
-//   * the split count comes from a small cost model (plan_dw): enough workgroups to stream at the
-//     chip's rate, few enough that the partial tiles (#workgroups x tile bytes) stay a small
-//     fraction of the operand bytes.
+//   * tile shape and split count come from a small cost model (plan_dw): enough workgroups to
+//     stream at the chip's rate, few enough that the partial tiles (#workgroups x tile bytes) stay a
+//     small fraction of the operand bytes.
 #include <cstdlib>
 #include <type_traits>
 
@@ -69,35 +71,51 @@ __device__ __forceinline__ bf16x8 dw_frag(const char* img, int rb, int kk, int l
 
 // SUMS: 0 none; 1 row sums of A (the bias gradient when A is the dY operand), written by the
 // nt == 0 tiles; 2 column sums of B (when the host swapped the operands), by the mt == 0 tiles.
-// NW = 8 waves (two per SIMD: one wave's DMA issue and LDS reads overlap its partner's MFMAs) in a
-// 4 x 2 grid of (BM/4) x 32 wave tiles, or NW = 4 in a 4 x 1 grid of (BM/4) x 64.
-// Partial tiles are stored in tile-fragment order: float4 ((rowfrag * 4 + colfrag) * 64 + lane),
-// rowfrag / colfrag = the 16-row / 16-column block within the BM x 64 tile.
-template <int BM, int SUMS, int NW, int NSTG = 4>
-__global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
-                                                             const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
-                                                             int64_t K, DwGrid g, float* __restrict__ part,
-                                                             float* __restrict__ sums) {
-  constexpr int NA = BM / 64;             // 64-row A images per stage
+// Tile BM x BN (BM, BN multiples of 64: NA + NB 64-column LDS images per token step), 8 waves
+// (two per SIMD: one wave's DMA issue and LDS reads overlap its partner's MFMAs) in a 4 x 2 grid
+// of (BM/4) x (BN/2) wave tiles.  Per 64-token step each wave issues piece `wid` (8 token rows x
+// 128 B) of every image; its per-lane source offsets are step-invariant (column clamps included)
+// and computed once, so a step's DMA is one SGPR base per operand + NA + NB instructions.
+// Partial tiles are stored in tile-fragment order: float4 ((rowfrag * BN/16 + colfrag) * 64 + lane),
+// rowfrag / colfrag = the 16-row / 16-column block within the tile.
+template <int BM, int BN, int SUMS, int NSTG>
+__global__ __launch_bounds__(512, 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
+                                                         const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
+                                                         int64_t K, DwGrid g, float* __restrict__ part,
+                                                         float* __restrict__ sums) {
+  constexpr int NA = BM / 64, NB = BN / 64, NI = NA + NB;  // 64-column LDS images per stage
   constexpr int IMG = 8192;
-  constexpr int STAGE = (NA + 1) * IMG;   // A images then the B image
-  constexpr int PER = (NA + 1) * (8 / NW);  // DMA wave-instructions per stage
-  constexpr int WM = BM / 4, FI = WM / 16, FJ = NW == 8 ? 2 : 4;
-  static_assert(NSTG == 3 || NSTG == 4, "3- or 4-stage ring");
+  constexpr int STAGE = NI * IMG;
+  constexpr int PER = NI;                 // DMA wave-instructions per wave per stage
+  constexpr int WM = BM / 4, FI = WM / 16, WN = BN / 2, FJ = WN / 16, CF = BN / 16;
+  static_assert(NSTG >= 2 && NSTG <= 4, "2- to 4-stage ring");
   __shared__ __attribute__((aligned(16))) char st0[STAGE];
   __shared__ __attribute__((aligned(16))) char st1[STAGE];
-  __shared__ __attribute__((aligned(16))) char st2[STAGE];
+  __shared__ __attribute__((aligned(16))) char st2[NSTG >= 3 ? STAGE : 16];
   __shared__ __attribute__((aligned(16))) char st3[NSTG == 4 ? STAGE : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rw = wid & 3, cw = wid >> 2;  // wave tile: rows rw*WM.., columns cw*FJ*16..
+  const int rw = wid & 3, cw = wid >> 2;  // wave tile: rows rw*WM.., columns cw*WN..
   const int tiles = g.tiles_m * g.tiles_n;
   const int t = xcd_remap(blockIdx.x, gridDim.x);   // one token slab's tiles are consecutive: one XCD
   const int split = t / tiles, rem = t % tiles, mt = rem / g.tiles_n, nt = rem % g.tiles_n;
-  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * 64;
+  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * BN;
   const int nk_all = (int)((K + 63) / 64);
   const int ks0 = split * g.ksteps, ks1 = ks0 + g.ksteps < nk_all ? ks0 + g.ksteps : nk_all;
   const int nk = ks1 - ks0;
+
+  // this lane's DMA position: token row krow of the step, 16-B chunk cch of its image row; columns
+  // past the operand re-read its last 8 (finite data, never stored)
+  const int krow = wid * 8 + (lane >> 3);
+  const int cch = (lane & 7) ^ dw_swz(krow);
+  auto col_of = [&](int j) -> int64_t {
+    const int64_t c0 = j < NA ? m0 + j * 64 : n0 + (j - NA) * 64;
+    const int64_t cols = j < NA ? M : N;
+    return c0 + cch * 8 <= cols - 8 ? c0 + cch * 8 : cols - 8;
+  };
+  uint32_t off[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) off[j] = (uint32_t)(((int64_t)krow * (j < NA ? lda : ldb) + col_of(j)) * 2);
 
   f32x4 acc[FI][FJ];
 #pragma unroll
@@ -111,10 +129,19 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
 
   auto issue = [&](int s, char* stg) {
     const int64_t k0 = (int64_t)(ks0 + s) * 64;
-    const int kv = K - k0 < 64 ? (int)(K - k0) : 64;
+    const char* ba = (const char*)(A + k0 * lda);
+    const char* bb = (const char*)(B + k0 * ldb);
+    if (K - k0 >= 64) {
 #pragma unroll
-    for (int a = 0; a < NA; ++a) dw_dma<NW>(stg + a * IMG, A, lda, m0 + a * 64, M, k0, kv, wid, lane);
-    dw_dma<NW>(stg + NA * IMG, B, ldb, n0, N, k0, kv, wid, lane);
+      for (int j = 0; j < NI; ++j) glds16_asm_so(j < NA ? ba : bb, off[j], stg + j * IMG + wid * 1024);
+    } else {  // the reduction's last, partial step: token rows past K re-read row K-1 (zeroed in LDS)
+      const int kv = (int)(K - k0);
+      const int kk = krow < kv ? krow : kv - 1;
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        glds16_asm_so(j < NA ? ba : bb, (uint32_t)(((int64_t)kk * (j < NA ? lda : ldb) + col_of(j)) * 2),
+                      stg + j * IMG + wid * 1024);
+    }
   };
   auto compute = [&](const char* stg) {
 #pragma unroll
@@ -126,7 +153,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
         af[i] = dw_frag(stg + (r >> 6) * IMG, r & 63, kk, lane);
       }
 #pragma unroll
-      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, (cw * FJ + j) * 16, kk, lane);
+      for (int j = 0; j < FJ; ++j) {
+        const int cidx = cw * WN + j * 16;
+        bfr[j] = dw_frag(stg + (NA + (cidx >> 6)) * IMG, cidx & 63, kk, lane);
+      }
       if (sum_on) {
         if constexpr (SUMS == 1) {
 #pragma unroll
@@ -149,17 +179,18 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
   // rows k >= k_valid of a partial last step hold re-read data: zero them in every image
   auto zero_tail = [&](char* stg, int kv) {
     const int bytes = (64 - kv) * 128;
-    for (int a = 0; a <= NA; ++a)
-      for (int o = tid * 16; o < bytes; o += NW * 64 * 16) *(uint4*)(stg + a * IMG + kv * 128 + o) = make_uint4(0, 0, 0, 0);
+    for (int a = 0; a < NI; ++a)
+      for (int o = tid * 16; o < bytes; o += 512 * 16) *(uint4*)(stg + a * IMG + kv * 128 + o) = make_uint4(0, 0, 0, 0);
   };
+  auto stage_ptr = [&](int i) -> char* { return i == 0 ? st0 : i == 1 ? st1 : i == 2 ? st2 : st3; };
   auto step = [&](int s, auto sc) {
     constexpr int S = decltype(sc)::value;
-    char* cur = S == 0 ? st0 : S == 1 ? st1 : S == 2 ? st2 : st3;
-    // stage of step s + NSTG - 1 (the one step s - 1 used)
-    char* far = NSTG == 4 ? (S == 0 ? st3 : S == 1 ? st0 : S == 2 ? st1 : st2) : (S == 0 ? st2 : S == 1 ? st0 : st1);
+    char* cur = stage_ptr(S);
+    char* far = stage_ptr((S + NSTG - 1) % NSTG);  // the stage step s - 1 used
     // steps s+1 .. s+NSTG-2 may stay in flight
-    if (NSTG == 4 && s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-    else if (s + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    const int ahead = nk - 1 - s;
+    if (NSTG >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (NSTG >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's step-s pieces landed; step s-1's stage is free
@@ -174,24 +205,24 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
     if (s + NSTG - 1 < nk) issue(s + NSTG - 1, far);
     compute(cur);
   };
-  if (nk > 0) issue(0, st0);
-  if (nk > 1) issue(1, st1);
-  if (NSTG == 4 && nk > 2) issue(2, st2);
+#pragma unroll
+  for (int i = 0; i < NSTG - 1; ++i)
+    if (i < nk) issue(i, stage_ptr(i));
   for (int s = 0; s < nk; s += NSTG) {
     step(s, IC<0>{});
-    if (s + 1 < nk) step(s + 1, IC<1>{});
-    if (s + 2 < nk) step(s + 2, IC<2>{});
-    if (NSTG == 4 && s + 3 < nk) step(s + 3, IC<3>{});
+    if (s + 1 < nk) step(s + 1, IC<1 % NSTG>{});
+    if (NSTG >= 3 && s + 2 < nk) step(s + 2, IC<2 % NSTG>{});
+    if (NSTG >= 4 && s + 3 < nk) step(s + 3, IC<3 % NSTG>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * 64));
+  float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * BN));
 #pragma unroll
   for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
       const f32x4 v = acc[i][j];
-      pt[((rw * FI + i) * 4 + cw * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
+      pt[((rw * FI + i) * CF + cw * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
     }
   if (sum_on) {
     // lane groups g = lane >> 4 hold disjoint k; rows / columns (lane & 15)
@@ -209,169 +240,27 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_dw_kernel(const bf16_t* __res
 #pragma unroll
         for (int i = 0; i < FI; ++i) so[rw * WM + i * 16 + lane] = sacc[i];
       } else if constexpr (SUMS == 2) {
-        float* so = sums + ((int64_t)nt * g.splits + split) * 64;
+        float* so = sums + ((int64_t)nt * g.splits + split) * BN;
 #pragma unroll
-        for (int j = 0; j < FJ; ++j) so[(cw * FJ + j) * 16 + lane] = sacc[j];
+        for (int j = 0; j < FJ; ++j) so[cw * WN + j * 16 + lane] = sacc[j];
       }
     }
   }
 }
 
-// The same product with REGISTER-staged operands: per 64-token step each thread loads (NA+1)*2
-// 16-B chunks with global_load_dwordx4 (a few issue cycles each, against ~60-180 for an LDS-DMA
-// piece, which made the DMA ring above issue-bound at ~26 GB/s per CU with one wave per SIMD),
-// two steps in flight in two register sets, written into a double-buffered LDS image one step
-// ahead of the MFMAs (guide T14: issue early, write late).  64 KB of LDS at BM = 192: two
-// workgroups per CU, 8 waves to hide the load latency.  Token rows past K load zeros.
-template <int BM, int SUMS>
-__global__ __launch_bounds__(256, 2) void gemm_dw_reg_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
-                                                             const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
-                                                             int64_t K, DwGrid g, float* __restrict__ part,
-                                                             float* __restrict__ sums) {
-  constexpr int NA = BM / 64;
-  constexpr int IMG = 8192;
-  constexpr int STAGE = (NA + 1) * IMG;
-  constexpr int CPT = (NA + 1) * 2;       // 16-B chunks per thread per step
-  constexpr int WM = BM / 4, FI = WM / 16, FJ = 4;
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles = g.tiles_m * g.tiles_n;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = t / tiles, rem = t % tiles, mt = rem / g.tiles_n, nt = rem % g.tiles_n;
-  const int64_t m0 = (int64_t)mt * BM, n0 = (int64_t)nt * 64;
-  const int nk_all = (int)((K + 63) / 64);
-  const int ks0 = split * g.ksteps, ks1 = ks0 + g.ksteps < nk_all ? ks0 + g.ksteps : nk_all;
-  const int nk = ks1 - ks0;
-
-  // chunk c of this thread: image im = c / 2 (im == NA: B), index i = tid + 256 (c & 1):
-  // k = i / 8, 16-B column chunk q = i % 8 (one 128-B segment per 8 lanes)
-  const int kq0 = tid >> 3, q = tid & 7;  // i = tid (+256 -> k + 32)
-  auto load = [&](uint4 (&r)[CPT], int s) {
-    const int64_t k0 = (int64_t)(ks0 + s) * 64;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int im = c >> 1, k = kq0 + 32 * (c & 1);
-      const bf16_t* p = im < NA ? A : B;
-      const int64_t ld = im < NA ? lda : ldb;
-      const int64_t col = (im < NA ? m0 + im * 64 : n0) + q * 8;
-      const int64_t lim = im < NA ? M : N;
-      const bool ok = k0 + k < K && col < lim;
-      r[c] = ok ? *(const uint4*)(p + (k0 + k) * ld + col) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto store = [&](const uint4 (&r)[CPT], char* stg) {
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int im = c >> 1, k = kq0 + 32 * (c & 1);
-      *(uint4*)(stg + im * IMG + k * 128 + ((q ^ dw_swz(k)) << 4)) = r[c];
-    }
-  };
-
-  f32x4 acc[FI][FJ];
-#pragma unroll
-  for (int i = 0; i < FI; ++i)
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool sum_on = (SUMS == 1 && nt == 0) || (SUMS == 2 && mt == 0 && wid == 0);
-  float sacc[SUMS == 2 ? FJ : FI];
-#pragma unroll
-  for (int i = 0; i < (SUMS == 2 ? FJ : FI); ++i) sacc[i] = 0.f;
-
-  auto compute = [&](const char* stg) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[FI], bfr[FJ];
-#pragma unroll
-      for (int i = 0; i < FI; ++i) {
-        const int r = wid * WM + i * 16;
-        af[i] = dw_frag(stg + (r >> 6) * IMG, r & 63, kk, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < FJ; ++j) bfr[j] = dw_frag(stg + NA * IMG, j * 16, kk, lane);
-      if (sum_on) {
-        if constexpr (SUMS == 1) {
-#pragma unroll
-          for (int i = 0; i < FI; ++i)
-#pragma unroll
-            for (int qq = 0; qq < 8; ++qq) sacc[i] += (float)af[i][qq];
-        } else if constexpr (SUMS == 2) {
-#pragma unroll
-          for (int j = 0; j < FJ; ++j)
-#pragma unroll
-            for (int qq = 0; qq < 8; ++qq) sacc[j] += (float)bfr[j][qq];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  uint4 ra[CPT], rb[CPT];
-  if (nk > 0) load(ra, 0);
-  if (nk > 1) load(rb, 1);
-  if (nk > 0) store(ra, lds);                 // waits for step 0's loads only (compiler-counted)
-  if (nk > 2) load(ra, 2);
-  __syncthreads();
-  // step s computes from lds[s & 1]; meanwhile step s+1 (regs) is stored into the other half and
-  // step s+3 is loaded into the freed register set
-  auto step = [&](int s, uint4 (&cur)[CPT], uint4 (&nxt)[CPT]) {
-    compute(lds + (s & 1) * STAGE);
-    if (s + 1 < nk) store(cur, lds + ((s + 1) & 1) * STAGE);
-    if (s + 3 < nk) load(cur, s + 3);
-    __syncthreads();
-    (void)nxt;
-  };
-  for (int s = 0; s < nk; s += 2) {
-    step(s, rb, ra);
-    if (s + 1 < nk) step(s + 1, ra, rb);
-  }
-
-  float4* pt = (float4*)(part + ((int64_t)rem * g.splits + split) * (BM * 64));
-#pragma unroll
-  for (int i = 0; i < FI; ++i)
-#pragma unroll
-    for (int j = 0; j < FJ; ++j) {
-      const f32x4 v = acc[i][j];
-      pt[((wid * FI + i) * FJ + j) * 64 + lane] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  if (sum_on) {
-    constexpr int NS = SUMS == 2 ? FJ : FI;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      float v = sacc[i];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      sacc[i] = v;
-    }
-    if (lane < 16) {
-      if constexpr (SUMS == 1) {
-        float* so = sums + ((int64_t)mt * g.splits + split) * BM;
-#pragma unroll
-        for (int i = 0; i < FI; ++i) so[wid * WM + i * 16 + lane] = sacc[i];
-      } else if constexpr (SUMS == 2) {
-        float* so = sums + ((int64_t)nt * g.splits + split) * 64;
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) so[j * 16 + lane] = sacc[j];
-      }
-    }
-  }
-}
-
-// C (+)= sum over splits of the fragment-order partial tiles.  A workgroup owns 64 float4 of one
-// tile (one per lane); wave w sums splits w, w+4, ... (all loads of its share issued before the
-// adds), then the four wave sums are added in wave order through LDS — a fixed order that depends
-// only on the split count (bitwise reproducible).  Blocks after the tile blocks reduce the bias
-// sums.  TRANS: the kernel ran on swapped operands, so its tile element (m, n) is C[n][m].
-template <int BM, bool TRANS>
+// C (+)= sum over splits of the fragment-order partial tiles, many splits (the C2 shapes: 21-49).
+// A workgroup owns 64 float4 of one tile (one per lane); wave w sums splits w, w+16, ... (four loads
+// in flight each), then the 16 wave sums are added in wave order through LDS — a fixed order that
+// depends only on the split count (bitwise reproducible).  Blocks after the tile blocks reduce the
+// bias sums (8 loads in flight per thread).
+template <int BM, int BN, bool TRANS>
 __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__ part, const float* __restrict__ sums,
                                                        DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
                                                        int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
                                                        int sum_tiles, int sum_w) {
-  constexpr int Q = BM * 16;  // float4 per tile
-  constexpr int NWR = 16;     // waves per block: wave w sums splits w, w + 16, ... (<= 4 loads in flight each)
+  constexpr int Q = BM * BN / 4;  // float4 per tile
+  constexpr int CF = BN / 16;
+  constexpr int NWR = 16;
   const int tiles = g.tiles_m * g.tiles_n;
   const int64_t blk = blockIdx.x;
   const int64_t tile_blocks = (int64_t)tiles * (Q / 64);
@@ -380,7 +269,7 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
     __shared__ float4 red[NWR][64];
     const int tile = (int)(blk / (Q / 64));
     const int q = (int)(blk % (Q / 64)) * 64 + lane;
-    const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
+    const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * BN)) + q;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int sp0 = w; sp0 < g.splits; sp0 += NWR * 4) {
       float4 v[4];
@@ -402,9 +291,9 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
       const float4 o = red[k][lane];
       s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
     }
-    const int f = q >> 6, rf = f >> 2, cf = f & 3;
+    const int f = q >> 6, rf = f / CF, cf = f % CF;
     const int mt = tile / g.tiles_n, nt = tile % g.tiles_n;
-    const int64_t n = (int64_t)nt * 64 + cf * 16 + (lane & 15);
+    const int64_t n = (int64_t)nt * BN + cf * 16 + (lane & 15);
     const int64_t mb = (int64_t)mt * BM + rf * 16 + (lane >> 4) * 4;
     const float vv[4] = {s.x, s.y, s.z, s.w};
     if (n < N) {
@@ -426,7 +315,7 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
   const float* p = sums + st * (int64_t)g.splits * sum_w + off;
   float s = 0.f;
   int sp = 0;
-  for (; sp + 8 <= g.splits; sp += 8) {  // 8 loads in flight (a serial chain of 50 loads took ~10 us)
+  for (; sp + 8 <= g.splits; sp += 8) {
     float v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(sp + u) * sum_w];
@@ -437,30 +326,42 @@ __global__ __launch_bounds__(1024) void gemm_dw_reduce(const float* __restrict__
   bias_out[e] += s;
 }
 
-// The same reduction for few splits (S <= 8: the ViT-Base products, whose many output tiles leave
-// one or two splits): one float4 of a tile per thread in 256-thread blocks, the splits added in
-// split order (the 16-wave layout above left 15 of 16 waves idle there and ran latency-bound,
-// 363 us for a 9.4 MB dW at S = 1).  TRANS stores the 4 consecutive m of a lane as one float4.
-template <int BM, bool TRANS>
+// Few splits (S <= 8: ViT-Base's many output tiles leave one to three): one float4 of a tile per
+// thread, the splits added in split order (a fixed order: bitwise reproducible).  Threads after the
+// tile items reduce the bias sums.  TRANS: the kernel ran on swapped operands, so its tile element
+// (m, n) is C[n][m] (the 4 consecutive m of a lane are then one float4 of C).
+template <int BM, int BN, bool TRANS>
 __global__ __launch_bounds__(256) void gemm_dw_reduce_few(const float* __restrict__ part, const float* __restrict__ sums,
-                                                          DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
-                                                          int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
-                                                          int sum_tiles, int sum_w) {
-  constexpr int Q = BM * 16;  // float4 per tile
+                                                      DwGrid g, int64_t M, int64_t N, float* __restrict__ c,
+                                                      int64_t ldc, float* __restrict__ bias_out, int64_t sum_len,
+                                                      int sum_tiles, int sum_w) {
+  constexpr int Q = BM * BN / 4;  // float4 per tile
+  constexpr int CF = BN / 16;
   const int tiles = g.tiles_m * g.tiles_n;
   const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tile_items = (int64_t)tiles * Q;
+  const int S = g.splits;
   if (item < tile_items) {
     const int tile = (int)(item / Q), q = (int)(item % Q), lane = q & 63;
-    const float4* p = (const float4*)(part + (int64_t)tile * g.splits * (BM * 64)) + q;
+    const float4* p = (const float4*)(part + (int64_t)tile * S * (BM * BN)) + q;
     float4 sum = p[0];
-    for (int sp = 1; sp < g.splits; ++sp) {
+    int sp = 1;
+    for (; sp + 8 <= S; sp += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(sp + u) * Q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sum.x += v[u].x; sum.y += v[u].y; sum.z += v[u].z; sum.w += v[u].w;
+      }
+    }
+    for (; sp < S; ++sp) {
       const float4 o = p[(int64_t)sp * Q];
       sum.x += o.x; sum.y += o.y; sum.z += o.z; sum.w += o.w;
     }
-    const int f = q >> 6, rf = f >> 2, cf = f & 3;
+    const int f = q >> 6, rf = f / CF, cf = f % CF;
     const int mt = tile / g.tiles_n, nt = tile % g.tiles_n;
-    const int64_t n = (int64_t)nt * 64 + cf * 16 + (lane & 15);
+    const int64_t n = (int64_t)nt * BN + cf * 16 + (lane & 15);
     const int64_t mb = (int64_t)mt * BM + rf * 16 + (lane >> 4) * 4;
     if (n >= N) return;
     const float vv[4] = {sum.x, sum.y, sum.z, sum.w};
@@ -485,9 +386,17 @@ __global__ __launch_bounds__(256) void gemm_dw_reduce_few(const float* __restric
   if (e >= sum_len) return;
   const int64_t st = e / sum_w, off = e % sum_w;
   if (st >= sum_tiles) return;
-  const float* ps = sums + st * (int64_t)g.splits * sum_w + off;
+  const float* ps = sums + st * (int64_t)S * sum_w + off;
   float acc = 0.f;
-  for (int sp = 0; sp < g.splits; ++sp) acc += ps[(int64_t)sp * sum_w];
+  int sp = 0;
+  for (; sp + 8 <= S; sp += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ps[(int64_t)(sp + u) * sum_w];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; sp < S; ++sp) acc += ps[(int64_t)sp * sum_w];
   bias_out[e] += acc;
 }
 
@@ -666,51 +575,60 @@ static int env_int(const char* name, int dflt) {
   return v && v[0] ? atoi(v) : dflt;
 }
 
-// Cost model (microseconds): the workgroups stream their token slab of both operands (L2/HBM ->
-// LDS at ~80 GB/s per CU), then the partial tiles are written and re-read by the reduce (at ~5 TB/s
-// each way), plus the reduce launch.  Splits keep >= 8 token steps each.
+// Cost model (microseconds), fitted to rocprof durations of the C2 shapes: a launch pays ~10 us of
+// fixed cost (dispatch, the prologue burst of every workgroup's first stages, the partial-tile store
+// burst at the end, the reduce launch); a 64-token step costs ~0.25 us + 0.02 us per MFMA of a wave
+// (0.49 us at 192 x 64, 0.73 us at 192 x 128), and the partial tiles cost ~0.3 us per MB (stored,
+// then re-read by the reduce).  Splits keep >= 8 token steps each.  VSPIKE_DW_BM / _BN / _SPLITS /
+// _STAGES force a choice (A/B runs, tests).
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   DwPlan best = {};
   best.valid = false;
   const bool swap = M > N;
   const int64_t Ma = swap ? N : M, Nb = swap ? M : N;
   const int64_t nk = (K + 63) / 64;
-  const int force_bm = env_int("VSPIKE_DW_BM", 0);
-  const bool dma = env_int("VSPIKE_DW_MODE", 1) == 1;   // 1: 8-wave LDS-DMA ring (default), 0: register-staged
+  const int force_bm = env_int("VSPIKE_DW_BM", 0), force_bn = env_int("VSPIKE_DW_BN", 0);
+  const int force_s = env_int("VSPIKE_DW_SPLITS", 0), force_stg = env_int("VSPIKE_DW_STAGES", 0);
   double best_t = 1e30;
-  for (int BM : {64, 128, 192}) {
-    if (force_bm && BM != force_bm) continue;
-    const int64_t tm = (Ma + BM - 1) / BM, tn = (Nb + 63) / 64, tiles = tm * tn;
-    const int slots = (BM == 64 || !dma) ? 512 : 256;
-    int64_t S = slots / tiles;
-    const int force_s = env_int("VSPIKE_DW_SPLITS", 0);
-    if (force_s > 0) S = force_s;
-    if (S < 1) S = 1;
-    const int64_t smax = nk / 8 > 0 ? nk / 8 : 1;
-    if (S > smax) S = smax;
-    int64_t kps = (nk + S - 1) / S;
-    S = (nk + kps - 1) / kps;
-    const int64_t wgs = tiles * S;
-    const double per_wg = (double)kps * 64.0 * (BM + 64) * 2.0;
-    const double rate = slots == 512 ? 40e3 : 80e3;  // bytes / us per workgroup (2 or 1 per CU)
-    const double rounds = (double)((wgs + slots - 1) / slots);
-    const double part = (double)wgs * BM * 64 * 4.0;
-    const double t = rounds * per_wg / rate + 2.0 * part / 5e6 + 3.0 + (BM - Ma > 0 ? 0.0 : 0.0);
-    // wasted rows of the last A tile cost their share of the stream
-    const double waste = (double)(tm * BM - Ma) / (double)(tm * BM);
-    const double tt = t * (1.0 + 0.5 * waste);
-    if (tt < best_t) {
-      best_t = tt;
-      best.valid = true;
-      best.dma = dma;
-      best.swap = swap;
-      best.BM = BM;
-      best.g.tiles_m = (int)tm;
-      best.g.tiles_n = (int)tn;
-      best.g.splits = (int)S;
-      best.g.ksteps = (int)kps;
-      best.part_floats = (int64_t)wgs * BM * 64;
-      best.sum_floats = (int64_t)S * (tm * BM > tn * 64 ? tm * BM : tn * 64);
+  for (int BN : {64, 128}) {
+    if (force_bn && BN != force_bn) continue;
+    if (!force_bn && BN > 64 && Nb <= 64) continue;
+    for (int BM : {64, 128, 192}) {
+      if (force_bm && BM != force_bm) continue;
+      const int stage = (BM + BN) / 64 * 8192;
+      int nstg = 4 * stage <= 131072 ? 4 : 3;
+      if (force_stg == 3 || (force_stg == 4 && 4 * stage <= 131072)) nstg = force_stg;
+      const int per_cu = nstg * stage <= 81920 ? 2 : 1;
+      const int slots = 256 * per_cu;
+      const int64_t tm = (Ma + BM - 1) / BM, tn = (Nb + BN - 1) / BN, tiles = tm * tn;
+      int64_t S = force_s > 0 ? force_s : slots / tiles;
+      if (S < 1) S = 1;
+      const int64_t smax = nk / 8 > 0 ? nk / 8 : 1;
+      if (S > smax) S = smax;
+      int64_t kps = (nk + S - 1) / S;
+      S = (nk + kps - 1) / kps;
+      const int64_t wgs = tiles * S;
+      const double rounds = (double)((wgs + slots - 1) / slots);
+      const double t_step = (0.25 + 0.02 * (BM * BN / 1024)) * per_cu;
+      const double part = (double)wgs * BM * BN * 4.0;
+      double t = 10.0 + rounds * (double)kps * t_step + 0.3 * part / 1e6;
+      // rows / columns of the last tiles past the operands cost their share of the stream
+      const double waste = 1.0 - (double)(Ma * Nb) / (double)(tm * BM * tn * BN);
+      t *= 1.0 + 0.5 * waste;
+      if (t < best_t) {
+        best_t = t;
+        best.valid = true;
+        best.swap = swap;
+        best.BM = BM;
+        best.BN = BN;
+        best.stages = nstg;
+        best.g.tiles_m = (int)tm;
+        best.g.tiles_n = (int)tn;
+        best.g.splits = (int)S;
+        best.g.ksteps = (int)kps;
+        best.part_floats = wgs * BM * BN;
+        best.sum_floats = S * (tm * BM > tn * BN ? tm * BM : tn * BN);
+      }
     }
   }
   return best;
@@ -722,22 +640,23 @@ size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   return (size_t)(p.part_floats + p.sum_floats + 64) * 4;
 }
 
-template <int BM, int SUMS, bool TRANS>
+template <int BM, int BN, int SUMS, bool TRANS>
 static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* b, int64_t ldb, int64_t Nb, int64_t K,
                         const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
   const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
-  static const int stages = env_int("VSPIKE_DW_STAGES", 4);
-  if (p.dma && stages == 3)
-    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS, 8, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
+  if constexpr ((BM + BN) / 64 * 8192 * 4 <= 131072) {
+    if (p.stages == 4) {
+      hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 4>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
+                         part, sums);
+    } else {
+      hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
+                         part, sums);
+    }
+  } else {
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
                        part, sums);
-  else if (p.dma)
-    hipLaunchKernelGGL((gemm_dw_kernel<BM, SUMS, 8>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
-                       sums);
-  else
-    hipLaunchKernelGGL((gemm_dw_reg_kernel<BM, SUMS>), dim3(nwg), dim3(256), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g, part,
-                       sums);
+  }
   const int tiles = p.g.tiles_m * p.g.tiles_n;
-  const int64_t tile_blocks = (int64_t)tiles * (BM * 16 / 64);
   int64_t sum_len = 0, sum_w = 1;
   int sum_tiles = 0;
   if (SUMS == 1) {
@@ -745,20 +664,20 @@ static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* 
     sum_tiles = p.g.tiles_m;
     sum_len = Ma;
   } else if (SUMS == 2) {
-    sum_w = 64;
+    sum_w = BN;
     sum_tiles = p.g.tiles_n;
     sum_len = Nb;
   }
   // C is [M][N] of the ORIGINAL product: with TRANS the kernel's (m, n) = (original n, original m)
   if (p.g.splits <= 8) {
-    const int64_t items = (int64_t)tiles * (BM * 16) + sum_len;
-    hipLaunchKernelGGL((gemm_dw_reduce_few<BM, TRANS>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, part,
-                       sums, p.g, Ma, Nb, c, ldc, bias, sum_len, sum_tiles, (int)sum_w);
+    const int64_t items = (int64_t)tiles * (BM * BN / 4) + sum_len;
+    hipLaunchKernelGGL((gemm_dw_reduce_few<BM, BN, TRANS>), dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s,
+                       part, sums, p.g, Ma, Nb, c, ldc, bias, sum_len, sum_tiles, (int)sum_w);
     return;
   }
-  const int64_t blocks = tile_blocks + (sum_len + 1023) / 1024;
-  hipLaunchKernelGGL((gemm_dw_reduce<BM, TRANS>), dim3((unsigned)blocks), dim3(1024), 0, s, part, sums, p.g, Ma, Nb, c,
-                     ldc, bias, sum_len, sum_tiles, (int)sum_w);
+  const int64_t blocks = (int64_t)tiles * (BM * BN / 256) + (sum_len + 1023) / 1024;
+  hipLaunchKernelGGL((gemm_dw_reduce<BM, BN, TRANS>), dim3((unsigned)blocks), dim3(1024), 0, s, part, sums, p.g, Ma, Nb,
+                     c, ldc, bias, sum_len, sum_tiles, (int)sum_w);
 }
 
 int launch_dw(const vs_gemm_desc* d, hipStream_t s) {
@@ -777,20 +696,26 @@ int launch_dw(const vs_gemm_desc* d, hipStream_t s) {
   const int64_t la = p.swap ? d->ldb : d->lda, lb = p.swap ? d->lda : d->ldb;
   const int64_t Ma = p.swap ? d->N : d->M, Nb = p.swap ? d->M : d->N;
   const int sm = !bias ? 0 : (p.swap ? 2 : 1);
-#define DW_(BM_, S_, T_) launch_dw_t<BM_, S_, T_>(aa, la, Ma, bb, lb, Nb, d->K, p, part, sums, c, d->ldc, bias, s)
-#define DW_BM(BM_)                                  \
+#define DW_(BM_, BN_, S_, T_) launch_dw_t<BM_, BN_, S_, T_>(aa, la, Ma, bb, lb, Nb, d->K, p, part, sums, c, d->ldc, bias, s)
+#define DW_BM(BM_, BN_)                             \
   do {                                              \
     if (p.swap) {                                   \
-      if (sm == 2) DW_(BM_, 2, true);               \
-      else DW_(BM_, 0, true);                       \
+      if (sm == 2) DW_(BM_, BN_, 2, true);          \
+      else DW_(BM_, BN_, 0, true);                  \
     } else {                                        \
-      if (sm == 1) DW_(BM_, 1, false);              \
-      else DW_(BM_, 0, false);                      \
+      if (sm == 1) DW_(BM_, BN_, 1, false);         \
+      else DW_(BM_, BN_, 0, false);                 \
     }                                               \
   } while (0)
-  if (p.BM == 64) DW_BM(64);
-  else if (p.BM == 128) DW_BM(128);
-  else DW_BM(192);
+#define DW_BN(BM_)                   \
+  do {                               \
+    if (p.BN == 128) DW_BM(BM_, 128); \
+    else DW_BM(BM_, 64);             \
+  } while (0)
+  if (p.BM == 64) DW_BN(64);
+  else if (p.BM == 128) DW_BN(128);
+  else DW_BN(192);
+#undef DW_BN
 #undef DW_BM
 #undef DW_
   VS_LAUNCH_CHECK();
