@@ -214,6 +214,58 @@ def test_gemm_wide_row_slab_path(bkc, shape, epi):
 
 
 @pytest.mark.parametrize("bkc", [True, False])
+@pytest.mark.parametrize("shape", [(8269, 384, 192), (25093, 576, 192), (25088, 768, 192)])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none"])
+def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
+    """K = 192, N a multiple of 192 (qkv, fc1 + GELU, the GELU' product) run on the W-resident kernel
+    (W part in LDS once per workgroup, permuted rows so a lane stores 8 consecutive columns, ragged
+    row ranges / token blocks): fp64 reference on the same bf16 inputs (tolerances as the wide
+    row-slab test), and the same values as the tile kernels (VSPIKE_NO_WRES=1) to bf16 rounding."""
+    from vspike import ops, _lib as L
+    monkeypatch.setenv("VSPIKE_WRES_GBWD", "1")   # the GELU' product too (off by default)
+    M, N, K = shape
+    x = _rand(M, K, seed=41).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=42, scale=0.1).to(torch.bfloat16).to(DEV)
+    bias = _rand(N, seed=43).to(DEV)
+    pre_in = _rand(M, N, seed=44).to(torch.bfloat16).to(DEV)
+    b_dev, ldb = (w, K) if bkc else (w.t().contiguous(), N)
+    kw = dict(M=M, N=N, K=K, a_kcontig=True, b_kcontig=bkc, lda=K, ldb=ldb, ldc=N)
+
+    def run():
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        pre = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+        if epi == "bias":
+            ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS, bias=bias, **kw)
+        elif epi == "none":
+            ops.gemm(x, b_dev, out, **kw)
+        elif epi == "gelu":
+            ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU, bias=bias, aux_out=pre, ld_aux_out=N, **kw)
+        else:
+            ops.gemm(x, b_dev, out, epilogue=L.EPI_GELU_BWD, aux_in=pre_in, ld_aux_in=N, **kw)
+        torch.cuda.synchronize()
+        return out, pre
+
+    out, pre = run()
+    ref = x.double() @ w.double().t()
+    tol = 8e-3
+    if epi in ("bias", "gelu"):
+        ref = ref + bias.double()
+    if epi == "gelu":
+        assert rel(pre.float(), ref) < 8e-3
+        ref = torch.nn.functional.gelu(ref)
+    if epi == "gelu_bwd":
+        xp = pre_in.double().requires_grad_()
+        ref = ref * torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        tol = 1.5e-2
+    assert rel(out.float(), ref) < tol
+    monkeypatch.setenv("VSPIKE_NO_WRES", "1")
+    out2, pre2 = run()
+    assert (out.float() - out2.float()).abs().max() <= 1e-2 * out2.float().abs().max()
+    if epi == "gelu":
+        assert (pre.float() - pre2.float()).abs().max() <= 1e-2 * pre2.float().abs().max()
+
+
+@pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape,epi", [((25088, 3072, 768), "gelu"), ((25088, 768, 3072), "bias_res"),
                                        ((4100, 512, 512), "bias"), ((8192, 2304, 768), "none"),
                                        ((6000, 768, 1536), "gelu_bwd")])

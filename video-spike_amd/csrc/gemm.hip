@@ -1040,6 +1040,180 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
 }
 
 // ----------------------------------------------------------------------------------------------
+// bf16 W-resident kernel for the wide K = 192 products of the ViT block: qkv (N = 576), fc1 + GELU
+// (N = 768, two bf16 outputs) and the GELU' dX product da = (dx' W2) * gelu'(a_pre) (N = 768).
+// Outputs are 3-4x the input, so the bound is the output stream; the per-tile kernels re-read
+// their A tile once per 64-column tile and spend a barrier per tile.  Here:
+//   * the N columns are cut in parts of 192; a workgroup copies its part of W (192 x 192 bf16,
+//     76.8 KB with padded rows) into LDS ONCE and keeps it for its whole row range (2 workgroups
+//     per CU, persistent: grid = 512, workgroup = (row range, part), XCD-grouped so the parts of
+//     a range share an L2);
+//   * no barrier after the fill: each wave walks its own (16-token block, 64-column chunk) units;
+//     the token block's operand rows come straight from HBM as MFMA B fragments (8 consecutive k of
+//     one token per lane: the K-contiguous layout), loaded once per block;
+//   * the product is computed transposed, C^T = W X^T (W rows as the MFMA A operand), with the W
+//     rows permuted in LDS so that a lane's two accumulator quads are 8 CONSECUTIVE output columns
+//     of one token: the epilogue (bias, GELU / GELU', bf16 casts) runs on registers and writes
+//     16-B vectors, no staging.  The GELU' operand of a chunk is loaded before its MFMAs.
+// ----------------------------------------------------------------------------------------------
+constexpr int kWresNH = 192;                  // columns per part
+constexpr int kWresRow = 192 * 2 + 16;        // LDS bytes per W row (K = 192, +16 B: bank spread)
+
+// LDS row of part-local column n: chunk ch = n / 64; within it MFMA tile jj = 2 (r / 32) + (r % 8) / 4
+// and tile row i = 4 ((r % 32) / 8) + r % 4 (r = n % 64), so that accumulator rows 4g..4g+3 of
+// tiles 2p and 2p+1 are the columns 32p + 8g .. 32p + 8g + 7 of the chunk.
+__device__ __forceinline__ int wres_lds_row(int n) {
+  const int ch = n >> 6, r = n & 63, p = r >> 5, q = r & 31;
+  return ch * 64 + (2 * p + ((q >> 2) & 1)) * 16 + 4 * (q >> 3) + (q & 3);
+}
+
+template <bool BKC, uint32_t EF>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                const bf16_t* __restrict__ B, int64_t ldb,
+                                                                EpiParams e) {
+  constexpr int K = 192, KS = K / 32, NCH = kWresNH / 64;
+  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0;
+  __shared__ __attribute__((aligned(16))) char wl[kWresNH * kWresRow];
+  __shared__ __attribute__((aligned(16))) float bl[kWresNH];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int parts = (int)(e.N / kWresNH);
+  const int G = gridDim.x, ranges = G / parts;
+  const int logical = xcd_remap(blockIdx.x, G);
+  const int part = logical % parts, range = logical / parts;
+  if (range >= ranges) return;  // workgroup-uniform (at most parts - 1 idle workgroups)
+  const int64_t r_begin = (int64_t)range * e.M / ranges, r_end = ((int64_t)range + 1) * e.M / ranges;
+  const int64_t n_part = (int64_t)part * kWresNH;
+
+  // ---- W part -> LDS (permuted rows), once: every thread issues all 18 of its 16-B loads before
+  // its first LDS write (a load -> write chain per chunk serialises 18 HBM latencies)
+  constexpr int FILL = kWresNH * K / 8 / 256;  // 16-B chunks per thread
+  static_assert(FILL * 256 * 8 == kWresNH * K, "fill split");
+  uint4 fv[FILL];
+  if constexpr (BKC) {  // W[n][k]: 24 16-B chunks per row
+#pragma unroll
+    for (int i = 0; i < FILL; ++i) {
+      const int c = tid + 256 * i, n = c / (K / 8), kc = c % (K / 8);
+      fv[i] = *(const uint4*)(B + (n_part + n) * ldb + kc * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < FILL; ++i) {
+      const int c = tid + 256 * i, n = c / (K / 8), kc = c % (K / 8);
+      *(uint4*)(wl + wres_lds_row(n) * kWresRow + kc * 16) = fv[i];
+    }
+  } else {  // W[k][n] (N-contiguous): 8 columns per 16-B load, scattered into 8 LDS rows
+#pragma unroll
+    for (int i = 0; i < FILL; ++i) {
+      const int c = tid + 256 * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
+      fv[i] = *(const uint4*)(B + (int64_t)k * ldb + n_part + nc * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < FILL; ++i) {
+      const int c = tid + 256 * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
+      const uint32_t w[4] = {fv[i].x, fv[i].y, fv[i].z, fv[i].w};
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        *(uint16_t*)(wl + wres_lds_row(nc * 8 + t) * kWresRow + k * 2) = (uint16_t)(w[t >> 1] >> (16 * (t & 1)));
+    }
+  }
+  // the part's bias in LDS: the epilogue then issues no global load behind its own stores (on CDNA4
+  // vmcnt counts stores too, so a load after the previous unit's stores would wait for all of them)
+  if constexpr ((EF & VS_EPI_BIAS) != 0) {
+    if (tid < kWresNH) bl[tid] = e.bias[n_part + tid];
+  }
+  __syncthreads();
+
+  // ---- this wave's units: (16-token block, 64-column chunk), chunk-minor; the next block's
+  // operand rows are loaded while this block's chunks run
+  const int64_t rows = r_end - r_begin;
+  const int tb_n = (int)((rows + 15) / 16);
+  const int units = tb_n * NCH;
+  const int u0 = wid * units / 4, u1 = (wid + 1) * units / 4;
+  const int g = lane >> 4, tok = lane & 15;
+  const char* wbase = wl + tok * kWresRow + g * 16;  // + (tile row block) * kWresRow, + ks * 64
+  auto load_x = [&](int tb, bf16x8 (&dst)[KS]) {
+    int64_t m = r_begin + (int64_t)tb * 16 + tok;
+    m = m < r_end ? m : r_end - 1;  // rows past the range: its last row (never stored)
+    const bf16_t* p = A + m * lda + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) dst[ks] = *(const bf16x8*)(p + 32 * ks);
+  };
+  if (u0 >= u1) return;
+  const int tb0 = u0 / NCH, tb1 = (u1 - 1) / NCH;
+  bf16x8 xf[KS], xn[KS];
+  load_x(tb0, xn);
+  for (int tb = tb0; tb <= tb1; ++tb) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) xf[ks] = xn[ks];
+    if (tb < tb1) load_x(tb + 1, xn);
+    const int64_t m = r_begin + (int64_t)tb * 16 + tok;
+    const bool mok = m < r_end;
+    const int c0 = tb == tb0 ? u0 - tb * NCH : 0, c1 = tb == tb1 ? u1 - tb * NCH : NCH;
+    // GELU' operand: chunk c + 1's is loaded before chunk c's stores (a counted wait then skips them)
+    uint4 aux[2][2];
+    auto load_aux = [&](int ch, uint4 (&dst)[2]) {
+      if constexpr (GBWD) {
+        const int64_t n0 = n_part + ch * 64 + 8 * g;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          dst[p] = mok ? *(const uint4*)((const bf16_t*)e.aux_in + m * e.ld_aux_in + n0 + 32 * p) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    auto chunk = [&](int ch, uint4 (&ax)[2], uint4 (&axn)[2]) {
+      if (ch + 1 < c1) load_aux(ch + 1, axn);
+      const int64_t n0 = n_part + ch * 64 + 8 * g;  // this lane's columns: n0 .. n0 + 7 and n0 + 32 ..
+      f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 wf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(wbase + (ch * 64 + j * 16) * kWresRow + ks * 64);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[ks], acc[j], 0, 0, 0);
+      }
+      if (!mok) return;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * p][r] * e.alpha;
+          v[4 + r] = acc[2 * p + 1][r] * e.alpha;
+        }
+        bf16_t* crow = (bf16_t*)e.c + m * e.ldc + n0 + 32 * p;
+        if constexpr (GBWD) {
+          const uint32_t w[4] = {ax[p].x, ax[p].y, ax[p].z, ax[p].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] *= gelu_fast_grad(__uint_as_float(w[q] << 16));
+            v[2 * q + 1] *= gelu_fast_grad(__uint_as_float(w[q] & 0xffff0000u));
+          }
+        } else {
+          if constexpr ((EF & VS_EPI_BIAS) != 0) {
+            const float4 b0 = *(const float4*)&bl[ch * 64 + 32 * p + 8 * g];
+            const float4 b1 = *(const float4*)&bl[ch * 64 + 32 * p + 8 * g + 4];
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+          }
+          if constexpr ((EF & VS_EPI_GELU) != 0) {
+            st8((bf16_t*)e.aux_out + m * e.ld_aux_out + n0 + 32 * p, 0, 1, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = gelu_fast(bf2f(f2bf(v[k])));  // GELU of the stored value
+          }
+        }
+        st8(crow, 0, 1, v);
+      }
+    };
+    load_aux(c0, aux[0]);
+    for (int ch = c0; ch < c1; ch += 2) {
+      chunk(ch, aux[0], aux[1]);
+      if (ch + 1 < c1) chunk(ch + 1, aux[1], aux[0]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
 // bf16 wide row-slab kernel for K <= 192 and N > 192 (the ViT block's qkv, fc1 + GELU and the
 // GELU' dX product: outputs 3-4x the size of the input, so they are bound by their stores).  Same
 // balanced row ownership as the slab kernel (workgroup g owns rows [g M / G, (g+1) M / G), one
@@ -1474,6 +1648,16 @@ static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiPar
 }
 
 template <uint32_t EF>
+static void launch_bf16_wres_ef(const vs_gemm_desc* d, const EpiParams& e, hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_wres_kernel<true, EF>), dim3(512), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_wres_kernel<false, EF>), dim3(512), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
+}
+
+template <uint32_t EF>
 static void launch_bf16_big_ef(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e,
                                hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
@@ -1854,6 +2038,27 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     launch_bf16_big(d, (unsigned)((int64_t)g.tiles_m * g.tiles_n), g, e, s);
     VS_LAUNCH_CHECK();
     return VS_OK;
+  }
+  // W-resident path: K = 192, N a multiple of 192 (>= 384): qkv, fc1 + GELU, the GELU' product
+  {
+    const char* nv = getenv("VSPIKE_NO_WRES");  // A/B knob (read per call: tests toggle it)
+    const bool no_wres = nv && nv[0] && nv[0] != '0';
+    // the GELU' product stays on the wide row-slab kernel unless VSPIKE_WRES_GBWD=1: it measured
+    // 38.1 -> 40.1 us here (VALU-bound on gelu', where the row-slab kernel overlaps it better)
+    const char* gv = getenv("VSPIKE_WRES_GBWD");
+    const bool gbwd = gv && gv[0] && gv[0] != '0';
+    const bool ef_ok = (f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU) || f == 0 || (gbwd && f == VS_EPI_GELU_BWD)) &&
+                       e.op_bf16 && e.out_bf16;
+    if (!no_wres && ef_ok && d->dtype == VS_BF16 && d->a_kcontig && d->K == 192 && d->N % kWresNH == 0 &&
+        d->N >= 2 * kWresNH && d->N <= 64 * kWresNH && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->lda % 8 == 0 &&
+        d->ldb % 8 == 0 && aligned16(d->a) && aligned16(d->b)) {
+      if (f == VS_EPI_BIAS) launch_bf16_wres_ef<(uint32_t)VS_EPI_BIAS>(d, e, s);
+      else if (f == (VS_EPI_BIAS | VS_EPI_GELU)) launch_bf16_wres_ef<(uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, e, s);
+      else if (f == 0) launch_bf16_wres_ef<0u>(d, e, s);
+      else launch_bf16_wres_ef<(uint32_t)VS_EPI_GELU_BWD>(d, e, s);
+      VS_LAUNCH_CHECK();
+      return VS_OK;
+    }
   }
   // wide row-slab path: K <= 192, N > 192 (qkv, fc1 + GELU, the GELU' dX product)
   static const int no_wslab = getenv_flag5("VSPIKE_NO_WSLAB");
