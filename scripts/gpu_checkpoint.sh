@@ -8,7 +8,8 @@ scripts/gpu_steps.sh \
   "tests|700|python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider" \
   "smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
   "bench|300|python bench.py" \
-  "prof|240|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline"
+  "prof|240|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline" \
+  "prof_serial|240|VSPIKE_SIDE=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_serial -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline"
 scripts/pmc_traffic.sh $tag
 ONLY=attn scripts/pmc_attn.sh gpurun_out/pmc_attn
 ONLY=gemm:dW scripts/pmc_attn.sh gpurun_out/pmc_dw

@@ -237,6 +237,13 @@ class VideoMAE(nn.Module):
             setattr(s, k, act[pfx + k].data_ptr())
         return s
 
+    def set_side_stream(self, enabled: bool) -> None:
+        """Run the weight-gradient products on the side stream (default, overlapped with the next
+        products of the backward) or in order on the main stream (VSPIKE_SIDE=0 for the whole
+        process).  bench.py's instrumented pass uses the latter so every launch is timed alone."""
+        self.__dict__["_side"] = bool(enabled)
+        self._caches()[2].clear()
+
     def _caches(self):
         d = self.__dict__
         for k in ("_fwd_cache", "_bwd_cache", "_gs_cache", "_chains", "_lp"):
@@ -469,10 +476,11 @@ class VideoMAE(nn.Module):
                 gs.dy_lp = g["dy_lp"].data_ptr() if lp else None
                 gs.d_o, gs.d_qkv, gs.attn_ws = g["d_o"].data_ptr(), g["d_qkv"].data_ptr(), g["attn_ws"].data_ptr()
                 gs.ln_ws = g["ln_ws"].data_ptr()
-                gs.chain = self._chain(dev).handle if _SIDE else None
+                side = self.__dict__.get("_side", _SIDE)
+                gs.chain = self._chain(dev).handle if side else None
                 gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
                 # opt-in: every block but the last one defers its side-stream join to the next
-                gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER and _SIDE else 0)
+                gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER and side else 0)
                 gs.flags |= L.BWD_FUSE_LN if _LN_FUSE else 0
                 grads[i] = (gs, nxt)
                 cur = nxt
