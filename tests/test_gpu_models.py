@@ -278,6 +278,28 @@ def test_deferred_side_stream_joins_give_identical_grads(mode):
     assert (grads[0] - grads[mode]).norm().item() <= 1e-5 * grads[0].norm().item()
 
 
+def test_side_stream_off_gives_identical_grads():
+    """VideoMAE.set_side_stream(False) (bench.py's instrumented pass: every weight-gradient product
+    in order on the caller's stream) computes the same gradients as the default side stream, on the
+    same model across the switch (the cached per-block structs are rebuilt)."""
+    from vspike import poisson_nll_mean
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    m = _vit_model(cfg, 64, n, dtype="bf16")
+    grads = []
+    for side in (True, False, True):
+        m.set_side_stream(side)
+        m.enc_flat.grad = None
+        m.head_flat.grad = None
+        poisson_nll_mean(m(px), y).backward()
+        torch.cuda.synchronize()
+        grads.append((m.enc_flat.grad.detach().clone(), m.head_flat.grad.detach().clone()))
+    for g in grads[1:]:
+        assert (g[0] - grads[0][0]).norm().item() <= 1e-6 * grads[0][0].norm().item()
+        assert (g[1] - grads[0][1]).norm().item() <= 1e-6 * grads[0][1].norm().item()
+
+
 def test_bf16_shadows_written_by_fused_adamw():
     """FusedAdamW rewrites the bf16 weight shadows in its update pass (vs_adamw param_lp): after
     each step they equal the rounded master weights, and an autograd-visible in-place write to a

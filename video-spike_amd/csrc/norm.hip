@@ -9,6 +9,8 @@
 // per block.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace vs {
@@ -467,7 +469,12 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
   const int lpr = ln_vec_lpr(cols);
   if (lpr && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && (!dres || (lddres % 4 == 0 && aligned16(dres))) &&
       aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(gamma) && (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), kLnBwdBlocks);
+    static const int cap = [] {  // A/B knob: VSPIKE_LN_BLOCKS caps the grid (= partial rows) below 1024
+      const char* v = getenv("VSPIKE_LN_BLOCKS");
+      const int c = v ? atoi(v) : 0;
+      return c > 0 && c <= kLnBwdBlocks ? c : kLnBwdBlocks;
+    }();
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), cap);
     float* part = (float*)workspace;
 #define BV_(L)                                                                                                   \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<L, 3>), dim3(grid), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, \
