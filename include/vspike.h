@@ -66,6 +66,10 @@ int vs_struct_size(int which);
                                  /* splits are summed in a fixed order (no atomics); with RELU  */
                                  /* (skinny path only) C = relu(C + v)                          */
 #define VS_EPI_ACCUM     0x100u  /* C(m,n) += v (plain read-modify-write); C must be f32      */
+#define VS_EPI_GELU_GRAD 0x200u  /* with VS_EPI_GELU: aux_out(m,n) = gelu'(v) instead of v: the  */
+                                 /* factor the backward multiplies by (bf16 ViT path: the fc1    */
+                                 /* forward stores it, the GELU' dX product uses VS_EPI_MUL_AUX)  */
+#define VS_EPI_MUL_AUX   0x400u  /* v *= aux_in(m,n)                                            */
 
 typedef struct vs_gemm_desc {
   int32_t dtype;        /* operand element type, VS_F32 or VS_BF16 */

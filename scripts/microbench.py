@@ -85,6 +85,12 @@ def main():
         rep("bwd da = dx W2 * gelu'", lambda: timeit(lambda: ops.linear_dx(g_lp, w2, ga, epilogue=L.EPI_GELU_BWD, aux_in=pre,
                                                                       ld_aux_in=F), a.reps),
                M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
+        rep("bwd da = dx W2 * g (stored gelu')", lambda: timeit(lambda: ops.linear_dx(g_lp, w2, ga, epilogue=L.EPI_MUL_AUX,
+                                                                               aux_in=pre, ld_aux_in=F), a.reps),
+               M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
+        rep("fwd fc1 +GELU (act+gelu')", lambda: timeit(lambda: ops.linear(x, w1, a_, bias=b1, aux_out=pre, ld_aux_out=F,
+                                                                      epilogue=L.EPI_GELU | L.EPI_GELU_GRAD), a.reps),
+               M * D * e2 + 2 * M * F * e2, 2 * M * D * F)
         rep("bwd dh2 = da W1 (f32)", lambda: timeit(lambda: ops.linear_dx(ga, w1, y32), a.reps),
                M * F * e2 + M * D * 4, 2 * M * D * F)
         rep("bwd do = dy Wp", lambda: timeit(lambda: ops.linear_dx(g_lp, wd, o), a.reps), 2 * M * D * e2, 2 * M * D * D)

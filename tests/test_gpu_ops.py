@@ -215,7 +215,7 @@ def test_gemm_wide_row_slab_path(bkc, shape, epi):
 
 @pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape", [(8269, 384, 192), (25093, 576, 192), (25088, 768, 192)])
-@pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none"])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none", "gelu_grad", "mul_aux"])
 def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
     """K = 192, N a multiple of 192 (qkv, fc1 + GELU, the GELU' product) run on the W-resident kernel
     (W part in LDS once per workgroup, permuted rows so a lane stores 8 consecutive columns, ragged
@@ -240,6 +240,11 @@ def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
             ops.gemm(x, b_dev, out, **kw)
         elif epi == "gelu":
             ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU, bias=bias, aux_out=pre, ld_aux_out=N, **kw)
+        elif epi == "gelu_grad":   # the bf16 ViT fc1: aux_out = gelu'(pre), the backward's factor
+            ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_GRAD, bias=bias, aux_out=pre,
+                     ld_aux_out=N, **kw)
+        elif epi == "mul_aux":     # the bf16 ViT GELU' product: v *= stored gelu'
+            ops.gemm(x, b_dev, out, epilogue=L.EPI_MUL_AUX, aux_in=pre_in, ld_aux_in=N, **kw)
         else:
             ops.gemm(x, b_dev, out, epilogue=L.EPI_GELU_BWD, aux_in=pre_in, ld_aux_in=N, **kw)
         torch.cuda.synchronize()
@@ -248,11 +253,18 @@ def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
     out, pre = run()
     ref = x.double() @ w.double().t()
     tol = 8e-3
-    if epi in ("bias", "gelu"):
+    if epi in ("bias", "gelu", "gelu_grad"):
         ref = ref + bias.double()
     if epi == "gelu":
         assert rel(pre.float(), ref) < 8e-3
         ref = torch.nn.functional.gelu(ref)
+    if epi == "gelu_grad":
+        xp = ref.clone().requires_grad_()
+        gref = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        assert rel(pre.float(), gref) < 8e-3
+        ref = torch.nn.functional.gelu(ref)
+    if epi == "mul_aux":
+        ref = ref * pre_in.double()
     if epi == "gelu_bwd":
         xp = pre_in.double().requires_grad_()
         ref = ref * torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
@@ -261,7 +273,7 @@ def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
     monkeypatch.setenv("VSPIKE_NO_WRES", "1")
     out2, pre2 = run()
     assert (out.float() - out2.float()).abs().max() <= 1e-2 * out2.float().abs().max()
-    if epi == "gelu":
+    if epi in ("gelu", "gelu_grad"):
         assert (pre.float() - pre2.float()).abs().max() <= 1e-2 * pre2.float().abs().max()
 
 

@@ -109,6 +109,13 @@ __device__ __forceinline__ float gelu_fast_grad(float x) {
   const float cdf = phi_fast(x, g);
   return fmaf(x * 0.39894228040143268f, g, cdf);
 }
+// gelu(x) and gelu'(x) from one Phi / exp evaluation (the fc1 forward that stores gelu')
+__device__ __forceinline__ float gelu_fast_both(float x, float& grad) {
+  float g;
+  const float cdf = phi_fast(x, g);
+  grad = fmaf(x * 0.39894228040143268f, g, cdf);
+  return x * cdf;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

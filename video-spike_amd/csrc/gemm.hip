@@ -133,9 +133,16 @@ __device__ __forceinline__ void epi_one(const EpiParams& e, int64_t m, int64_t n
   if (f & VS_EPI_POS) v += e.pos[(m % e.pos_rows) * e.N + n];
   if (f & VS_EPI_GELU_BWD) v *= gelu_erf_grad(ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16));
   if (f & VS_EPI_RELU_BWD) v = ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16) > 0.f ? v : 0.f;
+  if (f & VS_EPI_MUL_AUX) v *= ld_any(e.aux_in, m * e.ld_aux_in + n, e.op_bf16);
   if (f & VS_EPI_GELU) {
-    st_any(e.aux_out, m * e.ld_aux_out + n, v, e.op_bf16);
-    v = gelu_erf(e.op_bf16 ? bf2f(f2bf(v)) : v);  // GELU of the value the backward will see
+    if (f & VS_EPI_GELU_GRAD) {  // store gelu'(x) for the backward, x = the value it would have seen
+      const float x = e.op_bf16 ? bf2f(f2bf(v)) : v;
+      st_any(e.aux_out, m * e.ld_aux_out + n, gelu_erf_grad(x), e.op_bf16);
+      v = gelu_erf(x);
+    } else {
+      st_any(e.aux_out, m * e.ld_aux_out + n, v, e.op_bf16);
+      v = gelu_erf(e.op_bf16 ? bf2f(f2bf(v)) : v);  // GELU of the value the backward will see
+    }
   }
   if (f & VS_EPI_RELU) v = fmaxf(v, 0.f);
   if (f & VS_EPI_RESIDUAL) v += e.residual[m * e.ldr + n];
@@ -168,10 +175,28 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
       for (int k = 0; k < 8; ++k) v[k] = t[k] > 0.f ? v[k] : 0.f;
     }
   }
-  if (f & VS_EPI_GELU) {
-    st8(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, v);
+  if (f & VS_EPI_MUL_AUX) {
+    ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = e.op_bf16 ? gelu_fast(bf2f(f2bf(v[k]))) : gelu_erf(v[k]);
+    for (int k = 0; k < 8; ++k) v[k] *= t[k];
+  }
+  if (f & VS_EPI_GELU) {
+    if (f & VS_EPI_GELU_GRAD) {  // store gelu'(x) for the backward, x = the value it would have seen
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float x = e.op_bf16 ? bf2f(f2bf(v[k])) : v[k];
+        if (e.op_bf16) v[k] = gelu_fast_both(x, t[k]);
+        else {
+          t[k] = gelu_erf_grad(x);
+          v[k] = gelu_erf(x);
+        }
+      }
+      st8(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, t);
+    } else {
+      st8(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = e.op_bf16 ? gelu_fast(bf2f(f2bf(v[k]))) : gelu_erf(v[k]);
+    }
   }
   if (f & VS_EPI_RELU) {
 #pragma unroll
@@ -1072,7 +1097,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ B, int64_t ldb,
                                                                 EpiParams e) {
   constexpr int K = 192, KS = K / 32, NCH = kWresNH / 64;
-  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0;
+  constexpr bool MULA = (EF & VS_EPI_MUL_AUX) != 0;             // v *= aux (the stored gelu')
+  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0 || MULA;    // an aux operand per output
   __shared__ __attribute__((aligned(16))) char wl[kWresNH * kWresRow];
   __shared__ __attribute__((aligned(16))) float bl[kWresNH];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1186,8 +1212,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __
           const uint32_t w[4] = {ax[p].x, ax[p].y, ax[p].z, ax[p].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            v[2 * q] *= gelu_fast_grad(__uint_as_float(w[q] << 16));
-            v[2 * q + 1] *= gelu_fast_grad(__uint_as_float(w[q] & 0xffff0000u));
+            const float lo = __uint_as_float(w[q] << 16), hi = __uint_as_float(w[q] & 0xffff0000u);
+            v[2 * q] *= MULA ? lo : gelu_fast_grad(lo);
+            v[2 * q + 1] *= MULA ? hi : gelu_fast_grad(hi);
           }
         } else {
           if constexpr ((EF & VS_EPI_BIAS) != 0) {
@@ -1196,7 +1223,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __
             v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
             v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
           }
-          if constexpr ((EF & VS_EPI_GELU) != 0) {
+          if constexpr ((EF & VS_EPI_GELU) != 0 && (EF & VS_EPI_GELU_GRAD) != 0) {
+            float gr[8];  // gelu' of the bf16-rounded pre-activation: what the backward multiplies by
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = gelu_fast_both(bf2f(f2bf(v[k])), gr[k]);
+            st8((bf16_t*)e.aux_out + m * e.ld_aux_out + n0 + 32 * p, 0, 1, gr);
+          } else if constexpr ((EF & VS_EPI_GELU) != 0) {
             st8((bf16_t*)e.aux_out + m * e.ld_aux_out + n0 + 32 * p, 0, 1, v);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = gelu_fast(bf2f(f2bf(v[k])));  // GELU of the stored value
@@ -1233,7 +1265,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wslab_kernel(const bf16_t* _
   using OB = OperandBf16<64, BKC>;
   constexpr int KS = 2 * KT;   // 32-deep MFMA k-steps
   constexpr int LDS_T = 68;    // staging row stride (floats)
-  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0;
+  constexpr bool MULA = (EF & VS_EPI_MUL_AUX) != 0;           // v *= aux (the stored gelu')
+  constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0 || MULA;  // an aux operand per output
   __shared__ __attribute__((aligned(16))) char wimg[KT * OB::BYTES];
   __shared__ __attribute__((aligned(16))) float stage[4][16 * LDS_T];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1314,8 +1347,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wslab_kernel(const bf16_t* _
             const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              v[2 * q] *= gelu_fast_grad(__uint_as_float(w[q] << 16));
-              v[2 * q + 1] *= gelu_fast_grad(__uint_as_float(w[q] & 0xffff0000u));
+              const float lo = __uint_as_float(w[q] << 16), hi = __uint_as_float(w[q] & 0xffff0000u);
+              v[2 * q] *= MULA ? lo : gelu_fast_grad(lo);
+              v[2 * q + 1] *= MULA ? hi : gelu_fast_grad(hi);
             }
             st8(e.c, m * e.ldc + n, e.out_bf16, v);
           } else {
@@ -1643,6 +1677,7 @@ static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiPar
     case 0: launch_bf16_wslab_ef<KT, 0u>(d, grid, e, s); break;
     case VS_EPI_BIAS: launch_bf16_wslab_ef<KT, (uint32_t)VS_EPI_BIAS>(d, grid, e, s); break;
     case VS_EPI_BIAS | VS_EPI_GELU: launch_bf16_wslab_ef<KT, (uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, grid, e, s); break;
+    case VS_EPI_MUL_AUX: launch_bf16_wslab_ef<KT, (uint32_t)VS_EPI_MUL_AUX>(d, grid, e, s); break;
     default: launch_bf16_wslab_ef<KT, (uint32_t)VS_EPI_GELU_BWD>(d, grid, e, s); break;
   }
 }
@@ -1676,6 +1711,9 @@ static void launch_bf16_big_ef(const vs_gemm_desc* d, unsigned nblk, const GridM
     case VS_EPI_BIAS | VS_EPI_RESIDUAL: CALL((uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL)); break; \
     case VS_EPI_BIAS | VS_EPI_GELU: CALL((uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)); break;    \
     case VS_EPI_GELU_BWD: CALL((uint32_t)VS_EPI_GELU_BWD); break;                          \
+    case VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD:                                     \
+      CALL((uint32_t)(VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD)); break;               \
+    case VS_EPI_MUL_AUX: CALL((uint32_t)VS_EPI_MUL_AUX); break;                            \
     default: CALL(kEpiRuntime); break;                                                     \
   }
 
@@ -2043,11 +2081,14 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   {
     const char* nv = getenv("VSPIKE_NO_WRES");  // A/B knob (read per call: tests toggle it)
     const bool no_wres = nv && nv[0] && nv[0] != '0';
-    // the GELU' product stays on the wide row-slab kernel unless VSPIKE_WRES_GBWD=1: it measured
-    // 38.1 -> 40.1 us here (VALU-bound on gelu', where the row-slab kernel overlaps it better)
+    // the GELU' product (GELU_BWD, or MUL_AUX on the stored gelu') stays on the wide row-slab kernel
+    // unless VSPIKE_WRES_GBWD=1: 35.7 vs 41.2 us (GELU_BWD), 27.8 vs 32.6 us (MUL_AUX) there — its
+    // operand stream (a 16-B aux read per 8 outputs) overlaps better with the row-slab schedule
     const char* gv = getenv("VSPIKE_WRES_GBWD");
     const bool gbwd = gv && gv[0] && gv[0] != '0';
-    const bool ef_ok = (f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU) || f == 0 || (gbwd && f == VS_EPI_GELU_BWD)) &&
+    const bool ef_ok = (f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU) || f == 0 ||
+                        f == (VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD) ||
+                        (gbwd && (f == VS_EPI_GELU_BWD || f == VS_EPI_MUL_AUX))) &&
                        e.op_bf16 && e.out_bf16;
     if (!no_wres && ef_ok && d->dtype == VS_BF16 && d->a_kcontig && d->K == 192 && d->N % kWresNH == 0 &&
         d->N >= 2 * kWresNH && d->N <= 64 * kWresNH && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->lda % 8 == 0 &&
@@ -2055,6 +2096,9 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       if (f == VS_EPI_BIAS) launch_bf16_wres_ef<(uint32_t)VS_EPI_BIAS>(d, e, s);
       else if (f == (VS_EPI_BIAS | VS_EPI_GELU)) launch_bf16_wres_ef<(uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, e, s);
       else if (f == 0) launch_bf16_wres_ef<0u>(d, e, s);
+      else if (f == (VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD))
+        launch_bf16_wres_ef<(uint32_t)(VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD)>(d, e, s);
+      else if (f == VS_EPI_MUL_AUX) launch_bf16_wres_ef<(uint32_t)VS_EPI_MUL_AUX>(d, e, s);
       else launch_bf16_wres_ef<(uint32_t)VS_EPI_GELU_BWD>(d, e, s);
       VS_LAUNCH_CHECK();
       return VS_OK;
@@ -2069,7 +2113,8 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   static const int all_wslab = getenv_flag5("VSPIKE_WSLAB");
   if (!no_wslab && d->dtype == VS_BF16 && d->a_kcontig && d->N % 64 == 0 && d->N > 192 &&
       (d->K == 64 || d->K == 128 || d->K == 192) && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
-      (f == VS_EPI_GELU_BWD || (all_wslab && (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU))))) {
+      (f == VS_EPI_GELU_BWD || (f == VS_EPI_MUL_AUX && e.op_bf16) ||
+       (all_wslab && (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU))))) {
     static const int gw = getenv("VSPIKE_WSLAB_G") ? atoi(getenv("VSPIKE_WSLAB_G")) : 512;  // A/B knob
     const int64_t G = d->M / 16 < gw ? d->M / 16 : gw;
     if (d->K == 64) launch_bf16_wslab<1>(d, (unsigned)G, e, s);

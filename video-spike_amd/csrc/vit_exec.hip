@@ -95,7 +95,10 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   }
   VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
   {
-    vs_gemm_desc g = gdesc(T, T, true, true, M, F, D, L->h2, D, L->w_fc1, D, L->a_act, F, VS_EPI_BIAS | VS_EPI_GELU);
+    // bf16: a_pre holds gelu'(pre) (VS_EPI_GELU_GRAD), so the backward's GELU' product is a plain
+    // multiply (VS_EPI_MUL_AUX) instead of an erf/exp evaluation per element; f32 keeps pre.
+    const uint32_t epi = VS_EPI_BIAS | VS_EPI_GELU | (T == VS_BF16 ? VS_EPI_GELU_GRAD : 0u);
+    vs_gemm_desc g = gdesc(T, T, true, true, M, F, D, L->h2, D, L->w_fc1, D, L->a_act, F, epi);
     TimerTag tag(VS_TIMER_FWD_FC1);
     g.bias = L->b_fc1;
     g.aux_out = L->a_pre;
@@ -158,7 +161,8 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   }
   VS_CALL(wait_prev(1));  // d_a is read by the previous block's dW1
   {  // d(pre-act) = (dx' W2) * gelu'(pre)
-    vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F, VS_EPI_GELU_BWD);
+    vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F,
+                           lp ? VS_EPI_MUL_AUX : VS_EPI_GELU_BWD);  // bf16: a_pre = gelu'(pre)
     TimerTag tag(VS_TIMER_DX_FC2);
     g.aux_in = L->a_pre;
     g.ld_aux_in = F;

@@ -16,6 +16,7 @@ from .build import LIB_PATH
 VS_F32, VS_BF16, VS_U8 = 0, 1, 2
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
+EPI_GELU_GRAD, EPI_MUL_AUX = 0x200, 0x400
 BWD_DEFER_JOIN = 0x1
 BWD_DEFER_LAST = 0x2
 BWD_FUSE_LN = 0x4
