@@ -116,6 +116,12 @@ int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, 
                      int64_t ldx, const float* mean, const float* rstd, const float* gamma,
                      const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
                      float* dgamma, float* dbeta, void* workspace, void* stream);
+/* The same with a bf16 incoming gradient (dy_dtype VS_BF16, 8-B aligned rows; VS_F32 = the call
+ * above): the bf16 ViT block writes its dX products dh1 / dh2 in bf16 and normalises from them. */
+int vs_layernorm_bwd_dt(int32_t dy_dtype, int64_t rows, int64_t cols, const void* dy, int64_t lddy,
+                        const float* x, int64_t ldx, const float* mean, const float* rstd, const float* gamma,
+                        const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp, float* dgamma,
+                        float* dbeta, void* workspace, void* stream);
 /* The dX product of a Linear fed straight into the backward of the LayerNorm before it (the ViT
  * block's dh2 = da W1 -> LN2' and dh1 = dqkv Wqkv -> LN1', mv:416-417 + mv:373-383 / mv:233-236):
  *   dh = A B (d: the GEMM, epilogue 0, d->c = an [M, N] f32 scratch used only off the fused path);

@@ -491,6 +491,16 @@ def test_layernorm_fwd_bwd(dtype, cols, ws):
     ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx2, dg, db, workspace=ws)
     assert rel(dg, gg) < 1e-5 and rel(db, gb) < 1e-5
     assert rel(dx2, gx) < 1e-5
+    # bf16 incoming gradient (the bf16 ViT block's dh1 / dh2): exact vs fp64 on the same rounded dy
+    dyb = dy.to(torch.bfloat16)
+    yr2 = torch.nn.functional.layer_norm(xr, (cols,), gr, br, 1e-12)
+    gxb, ggb, gbb = torch.autograd.grad(yr2, (xr, gr, br), dyb.double())
+    dx3 = torch.empty(rows, cols, device=DEV)
+    dg.zero_()
+    db.zero_()
+    ops.layernorm_bwd(dyb.to(DEV), x.to(DEV), mean, rstd, g.to(DEV), dx3, dg, db, dres=dres.to(DEV), workspace=ws)
+    assert rel(dx3, gxb + dres.double()) < 1e-5
+    assert rel(dg, ggb) < 1e-5 and rel(db, gbb) < 1e-5
 
 
 # ----------------------------------------------------------------------------------- attention

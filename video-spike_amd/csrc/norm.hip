@@ -15,6 +15,17 @@
 
 namespace vs {
 
+// the backward's incoming gradient dy is f32, or bf16 in the bf16 ViT block (its dX products write
+// dh in the compute dtype: one more bf16 rounding of a gradient, as every other bf16 operand)
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float4 ld4(const bf16_t* p) {
+  const uint2 u = *(const uint2*)p;
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
 template <typename TO, int VPL, int RPW>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ g, const float* __restrict__ b,
@@ -63,8 +74,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-template <int VPL, int RPW>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int64_t lddy,
+template <int VPL, int RPW, typename TD>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, int64_t lddy,
                                                      const float* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const float* __restrict__ g, const float* __restrict__ dres,
@@ -93,7 +104,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
       for (int i = 0; i < VPL; ++i) {
         const int c = lane + 64 * i;
         const bool in = ok && c < cols;
-        d[k][i] = in ? dy[row * lddy + c] : 0.f;
+        d[k][i] = in ? ld1(dy + row * lddy + c) : 0.f;
         xv[k][i] = in ? x[row * ldx + c] : 0.f;
       }
     }
@@ -212,8 +223,8 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict
   }
 }
 
-template <int LPR, int VEC>
-__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict__ dy, int64_t lddy,
+template <int LPR, int VEC, typename TD>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const TD* __restrict__ dy, int64_t lddy,
                                                          const float* __restrict__ x, int64_t ldx,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, const float* __restrict__ g,
@@ -243,7 +254,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const int c = 4 * (gl + LPR * j);
-      dd[j] = *(const float4*)(dy + rw * lddy + c);
+      dd[j] = ld4(dy + rw * lddy + c);
       xx[j] = *(const float4*)(x + rw * ldx + c);
       rr[j] = dres ? *(const float4*)(dres + rw * lddres + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -377,15 +388,15 @@ static void launch_fwd(int64_t rows, int64_t cols, const float* x, int64_t ldx, 
                      rstd, rows, (int)cols);
 }
 
-template <int VPL>
-static void launch_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+template <int VPL, typename TD>
+static void launch_bwd(int64_t rows, int64_t cols, const TD* dy, int64_t lddy, const float* x, int64_t ldx,
                        const float* mean, const float* rstd, const float* gamma, const float* dres, int64_t lddres,
                        float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta, hipStream_t s) {
   constexpr int RPW = VPL <= 4 ? 4 : (VPL <= 8 ? 2 : 1);
   int64_t nb = cdiv(rows, 4 * RPW * 2);  // ~2 row-groups per wave: amortises the column reduction
   if (nb > 2048) nb = 2048;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL((ln_bwd_kernel<VPL, RPW>), dim3((unsigned)nb), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd,
+  hipLaunchKernelGGL((ln_bwd_kernel<VPL, RPW, TD>), dim3((unsigned)nb), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd,
                      gamma, dres, lddres, dx, lddx, (bf16_t*)dx_lp, dgamma, dbeta, rows, (int)cols);
 }
 
@@ -454,21 +465,20 @@ extern "C" size_t vs_layernorm_bwd_workspace_bytes(int64_t rows, int64_t cols) {
   return (size_t)kLnBwdBlocks * 2 * (size_t)(cols > 0 ? cols : 0) * sizeof(float);
 }
 
-extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, const float* x, int64_t ldx,
-                                const float* mean, const float* rstd, const float* gamma, const float* dres,
-                                int64_t lddres, float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta,
-                                void* workspace, void* stream) {
-  VS_REQUIRE(dy && x && mean && rstd && gamma && dx && dgamma && dbeta, "vs_layernorm_bwd: null pointer");
-  VS_REQUIRE(cols > 0 && cols <= 1024, "vs_layernorm_bwd: cols must be in [1, 1024]");
-  if (rows == 0) return VS_OK;
-  hipStream_t s = (hipStream_t)stream;
+template <typename TD>
+static int layernorm_bwd_t(int64_t rows, int64_t cols, const TD* dy, int64_t lddy, const float* x, int64_t ldx,
+                           const float* mean, const float* rstd, const float* gamma, const float* dres, int64_t lddres,
+                           float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta, void* workspace,
+                           hipStream_t s) {
+  constexpr bool BF = sizeof(TD) == 2;
   // algorithmic bytes: dy, x, (dres) read, dx (+ its bf16 copy) written, row stats, gamma, dgamma/dbeta
   ScopedTimer timer(VS_TIMER_LN_BWD, s,
-                    (double)rows * (double)cols * (12.0 + (dres ? 4.0 : 0.0) + (dx_lp ? 2.0 : 0.0)) +
+                    (double)rows * (double)cols * ((BF ? 2.0 : 4.0) + 8.0 + (dres ? 4.0 : 0.0) + (dx_lp ? 2.0 : 0.0)) +
                         (double)rows * 8.0 + (double)cols * 20.0);
   const int lpr = ln_vec_lpr(cols);
   if (lpr && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && (!dres || (lddres % 4 == 0 && aligned16(dres))) &&
-      aligned16(dy) && aligned16(x) && aligned16(dx) && aligned16(gamma) && (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {
+      (((uintptr_t)dy) & (BF ? 7 : 15)) == 0 && aligned16(x) && aligned16(dx) && aligned16(gamma) &&
+      (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {
     static const int cap = [] {  // A/B knob: VSPIKE_LN_BLOCKS caps the grid (= partial rows) below 1024
       const char* v = getenv("VSPIKE_LN_BLOCKS");
       const int c = v ? atoi(v) : 0;
@@ -476,8 +486,8 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
     }();
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), cap);
     float* part = (float*)workspace;
-#define BV_(L)                                                                                                   \
-  hipLaunchKernelGGL((ln_bwd_vec_kernel<L, 3>), dim3(grid), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, \
+#define BV_(L)                                                                                                       \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<L, 3, TD>), dim3(grid), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, \
                      dres, lddres, dx, lddx, (bf16_t*)dx_lp, dgamma, dbeta, part, rows)
     if (lpr == 16) BV_(16); else if (lpr == 32) BV_(32); else BV_(64);
 #undef BV_
@@ -487,10 +497,34 @@ extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
-#define B_(V) launch_bwd<V>(rows, cols, dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp, dgamma, \
-                            dbeta, s)
+#define B_(V) launch_bwd<V, TD>(rows, cols, dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp, dgamma, \
+                                dbeta, s)
   VS_LN_DISPATCH(B_);
 #undef B_
   VS_LAUNCH_CHECK();
   return VS_OK;
+}
+
+extern "C" int vs_layernorm_bwd(int64_t rows, int64_t cols, const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                                const float* mean, const float* rstd, const float* gamma, const float* dres,
+                                int64_t lddres, float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta,
+                                void* workspace, void* stream) {
+  return vs_layernorm_bwd_dt(VS_F32, rows, cols, dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp,
+                             dgamma, dbeta, workspace, stream);
+}
+
+extern "C" int vs_layernorm_bwd_dt(int32_t dy_dtype, int64_t rows, int64_t cols, const void* dy, int64_t lddy,
+                                   const float* x, int64_t ldx, const float* mean, const float* rstd,
+                                   const float* gamma, const float* dres, int64_t lddres, float* dx, int64_t lddx,
+                                   void* dx_lp, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  VS_REQUIRE(dy && x && mean && rstd && gamma && dx && dgamma && dbeta, "vs_layernorm_bwd: null pointer");
+  VS_REQUIRE(cols > 0 && cols <= 1024, "vs_layernorm_bwd: cols must be in [1, 1024]");
+  VS_REQUIRE(dy_dtype == VS_F32 || dy_dtype == VS_BF16, "vs_layernorm_bwd: dy must be f32 or bf16");
+  if (rows == 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dy_dtype == VS_BF16)
+    return layernorm_bwd_t(rows, cols, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx,
+                           dx_lp, dgamma, dbeta, workspace, s);
+  return layernorm_bwd_t(rows, cols, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp,
+                         dgamma, dbeta, workspace, s);
 }

@@ -8,9 +8,19 @@
 //   x' = y + a W2^T + b2 [f32]
 // Backward mirrors it with the weight gradients accumulated in f32 (split-K atomics for the
 // token-reduction dW products, whose K is B*N = 25,088 rows at the bench shape).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace vs {
+
+static bool dh_f32() {
+  static const bool v = [] {
+    const char* e = getenv("VSPIKE_DH_F32");
+    return e && e[0] && e[0] != '0';
+  }();
+  return v;
+}
 
 static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t M, int64_t N, int64_t K, const void* a,
                           int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, uint32_t epi) {
@@ -181,15 +191,18 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   // dh2 = da W1;  dy = dx' + LN2'(dh2)  (VS_BWD_FUSE_LN: one launch, dh2 stays on the chip)
   VS_CALL(wait_prev(2));  // dy / dy_lp are read by the previous block's dWp
   {
-    vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
+    // bf16: dh2 in bf16 (half the bytes written here and read by LN2'), as every other bf16 operand
+    // (VSPIKE_DH_F32=1 keeps it f32, for A/B)
+    const int hdt = (G->flags & VS_BWD_FUSE_LN) || dh_f32() ? VS_F32 : T;
+    vs_gemm_desc g = gdesc(T, hdt, true, false, M, D, F, G->d_a, F, L->w_fc1, D, G->d_h, D, 0);
     TimerTag tag(VS_TIMER_DX_FC1);
     if (G->flags & VS_BWD_FUSE_LN) {
       VS_CALL(vs_gemm_ln_bwd(&g, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
                              lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
     } else {
       VS_CALL(vs_gemm(&g, stream));
-      VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy, D,
-                               lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
+      VS_CALL(vs_layernorm_bwd_dt(hdt, M, D, G->d_h, D, L->y, D, L->mean2, L->rstd2, L->ln2_g, G->dx_out, D, G->dy,
+                                  D, lp ? G->dy_lp : nullptr, G->ln2_g, G->ln2_b, G->ln_ws, stream));
     }
   }
   // ---- attention: y = x + o Wp^T + bp
@@ -227,15 +240,16 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   // dh1 = dqkv Wqkv;  dx = dy + LN1'(dh1)  (one launch, as above)
   VS_CALL(wait_prev(0));  // dx_in is the previous block's dx_out, read by its dW2
   {
-    vs_gemm_desc g = gdesc(T, VS_F32, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
+    const int hdt = (G->flags & VS_BWD_FUSE_LN) || dh_f32() ? VS_F32 : T;  // bf16 dh1, as dh2 above
+    vs_gemm_desc g = gdesc(T, hdt, true, false, M, D, 3 * D, G->d_qkv, 3 * D, L->w_qkv, D, G->d_h, D, 0);
     TimerTag tag(VS_TIMER_DX_QKV);
     if (G->flags & VS_BWD_FUSE_LN) {
       VS_CALL(vs_gemm_ln_bwd(&g, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
                              lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
     } else {
       VS_CALL(vs_gemm(&g, stream));
-      VS_CALL(vs_layernorm_bwd(M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D, G->dx_in, D,
-                               lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
+      VS_CALL(vs_layernorm_bwd_dt(hdt, M, D, G->d_h, D, L->x_in, D, L->mean1, L->rstd1, L->ln1_g, G->dy, D,
+                                  G->dx_in, D, lp ? G->dx_in_lp : nullptr, G->ln1_g, G->ln1_b, G->ln_ws, stream));
     }
   }
   if (!ch) return VS_OK;

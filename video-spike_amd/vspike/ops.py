@@ -96,7 +96,7 @@ def layernorm_bwd_workspace_bytes(rows, cols):
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=None, workspace=None):
-    """LayerNorm backward; dgamma/dbeta accumulate.  `workspace` (f32, >= layernorm_bwd_workspace_bytes)
+    """LayerNorm backward (dy f32 or bf16); dgamma/dbeta accumulate.  `workspace` (f32, >= layernorm_bwd_workspace_bytes)
     is allocated here when not given; pass False to use the per-block atomic reduction instead."""
     require_device(dy, x, dx)
     rows, cols = x.shape
@@ -104,10 +104,10 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dgamma, dbeta, dres=None, dx_lp=
         workspace = torch.empty(layernorm_bwd_workspace_bytes(rows, cols) // 4 + 4, dtype=torch.float32,
                                 device=x.device)
     ws = None if workspace is False else workspace
-    check(lib().vs_layernorm_bwd(rows, cols, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
-                                 rstd.data_ptr(), gamma.data_ptr(), ptr(dres), dres.stride(0) if dres is not None else 0,
-                                 dx.data_ptr(), dx.stride(0), ptr(dx_lp), dgamma.data_ptr(), dbeta.data_ptr(),
-                                 ptr(ws), stream()), "vs_layernorm_bwd")
+    check(lib().vs_layernorm_bwd_dt(L.dtype_code(dy.dtype), rows, cols, dy.data_ptr(), dy.stride(0), x.data_ptr(),
+                                    x.stride(0), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), ptr(dres),
+                                    dres.stride(0) if dres is not None else 0, dx.data_ptr(), dx.stride(0), ptr(dx_lp),
+                                    dgamma.data_ptr(), dbeta.data_ptr(), ptr(ws), stream()), "vs_layernorm_bwd")
     return dx
 
 
