@@ -421,9 +421,11 @@ def test_kernel_timers_per_product():
 def test_fused_ln_backward_and_serial_schedule_match_default(side):
     """The opt-in schedules of the block backward (VS_BWD_FUSE_LN: dX product + LayerNorm' in one
     launch; VSPIKE_SIDE=0: no side stream) compute the same gradients as the default.  Geometry with
-    M = B x 1568 = 9,408 token rows, so the fused row-slab path (M >= 8192) runs.  Bar: 2e-5 of each
-    flat gradient's norm (the fused LN' sums a row in 16-lane groups, the unfused kernel too, but the
-    dgamma/dbeta partial rows are grouped differently)."""
+    M = B x 1568 = 9,408 token rows, so the fused row-slab path (M >= 8192) runs.  Bars: the serial
+    schedule 2e-5 of each flat gradient's norm (same products, dgamma/dbeta partial rows grouped
+    the same way); the fused LN' keeps dh in f32 on the chip while the default writes the bf16
+    dh1 / dh2 the bf16 block uses everywhere else, so 3e-3 (one bf16 rounding of a gradient;
+    measured 8.6e-4)."""
     import vspike.vit as V
     from vspike import poisson_nll_mean
     cfg = cpu_ref.ViTCfg(image_size=224, num_frames=16, hidden_size=192, num_hidden_layers=2,
@@ -433,8 +435,11 @@ def test_fused_ln_backward_and_serial_schedule_match_default(side):
     y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
     grads = {}
     old = (V._LN_FUSE, V._SIDE)
+    runs = {"default": (False, True), "fused": (True, side)}
+    if not side:
+        runs["serial"] = (False, False)
     try:
-        for key, (fuse, sd) in {"default": (False, True), "variant": (True, side)}.items():
+        for key, (fuse, sd) in runs.items():
             V._LN_FUSE, V._SIDE = fuse, sd
             m = _vit_model(cfg, 64, n, dtype="bf16")
             poisson_nll_mean(m(px), y).backward()
@@ -442,5 +447,8 @@ def test_fused_ln_backward_and_serial_schedule_match_default(side):
             grads[key] = (m.enc_flat.grad.detach().double().cpu(), m.head_flat.grad.detach().double().cpu())
     finally:
         V._LN_FUSE, V._SIDE = old
-    for a, b in zip(grads["default"], grads["variant"]):
-        assert (a - b).norm().item() <= 2e-5 * a.norm().item()
+    for a, b in zip(grads["default"], grads["fused"]):
+        assert (a - b).norm().item() <= 3e-3 * a.norm().item()
+    if not side:
+        for a, b in zip(grads["default"], grads["serial"]):
+            assert (a - b).norm().item() <= 2e-5 * a.norm().item()
