@@ -130,6 +130,13 @@ int vs_layernorm_bwd_dt(int32_t dy_dtype, int64_t rows, int64_t cols, const void
  *   vs_layernorm_bwd_workspace_bytes).
  * bf16 with N in {64, 128, 192} and M >= 8192 runs fused (dh never leaves the chip); otherwise it is
  * vs_gemm into d->c followed by vs_layernorm_bwd. */
+/* y = A W^T (+ bias) + residual (d: bf16 operands, out f32 = y, epilogue RESIDUAL [| BIAS]) and
+ * h = LayerNorm(y; gamma, beta, eps) in bf16 with its row mean / rstd, in ONE launch when the
+ * shape allows (the ViT block's proj product + LN2, N = 192: the row-slab kernel owns whole rows),
+ * else vs_gemm + vs_layernorm_fwd.  Replaces modeling_videomae.py:434-437 (attention output +
+ * residual, layernorm_after). */
+int vs_gemm_ln_fwd(const vs_gemm_desc* d, const float* gamma, const float* beta, float eps, void* h, int64_t ldh,
+                   float* mean, float* rstd, void* stream);
 int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const float* mean, const float* rstd,
                    const float* gamma, const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
                    float* dgamma, float* dbeta, void* workspace, void* stream);

@@ -326,6 +326,39 @@ def test_gemm_big_tile_path(bkc, shape, epi):
     assert rel(out.float(), ref) < tol
 
 
+@pytest.mark.parametrize("shape", [(25088, 192, 192), (9409, 192, 192), (25088, 192, 768)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_gemm_ln_fwd_fused(shape, bias):
+    """vs_gemm_ln_fwd: y = x W^T (+ b) + residual and h = LayerNorm(y) in one row-slab launch (the
+    ViT block's proj product + layernorm_after) — bitwise the two-launch result (same epilogue order,
+    same 16-lane row layout and reduction order as ln_fwd_vec_kernel), and close to fp64."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    x = _rand(M, K, seed=51).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=52, scale=0.1).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=53).to(DEV) if bias else None
+    res = _rand(M, N, seed=54).to(DEV)
+    g = (1 + 0.1 * _rand(N, seed=55)).to(DEV)
+    be = (0.1 * _rand(N, seed=56)).to(DEV)
+    y = torch.empty(M, N, device=DEV)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.linear_ln_fwd(x, w, y, res, g, be, 1e-12, h, mean, rstd, bias=b)
+    y2 = torch.empty_like(y)
+    epi = L.EPI_RESIDUAL | (L.EPI_BIAS if bias else 0)
+    ops.gemm(x, w, y2, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=K, ldb=K, ldc=N, epilogue=epi, bias=b,
+             residual=res, ld_residual=N)
+    h2 = torch.empty_like(h)
+    m2, r2 = torch.empty_like(mean), torch.empty_like(rstd)
+    ops.layernorm_fwd(y2, g, be, 1e-12, h2, m2, r2)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2) and torch.equal(h, h2) and torch.equal(mean, m2) and torch.equal(rstd, r2)
+    ref = x.double() @ w.double().t() + res.double() + (b.double() if bias else 0)
+    assert rel(y, ref) < 1e-5
+    href = torch.nn.functional.layer_norm(ref, (N,), g.double(), be.double(), 1e-12)
+    assert rel(h.float(), href) < 8e-3
+
+
 @pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 576), (12345, 128, 64), (40000, 64, 128),
                                    (300, 192, 256)])
 @pytest.mark.parametrize("dres,lp", [(True, True), (False, False)])

@@ -854,9 +854,17 @@ struct LnBwdParams {
   int64_t lddx;
   bf16_t* dx_lp;       // optional bf16 copy of dx (next GEMM operand)
   float* part;         // [gridDim.x][2][N] dgamma / dbeta partial rows (ln_partsum adds them)
+  // LayerNorm FORWARD fused into the epilogue (vs_gemm_ln_fwd): y = v + bias + residual is stored
+  // (e.c, f32) and normalised: h = (y - mean) rstd gamma + beta (bf16), mean / rstd per row
+  const float* beta;
+  float eps;
+  bf16_t* h;
+  int64_t ldh;
+  float* mean_out;
+  float* rstd_out;
 };
 
-template <int NT, bool BKC, uint32_t EF, bool LNB = false>
+template <int NT, bool BKC, uint32_t EF, bool LNB = false, bool LNF = false>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                 const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
                                                                 EpiParams e, LnBwdParams ln) {
@@ -1010,6 +1018,77 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
               u.y = (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16);
               *(uint2*)(ln.dx_lp + m * ln.lddx + c) = u;
             }
+          }
+        }
+      }
+      continue;
+    }
+    if constexpr (LNF) {
+      // y = (v + bias) + residual (epi_eight's order), stored f32; then ln_fwd_vec_kernel's LayerNorm
+      // on the row held by 16 lanes (same lane layout and reduction order: bitwise the unfused result)
+      constexpr float inv = 1.f / (float)N;
+      float4 rv[4][NT];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {  // every residual load of the 4 passes issued first
+        int64_t m = m0 + p * 16 + rsub;
+        m = m < m_end ? m : m_end - 1;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) rv[p][j] = *(const float4*)(e.residual + m * e.ldr + 4 * (gl + 16 * j));
+      }
+      float4 bia[NT], gam[NT], bet[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int c = 4 * (gl + 16 * j);
+        bia[j] = (EF & VS_EPI_BIAS) ? *(const float4*)(e.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        gam[j] = *(const float4*)(ln.gamma + c);
+        bet[j] = *(const float4*)(ln.beta + c);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int rr = p * 16 + rsub;
+        const int64_t m = m0 + rr;
+        const bool valid = m < m_end;
+        float4 v[NT];
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int c = 4 * (gl + 16 * j);
+          v[j] = *(const float4*)(stg + rr * LDT + c);
+          if constexpr ((EF & VS_EPI_BIAS) != 0) {
+            v[j].x += bia[j].x; v[j].y += bia[j].y; v[j].z += bia[j].z; v[j].w += bia[j].w;
+          }
+          v[j].x += rv[p][j].x; v[j].y += rv[p][j].y; v[j].z += rv[p][j].z; v[j].w += rv[p][j].w;
+          if (valid) *(float4*)((float*)e.c + m * e.ldc + c) = v[j];
+          sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+        const float mu = sm * inv;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          v[j].x -= mu; v[j].y -= mu; v[j].z -= mu; v[j].w -= mu;
+          q += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        const float rs = rsqrtf(q * inv + ln.eps);
+        if (valid) {
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            float4 o;
+            o.x = v[j].x * rs * gam[j].x + bet[j].x;
+            o.y = v[j].y * rs * gam[j].y + bet[j].y;
+            o.z = v[j].z * rs * gam[j].z + bet[j].z;
+            o.w = v[j].w * rs * gam[j].w + bet[j].w;
+            uint2 u;
+            u.x = (uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16);
+            u.y = (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16);
+            *(uint2*)(ln.h + m * ln.ldh + 4 * (gl + 16 * j)) = u;
+          }
+          if (gl == 0) {
+            ln.mean_out[m] = mu;
+            ln.rstd_out[m] = rs;
           }
         }
       }
@@ -1641,17 +1720,17 @@ static void launch_bf16_panel_ef(const vs_gemm_desc* d, unsigned grid, int64_t i
     hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, false, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
 }
 
-template <int NT, uint32_t EF, bool LNB = false>
+template <int NT, uint32_t EF, bool LNB = false, bool LNF = false>
 static void launch_bf16_slab_ef(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s,
                                 const LnBwdParams& ln = LnBwdParams{}) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
   if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, true, EF, LNB>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb,
-                       d->K, e, ln);
+    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, true, EF, LNB, LNF>), dim3(grid), dim3(256), 0, s, a, d->lda, b,
+                       d->ldb, d->K, e, ln);
   else
-    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, false, EF, LNB>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb,
-                       d->K, e, ln);
+    hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, false, EF, LNB, LNF>), dim3(grid), dim3(256), 0, s, a, d->lda, b,
+                       d->ldb, d->K, e, ln);
 }
 template <int NT>
 static void launch_bf16_slab(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s) {
@@ -2205,6 +2284,44 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, vec ? 64 : 256)), dim3(256), 0, s, e.part, g.splits,
                        d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_gemm_ln_fwd(const vs_gemm_desc* d, const float* gamma, const float* beta, float eps, void* h,
+                              int64_t ldh, float* mean, float* rstd, void* stream) {
+  using namespace vs;
+  VS_REQUIRE(d && gamma && beta && h && mean && rstd, "vs_gemm_ln_fwd: null pointer");
+  VS_REQUIRE((d->epilogue & ~(uint32_t)VS_EPI_BIAS) == VS_EPI_RESIDUAL && d->out_dtype == VS_F32 && d->split_k <= 1 &&
+                 !d->a_rowsum,
+             "vs_gemm_ln_fwd: the product is y = x W^T (+ bias) + residual, f32 out");
+  if (d->M == 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t M = d->M, N = d->N;
+  static const int no_fuse = getenv_flag5("VSPIKE_NO_LNF_FUSE");
+  const bool fused = !no_fuse && d->dtype == VS_BF16 && d->a_kcontig && N == 192 && d->K % 64 == 0 && d->K >= 64 &&
+                     M >= 8192 && aligned16(d->a) && aligned16(d->b) && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
+                     d->lda >= d->K && (d->b_kcontig ? d->ldb >= d->K : d->ldb >= N) && aligned16(d->c) &&
+                     d->ldc % 4 == 0 && aligned16(d->residual) && d->ld_residual % 4 == 0 &&
+                     (!(d->epilogue & VS_EPI_BIAS) || aligned16(d->bias)) && aligned16(gamma) && aligned16(beta) &&
+                     (((uintptr_t)h) & 7) == 0 && ldh % 4 == 0;
+  if (!fused) {  // the same two GPU launches, unfused
+    VS_CALL(vs_gemm(d, stream));
+    return vs_layernorm_fwd(VS_BF16, M, N, (const float*)d->c, d->ldc, gamma, beta, eps, h, ldh, mean, rstd, stream);
+  }
+  const double ea = esize(d->dtype);
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
+                    (double)(M + N) * (double)d->K * ea + (double)M * (double)N * (4.0 + 4.0 + 2.0) +
+                        (double)M * 8.0 + (double)N * 12.0);
+  EpiParams e = {};
+  e.M = M; e.N = N; e.alpha = d->alpha; e.vec_ok = 1;
+  e.c = d->c; e.ldc = d->ldc; e.out_bf16 = 0; e.flags = d->epilogue;
+  e.bias = d->bias; e.residual = d->residual; e.ldr = d->ld_residual;
+  LnBwdParams ln = {};
+  ln.gamma = gamma; ln.beta = beta; ln.eps = eps; ln.h = (bf16_t*)h; ln.ldh = ldh; ln.mean_out = mean; ln.rstd_out = rstd;
+  const int64_t G = M / 16 < 512 ? M / 16 : 512;
+  if (d->epilogue & VS_EPI_BIAS) launch_bf16_slab_ef<3, (uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL), false, true>(d, (unsigned)G, e, s, ln);
+  else launch_bf16_slab_ef<3, (uint32_t)VS_EPI_RESIDUAL, false, true>(d, (unsigned)G, e, s, ln);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

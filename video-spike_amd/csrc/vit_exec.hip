@@ -101,9 +101,14 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     TimerTag tag(VS_TIMER_FWD_PROJ);
     g.residual = L->x_in;
     g.ld_residual = D;
-    VS_CALL(vs_gemm(&g, stream));
+    if (T == VS_BF16) {  // y and LN2(y) in one launch (the row-slab kernel owns whole rows of y)
+      VS_CALL(vs_gemm_ln_fwd(&g, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
+    } else {
+      VS_CALL(vs_gemm(&g, stream));
+    }
   }
-  VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
+  if (T != VS_BF16)
+    VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
   {
     // bf16: a_pre holds gelu'(pre) (VS_EPI_GELU_GRAD), so the backward's GELU' product is a plain
     // multiply (VS_EPI_MUL_AUX) instead of an erf/exp evaluation per element; f32 keeps pre.

@@ -83,6 +83,7 @@ PROTOTYPES = {
                                         c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_layernorm_bwd_dt": (ctypes.c_int, [ctypes.c_int32, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
                                         c_i64, c_p, c_p, c_p, c_p, c_p]),
+    "vs_gemm_ln_fwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_p, ctypes.c_float, c_p, c_i64, c_p, c_p, c_p]),
     "vs_gemm_ln_bwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
                                       c_p, c_p, c_p, c_p, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),

@@ -137,6 +137,27 @@ def linear_dx_ln_bwd(dy, w, x, mean, rstd, gamma, dx, dgamma, dbeta, *, dres=Non
     return dx
 
 
+def linear_ln_fwd(x, w, y, residual, gamma, beta, eps, h, mean, rstd, *, bias=None):
+    """y = x @ w^T (+ bias) + residual (f32) and h = LayerNorm(y) (bf16) with its row mean / rstd
+    (vs_gemm_ln_fwd): the ViT block's attention-output product fused with layernorm_after."""
+    require_device(x, w, y, residual, h)
+    M, K = x.shape
+    N = w.shape[0]
+    d = L.GemmDesc()
+    d.dtype = L.dtype_code(x.dtype)
+    d.out_dtype = L.dtype_code(torch.float32)
+    d.a_kcontig, d.b_kcontig = 1, 1
+    d.M, d.N, d.K = M, N, K
+    d.a, d.lda, d.b, d.ldb, d.c, d.ldc = x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), y.stride(0)
+    d.alpha = 1.0
+    d.epilogue = L.EPI_RESIDUAL | (L.EPI_BIAS if bias is not None else 0)
+    d.bias = ptr(bias)
+    d.residual, d.ld_residual = residual.data_ptr(), residual.stride(0)
+    check(lib().vs_gemm_ln_fwd(ctypes.byref(d), gamma.data_ptr(), beta.data_ptr(), float(eps), h.data_ptr(),
+                               h.stride(0), mean.data_ptr(), rstd.data_ptr(), stream()), "vs_gemm_ln_fwd")
+    return h
+
+
 def attn_fwd(qkv, o, lse, B, N, H, scale=0.125):
     require_device(qkv, o, lse)
     check(lib().vs_attn_fwd(L.dtype_code(qkv.dtype), B, N, H, 64, qkv.data_ptr(), qkv.stride(0), o.data_ptr(),
