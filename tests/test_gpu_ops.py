@@ -326,6 +326,24 @@ def test_gemm_big_tile_path(bkc, shape, epi):
     assert rel(out.float(), ref) < tol
 
 
+@pytest.mark.parametrize("M", [25088, 9000])
+def test_patch_embed_gemm_pos_on_row_slab(M):
+    """The patch embedding x0 = cols W^T + b + sinusoid[token] (K = 1536, N = 192, pos rows = 1568)
+    on the row-slab kernel: fp64 reference, and the row -> table-row mapping m % pos_rows."""
+    from vspike import ops, _lib as L
+    N, K, P = 192, 1536, 1568
+    x = _rand(M, K, seed=61).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=62, scale=0.05).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=63).to(DEV)
+    pos = _rand(P, N, seed=64).to(DEV)
+    out = torch.empty(M, N, device=DEV)
+    ops.linear(x, w, out, bias=b, epilogue=L.EPI_POS, pos=pos, pos_rows=P)
+    torch.cuda.synchronize()
+    rows = torch.arange(M, device=DEV) % P
+    ref = x.double() @ w.double().t() + b.double() + pos.double()[rows]
+    assert rel(out, ref) < 1e-5
+
+
 @pytest.mark.parametrize("shape", [(25088, 192, 192), (9409, 192, 192), (25088, 192, 768)])
 @pytest.mark.parametrize("bias", [True, False])
 def test_gemm_ln_fwd_fused(shape, bias):

@@ -1737,6 +1737,9 @@ static void launch_bf16_slab(const vs_gemm_desc* d, unsigned grid, const EpiPara
   switch (e.flags) {
     case 0: launch_bf16_slab_ef<NT, 0u>(d, grid, e, s); break;
     case VS_EPI_BIAS: launch_bf16_slab_ef<NT, (uint32_t)VS_EPI_BIAS>(d, grid, e, s); break;
+    case VS_EPI_BIAS | VS_EPI_POS:  // the patch embedding + sinusoid table (K = 1536)
+      launch_bf16_slab_ef<NT, (uint32_t)(VS_EPI_BIAS | VS_EPI_POS)>(d, grid, e, s);
+      break;
     default: launch_bf16_slab_ef<NT, (uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL)>(d, grid, e, s); break;
   }
 }
@@ -2134,7 +2137,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   static const int no_slab = getenv_flag5("VSPIKE_NO_SLAB");
   if (!no_slab && d->dtype == VS_BF16 && d->a_kcontig && (d->N == 64 || d->N == 128 || d->N == 192) &&
       d->K % 64 == 0 && d->K >= 64 && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
-      (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_RESIDUAL))) {
+      (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_RESIDUAL) || f == (VS_EPI_BIAS | VS_EPI_POS))) {
     const int64_t G = d->M / 16 < 512 ? d->M / 16 : 512;
     if (d->N == 64) launch_bf16_slab<1>(d, (unsigned)G, e, s);
     else if (d->N == 128) launch_bf16_slab<2>(d, (unsigned)G, e, s);
