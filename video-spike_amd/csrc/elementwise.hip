@@ -7,49 +7,44 @@
 namespace vs {
 
 // ---------------------------------------------------------------------------------------------
-// im2col for the tubelet Conv3d (mv:176-181, 194-195).  One thread writes 8 consecutive columns
-// (8 consecutive j of one (c, t, i) row of a patch): two 16-B f32 reads of one image row, one 16-B
-// (bf16) / two 16-B (f32) stores.  32-bit index math (a row of 8-column groups is < 2^31 threads:
-// checked on the host); the previous version's eight 64-bit div/mods and element-wise 2-B stores
-// ran at 1.9 TB/s (59 us for the C2 batch).
+// im2col for the tubelet Conv3d (mv:176-181, 194-195), walked over the INPUT: a workgroup is 8 image
+// rows x 32 lanes; lane w8 < W / 8 reads 8 consecutive pixels (32 B) of its row — a row's lanes read
+// the whole 896-B row — and writes them as 8 consecutive columns (one 16-B bf16 / two 16-B f32
+// stores) of their token's row: col = ((c t + tt) p + i) p + j.  (b, f) come from blockIdx.x and
+// (c, h) from blockIdx.y and the lane's row, so the per-thread index math is a few shifts at the
+// ViT geometry (T = 2, P = 16 compile-time).  57 us for the C2 batch (115 MB) against 59-60 us for
+// the output-walking grid-stride versions: not index- or pattern-bound.
 // ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ px, T* __restrict__ out, int total8,
-                                                     int F, int C, int H, int W, int t, int p) {
-  const int Fp = F / t, Hp = H / p, Wp = W / p, p8 = p / 8;
-  const int ncol8 = C * t * p * p8;
-  for (int g = blockIdx.x * 256 + threadIdx.x; g < total8; g += gridDim.x * 256) {
-    const int row = g / ncol8, col8 = g - row * ncol8;
-    // col = ((c*t + tt)*p + i)*p + j, j = 8 * j8
-    const int j8 = col8 % p8;
-    int r = col8 / p8;
-    const int i = r % p;
-    r /= p;
-    const int tt = r % t, c = r / t;
-    // row = ((b*Fp + f')*Hp + hp)*Wp + wp
-    int q = row;
-    const int wp = q % Wp;
-    q /= Wp;
-    const int hp = q % Hp;
-    q /= Hp;
-    const int fp = q % Fp, b = q / Fp;
-    const int f = fp * t + tt;
-    const float* src = px + ((((int64_t)b * F + f) * C + c) * H + (hp * p + i)) * (int64_t)W + wp * p + 8 * j8;
-    const float4 a = *(const float4*)src;
-    const float4 bb = *(const float4*)(src + 4);
-    const float v[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
-    T* dst = out + (int64_t)g * 8;
-    if constexpr (sizeof(T) == 2) {
-      uint4 u;
-      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-      u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-      *(uint4*)dst = u;
-    } else {
-      *(float4*)dst = a;
-      *(float4*)(dst + 4) = bb;
-    }
+template <typename T, int TT, int PP>
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ px, T* __restrict__ out, int F, int C,
+                                                     int H, int W, int t_rt, int p_rt) {
+  const int t = TT > 0 ? TT : t_rt, p = PP > 0 ? PP : p_rt;
+  const int w8 = threadIdx.x & 31, rsub = threadIdx.x >> 5;
+  const int hc = blockIdx.y * 8 + rsub;  // c * H + h
+  if (w8 * 8 >= W || hc >= C * H) return;
+  const int bf = blockIdx.x;             // b * F + f (workgroup-uniform)
+  const int b = bf / F, f = bf - b * F;
+  const int c = hc / H, h = hc - c * H;
+  const int Fp = F / t, Hp = H / p, Wp = W / p;
+  const int ncol = C * t * p * p;
+  const int w0 = 8 * w8;
+  const float* src = px + (((int64_t)bf * C + c) * H + h) * W + w0;
+  const float4 a = *(const float4*)src;
+  const float4 bb = *(const float4*)(src + 4);
+  const int fp = f / t, tt = f - fp * t, hp = h / p, i = h - hp * p, wp = w0 / p, j = w0 - wp * p;
+  const int64_t row = (((int64_t)b * Fp + fp) * Hp + hp) * Wp + wp;
+  const int col = ((c * t + tt) * p + i) * p + j;
+  T* dst = out + row * ncol + col;
+  if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16);
+    u.y = (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16);
+    u.z = (uint32_t)f2bf(bb.x) | ((uint32_t)f2bf(bb.y) << 16);
+    u.w = (uint32_t)f2bf(bb.z) | ((uint32_t)f2bf(bb.w) << 16);
+    *(uint4*)dst = u;
+  } else {
+    *(float4*)dst = a;
+    *(float4*)(dst + 4) = bb;
   }
 }
 
@@ -241,13 +236,18 @@ extern "C" int vs_patch_im2col(int32_t out_dtype, int64_t B, int64_t F, int64_t 
   ScopedTimer timer(VS_TIMER_MISC, s, (double)total8 * 8.0 * (4.0 + (double)esize(out_dtype)));
   VS_REQUIRE(total8 < (1ll << 31) - 256 * 4096 && B * F * C * H * W < (1ll << 40), "vs_patch_im2col: batch too large");
   VS_REQUIRE((((uintptr_t)cols) & 15) == 0, "vs_patch_im2col: cols must be 16-byte aligned");
-  const unsigned g = grid_for(total8);
-  if (out_dtype == VS_BF16)
-    hipLaunchKernelGGL(im2col_kernel<bf16_t>, dim3(g), dim3(256), 0, s, pixels, (bf16_t*)cols, (int)total8, (int)F,
-                       (int)C, (int)H, (int)W, (int)tubelet, (int)patch);
-  else
-    hipLaunchKernelGGL(im2col_kernel<float>, dim3(g), dim3(256), 0, s, pixels, (float*)cols, (int)total8, (int)F,
-                       (int)C, (int)H, (int)W, (int)tubelet, (int)patch);
+  VS_REQUIRE(W <= 256 && W % 8 == 0, "vs_patch_im2col: image width must be <= 256 and a multiple of 8");
+  const dim3 grid((unsigned)(B * F), (unsigned)cdiv(C * H, 8));
+  const bool vit = tubelet == 2 && patch == 16;  // the VideoMAE tubelet: compile-time index math
+#define IM2COL_(TY, TT, PP)                                                                                           \
+  hipLaunchKernelGGL((im2col_kernel<TY, TT, PP>), grid, dim3(256), 0, s, pixels, (TY*)cols, (int)F, (int)C, (int)H,   \
+                     (int)W, (int)tubelet, (int)patch)
+  if (out_dtype == VS_BF16) {
+    if (vit) IM2COL_(bf16_t, 2, 16); else IM2COL_(bf16_t, 0, 0);
+  } else {
+    if (vit) IM2COL_(float, 2, 16); else IM2COL_(float, 0, 0);
+  }
+#undef IM2COL_
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
