@@ -49,7 +49,13 @@ TRAFFIC_CLASSES = ("attn_fwd", "attn_bwd", "ln_fwd", "ln_bwd", "adamw")
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU).  Without WORLD_SIZE in the environment, N > 1 starts N "
+                         "child ranks under torch.distributed.run before this process touches the GPU")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend of the gradient exchange (nccl = RCCL on ROCm; gloo lets "
+                         "several ranks share one GPU, for tests)")
+    ap.add_argument("--loss", default="poisson", choices=["poisson", "mse"], help="training.loss")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--profile-steps", type=int, default=10, help="instrumented steps after the timed region")
@@ -123,6 +129,57 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
     return out, loss4
 
 
+def _reference_grads(model):
+    """Gradients of the plugin under the reference's parameter names (numpy, f32)."""
+    from vspike.layout import modern_name
+    out = {}
+    for name, which, slot, rows in model.layout.hf_items():
+        flat = model.enc_flat.grad if which == "enc" else model.head_flat.grad
+        if flat is None:
+            continue
+        t = (model.layout.enc if which == "enc" else model.layout.head).view(flat, slot)
+        out[modern_name(name)] = (t if rows is None else t[rows]).detach().float().cpu().numpy()
+    return out
+
+
+# bf16 bars of the full-batch check: 2x the worst values measured at the bench geometry
+# (tests/test_gpu_parity_bench.py holds the same numbers for the B=16 fixture)
+PARITY_TOL = {"fp32": {"log_rates": 1e-4, "loss": 1e-5, "grad": 1e-3},
+              "bf16": {"log_rates": 1e-2, "loss": 1e-3, "grad": 4e-2}}
+
+
+def full_batch_parity(ccfg, params, pixels, target, gpu, args):
+    """The benched step's fwd+bwd (whole batch, initial weights) vs the CPU fp32 oracle on the same
+    clips: log-rates (max abs error / max |ref|), loss (relative) and every gradient (norm-relative)."""
+    import numpy as np
+    from oracle import cpu_ref
+    t0 = time.perf_counter()
+    P = cpu_ref.to_torch(params)
+    ref = cpu_ref.videomae_plugin_forward(pixels, P, ccfg, False)
+    loss_fn = cpu_ref.poisson_nll_mean if args.loss == "poisson" else (lambda x, y: ((x - y) ** 2).mean())
+    loss = loss_fn(ref, target)
+    loss.backward()
+    secs = time.perf_counter() - t0
+    ref_out = ref.detach().numpy()
+    e_out = float(np.abs(gpu["log_rates"].numpy() - ref_out).max() / max(np.abs(ref_out).max(), 1e-30))
+    e_loss = abs(gpu["loss"] - float(loss)) / abs(float(loss))
+    errs = {}
+    for k, g in gpu["grads"].items():
+        r = P[k].grad
+        if r is None:
+            continue
+        r = r.detach().numpy().reshape(g.shape)
+        errs[k] = float(np.linalg.norm((g - r).ravel()) / max(np.linalg.norm(r.ravel()), 1e-30))
+    worst = max(errs, key=errs.get) if errs else None
+    tol = PARITY_TOL[args.dtype]
+    ok = e_out < tol["log_rates"] and e_loss < tol["loss"] and (not errs or errs[worst] < tol["grad"])
+    return {"what": f"one fwd+bwd of the whole benched batch ({pixels.shape[0]} clips, the timed step's dispatch) at "
+                    "the initial weights: HIP path vs the CPU fp32 oracle (oracle/cpu_ref.py)",
+            "log_rates_maxrel": round(e_out, 7), "loss_rel": round(e_loss, 8), "n_grads": len(errs),
+            "worst_grad": worst, "worst_grad_rel": round(errs[worst], 6) if worst else None,
+            "tolerance": tol, "ok": bool(ok), "cpu_seconds": round(secs, 1)}
+
+
 def _traffic_lookup(kind, launches_per_step):
     """HBM bytes per timed call of a kernel class from the newest committed PMC summary
     (scripts/pmc_traffic.sh: separate FETCH_SIZE / WRITE_SIZE passes, FETCH doubled per the gfx950
@@ -161,18 +218,54 @@ def _pmc_lookup(kind):
     return None
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` started without a launcher: run N ranks of this script under
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous) as CHILD processes and return
+    their exit code.  Called before anything initialises the GPU in this process (no re-exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.call(cmd, env=env)
+
+
+def _param_digest(model, dev):
+    """Per-rank fingerprint of the trainable state after the steps (f64 sums of every flat buffer
+    and of its squares): replicas that stayed in sync agree exactly."""
+    vals = []
+    for p in model.parameters():
+        d = p.detach().double()
+        vals += [d.sum(), (d * d).sum()]
+    return torch.stack(vals).to(dev)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if world > ndev and args.backend == "nccl":
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPU(s): RCCL needs one GPU per rank "
+                         "(--backend gloo shares a device)")
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
-    from vspike import VideoMAE, load_run_config, ops, poisson_nll_mean
+    from vspike import VideoMAE, load_run_config, make_criterion, ops
     from vspike import _lib as L
     from vspike.dp import GradExchange
     from vspike.trainer import build_optimizer, Trainer
@@ -185,6 +278,8 @@ def main():
     config["model"]["freeze_encoder"] = bool(args.freeze)
     if args.lr is not None:
         config["optimizer"]["lr"] = args.lr
+    config["training"]["loss"] = args.loss
+    criterion = make_criterion(config)
     torch.manual_seed(1234)                      # identical replicas (GradExchange also broadcasts)
     model = VideoMAE(config["model"]).to(dev)
     bb = model.backbone
@@ -195,14 +290,22 @@ def main():
     target = torch.poisson(lam, generator=g)
     do_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     parity = None
-    if do_cpu:   # initial weights and the HIP loss on the first 4 clips, for the in-run parity check
+    L.dispatch_reset()
+    if do_cpu:
+        # in-run parity of the BENCHED dispatch: one fwd+bwd of the whole batch (M = B * tokens rows,
+        # the same kernels the timed step runs) at the initial weights, against the CPU oracle below
         init_params = {k: v.detach().cpu().numpy() for k, v in model.reference_state_dict(modern_names=True).items()}
-        with torch.no_grad():
-            gpu_loss4 = float(poisson_nll_mean(model(pixels[:4]), target[:4]))
+        out0 = model(pixels)
+        loss0 = criterion(out0, target)
+        loss0.backward()
+        gpu_par = {"loss": float(loss0), "log_rates": out0.detach().float().cpu(),
+                   "grads": _reference_grads(model)}
+        model.zero_grad(set_to_none=True)
+        del out0, loss0
     total = args.warmup + args.steps + args.profile_steps + (1 if args.profile_steps > 0 else 0)  # + the pass's re-warm step
     opt, sched = build_optimizer(model, config, total_steps=total, world=world)
     exchange = GradExchange(model) if world > 1 else None
-    trainer = Trainer(model, opt, sched, criterion=poisson_nll_mean, exchange=exchange)
+    trainer = Trainer(model, opt, sched, criterion=criterion, exchange=exchange)
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -213,6 +316,7 @@ def main():
     for _ in range(args.warmup):
         trainer.step(pixels, target)
     barrier_sync()
+    L.dispatch_reset()
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
@@ -224,6 +328,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(losses[-1].item())
+    dispatch = {k: round(v / args.steps, 2) for k, v in L.dispatch_counts().items() if v}
+    replicas_equal = None
+    if world > 1:   # every rank ends with the same weights (the exchange kept the replicas in sync)
+        hi = _param_digest(model, dev)
+        lo = -hi
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)       # max and min over ranks agree iff all equal
+        dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+        replicas_equal = bool(torch.equal(hi, -lo))
 
     # ---- instrumented pass (not part of `value`): every kernel class timed on its own stream
     kern = {}
@@ -293,11 +405,8 @@ def main():
                                                              "tubelet_size", "hidden_size", "num_hidden_layers",
                                                              "num_attention_heads", "intermediate_size",
                                                              "layer_norm_eps")})
-        cpu, cpu_loss4 = cpu_baseline(ccfg, init_params, pixels[:4].cpu(), target[:4].cpu(), args.cpu_seconds)
-        parity = {"what": "PoissonNLL of the first 4 clips at the initial weights: HIP path vs CPU fp32 oracle",
-                  "hip": round(gpu_loss4, 7), "cpu_fp32": round(cpu_loss4, 7),
-                  "rel": round(abs(gpu_loss4 - cpu_loss4) / abs(cpu_loss4), 7),
-                  "tolerance": 1e-4 if args.dtype == "fp32" else 2e-3}
+        cpu, _ = cpu_baseline(ccfg, init_params, pixels[:4].cpu(), target[:4].cpu(), args.cpu_seconds)
+        parity = full_batch_parity(ccfg, init_params, pixels.cpu(), target.cpu(), gpu_par, args)
 
     if rank == 0:
         workload = ("C3 ViT-Base/16" if bb.hidden_size == 768 else "C2 ViT-Tiny/16" if bb.hidden_size == 192
@@ -315,7 +424,8 @@ def main():
             "mfma_util_pct": round(100.0 * step_tflops / peak_mfma, 2),
             "model_tflops": round(step_tflops, 2),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
-            "lr": float(config["optimizer"]["lr"]),
+            "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
+            "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

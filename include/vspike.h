@@ -34,6 +34,10 @@ extern "C" {
 #define VS_U8 2   /* raw video frames only (vs_video_preprocess) */
 
 int vs_version(void);                 /* ABI version (monotonic) */
+/* sha256 prefix (16 hex digits) of the sources this library was compiled from: every csrc/ file
+ * and this header, hashed by vspike/build.py (source_hash) and baked into the build, so a test or
+ * bench can prove which sources the loaded binary was built from */
+const char* vs_build_id(void);
 const char* vs_last_error(void);      /* static string, last VS_EINVAL reason */
 int vs_device_arch(char* buf, int n); /* writes gcnArchName of the current device */
 /* sizeof() of the ABI structs, so bindings can verify their mirrors: 0 = vs_gemm_desc,
@@ -202,6 +206,15 @@ int vs_poisson_nll(int64_t n, const float* log_rate, const float* target, float*
 /* dx = g[0] * (exp(x) - y) / n with the upstream scalar gradient read from device memory */
 int vs_poisson_nll_bwd(int64_t n, const float* log_rate, const float* target,
                        const float* grad_out, float* dx, void* stream);
+/* The MSE regression head option (train config `loss: mse`; BASELINE north_star "Poisson/MSE
+ * spike-count regression head"), torch.nn.MSELoss(reduction="mean") semantics:
+ *   loss = mean((x - y)^2);  dx = grad_scale * 2 (x - y) / n.
+ * The reference trains with PoissonNLL only (src/train.py:59) and computes mse as an eval metric
+ * (src/utils/utils.py:169-171); same workspace size and determinism as vs_poisson_nll. */
+int vs_mse_loss(int64_t n, const float* pred, const float* target, float* loss_out, float* dx,
+                float grad_scale, void* workspace, void* stream);
+int vs_mse_loss_bwd(int64_t n, const float* pred, const float* target, const float* grad_out, float* dx,
+                    void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused AdamW step (torch.optim.AdamW semantics, src/train.py:44-49) over a flat f32 buffer.
@@ -355,6 +368,68 @@ const char* vs_shard_last_error(void);
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
 int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */
+
+/* ------------------------------------------------------------------------------------------
+ * Dispatch counters: every launch of a kernel path adds one to its counter (host-side, relaxed
+ * atomics), so a test can assert WHICH kernels an oracle-pinned run reached (e.g. that the
+ * benched B=16 step runs the row-slab / W-resident / fused-LN / dW-tile paths).
+ * ------------------------------------------------------------------------------------------ */
+#define VS_PATH_GEMM_DW       0   /* gemm_dw_kernel: token-reduction weight gradients */
+#define VS_PATH_GEMM_SKINNY   1   /* skinny split-K (head) */
+#define VS_PATH_GEMM_SLAB     2   /* gemm_bf16_slab: N <= 192 row slabs */
+#define VS_PATH_GEMM_BIG      3   /* gemm_bf16_big: 256 x 128 tiles */
+#define VS_PATH_GEMM_WRES     4   /* gemm_bf16_wres: W-resident K = 192 */
+#define VS_PATH_GEMM_WSLAB    5   /* gemm_bf16_wslab: wide row slabs */
+#define VS_PATH_GEMM_PANEL    6
+#define VS_PATH_GEMM_FULLK    7
+#define VS_PATH_GEMM_RING     8
+#define VS_PATH_GEMM_TILE     9   /* generic register-staged tiles */
+#define VS_PATH_GEMM_F32     10   /* exact-f32 MFMA kernel */
+#define VS_PATH_GEMM_LN_FWD  11   /* vs_gemm_ln_fwd fused (slab + LayerNorm) */
+#define VS_PATH_GEMM_LN_BWD  12   /* vs_gemm_ln_bwd fused (slab + LayerNorm') */
+#define VS_PATH_ATTN_FWD     13   /* bf16 flash forward */
+#define VS_PATH_ATTN_BWD     14   /* bf16 flash backward (row prep + dK/dV + dQ) */
+#define VS_PATH_ATTN_F32     15   /* exact-f32 attention, forward or backward */
+#define VS_PATH_PATCH_FUSED  16   /* patch embedding GEMM with the tubelet gather in its A-load */
+#define VS_PATH_DW_GROUPED   17   /* grouped dW launch (several weight gradients in one launch) */
+#define VS_PATH_COUNT        24
+/* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
+int vs_dispatch_counts(int64_t* out, int n);
+int vs_dispatch_reset(void);
+
+/* ------------------------------------------------------------------------------------------
+ * A/B and test knobs.  Each is read ONCE from the environment (VSPIKE_<NAME>, an integer; unset =
+ * the default, which is the benchmarked dispatch) on first use, and can then be overridden by
+ * vs_knob_set (tests select a path this way).  No entry point calls getenv on its launch path.
+ * ------------------------------------------------------------------------------------------ */
+#define VS_KNOB_DW_OLD       0   /* 1: dW products on the generic split-K tiles */
+#define VS_KNOB_NO_SKINNY    1
+#define VS_KNOB_NO_SLAB      2
+#define VS_KNOB_NO_BIG       3
+#define VS_KNOB_NO_WRES      4
+#define VS_KNOB_WRES_GBWD    5   /* 1: the GELU' dX product on the W-resident kernel */
+#define VS_KNOB_NO_WSLAB     6
+#define VS_KNOB_WSLAB        7   /* 1: every eligible K <= 192 product on the wide row slabs */
+#define VS_KNOB_WSLAB_G      8   /* wide row-slab grid cap (default 512) */
+#define VS_KNOB_PANEL        9
+#define VS_KNOB_NO_PANEL    10
+#define VS_KNOB_PANEL_GRID  11   /* default 512 */
+#define VS_KNOB_NO_FULLK    12
+#define VS_KNOB_NO_RING     13
+#define VS_KNOB_NO_LNF_FUSE 14
+#define VS_KNOB_NO_LN_FUSE  15
+#define VS_KNOB_DW_BM       16   /* force the dW tile / split / stage choice (0 = planned) */
+#define VS_KNOB_DW_BN       17
+#define VS_KNOB_DW_SPLITS   18
+#define VS_KNOB_DW_STAGES   19
+#define VS_KNOB_LN_BLOCKS   20   /* LayerNorm' grid cap (0 = default 1024) */
+#define VS_KNOB_DH_F32      21   /* 1: the ViT block's dh1 / dh2 stay f32 in bf16 mode */
+#define VS_KNOB_NO_PATCH_FUSED 22 /* 1: im2col + GEMM instead of the fused patch embedding */
+#define VS_KNOB_NO_DW_GROUP 23   /* 1: one launch per weight gradient instead of the grouped dW launch */
+#define VS_KNOB_ATTN_VARIANT 24  /* attention kernel variant (0 = default) */
+#define VS_KNOB_COUNT       32
+int vs_knob_get(int knob);               /* VS_EINVAL for an unknown id */
+int vs_knob_set(int knob, int value);    /* returns the previous value; VS_EINVAL for an unknown id */
 
 #ifdef __cplusplus
 }

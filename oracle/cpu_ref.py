@@ -253,17 +253,26 @@ def to_torch(params: Dict[str, np.ndarray], requires_grad=True) -> Dict[str, tor
     return {k: torch.tensor(v, dtype=torch.float32, requires_grad=requires_grad) for k, v in params.items()}
 
 
+def mse_mean(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """`torch.nn.MSELoss()` (mean reduction): the north_star's MSE head option.  The reference
+    itself trains with PoissonNLL only (src/train.py:59) and computes mse as an eval metric
+    (src/utils/utils.py:169-171)."""
+    return ((pred - target) ** 2).mean()
+
+
 def train_curve(forward, params: Dict[str, torch.Tensor], batches, lr=5e-5, wd=0.01, eps=1e-8,
-                warmup_pct=0.15, div_factor=10.0, trainable=None) -> List[float]:
+                warmup_pct=0.15, div_factor=10.0, trainable=None, criterion=None) -> List[float]:
     """`src/train.py:44-57` (AdamW + OneCycleLR, total_steps = len(batches)) and the loop body of
-    `src/trainer/base.py:144-159`.  Returns the per-step training loss."""
+    `src/trainer/base.py:144-159`.  Returns the per-step training loss.  criterion: default the
+    reference's PoissonNLL mean (src/train.py:59)."""
+    criterion = criterion or poisson_nll_mean
     names = list(params) if trainable is None else [n for n in params if trainable(n)]
     opt = torch.optim.AdamW([params[n] for n in names], lr=lr, weight_decay=wd, eps=eps)
     sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=len(batches), max_lr=lr,
                                                 pct_start=warmup_pct, div_factor=div_factor)
     losses = []
     for x, y in batches:
-        loss = poisson_nll_mean(forward(x, params), y)
+        loss = criterion(forward(x, params), y)
         loss.backward()
         opt.step()
         sched.step()

@@ -243,6 +243,59 @@ def gen_vit_tiny12():
     print("vit_tiny12", fx["loss"], fx["curve_train"])
 
 
+def gen_vit_tiny12_b16():
+    """The bench's EXACT dispatch (BASELINE C2 at the bench batch: ViT-Tiny/16, 12 layers, B=16 ->
+    M = 25,088 token rows, n=128, trainable encoder): forward, every gradient (summarised) and a
+    3-step train curve (AdamW wd 0.01 + OneCycleLR, lr 1e-6 as gen_vit_tiny12).  At M >= 8192 the
+    HIP path runs its row-slab, W-resident, fused GEMM+LayerNorm and dW-tile kernels, which the
+    B=2 fixture (M = 3,136) never reaches."""
+    cfg = cpu_ref.VIT_TINY
+    B, enc_out, n = 16, 64, 128
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=16))
+    y = torch.from_numpy(prng.spike_targets(16, (B, 100, n)))
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(_grads_summary_small({k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}))
+    del out, loss
+    _load_vit(m, cfg, enc_out, n)
+    for k, p in m.named_parameters():
+        p.grad = None
+        p.requires_grad = ".key.bias" not in k
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=600 + s)),
+                torch.from_numpy(prng.spike_targets(650 + s, (B, 100, n)))) for s in range(3)]
+    fx["curve_train"] = _ref_train_loop(m, batches, [p for p in m.parameters() if p.requires_grad], lr=1e-6)
+    np.savez_compressed(os.path.join(OUT, "vit_tiny12_b16.npz"), **fx)
+    print("vit_tiny12_b16", fx["loss"], fx["curve_train"])
+
+
+def gen_vit_base32f():
+    """BASELINE C5's encoder geometry (videomae-base width, 32 frames -> 3,136 tokens = 24 * 128 + 64,
+    n = 1024) with one layer, B=1, trainable: forward and every gradient.  C5's temporal transformer
+    and fp8 have no reference code; the encoder is the reference plugin's at
+    num_frames=32."""
+    cfg = cpu_ref.ViTCfg(num_frames=32, num_hidden_layers=1)
+    B, enc_out, n = 1, 64, 1024
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=32))
+    y = torch.from_numpy(prng.spike_targets(32, (B, 100, n)))
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(_grads_summary_small({k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}))
+    np.savez_compressed(os.path.join(OUT, "vit_base32f.npz"), **fx)
+    print("vit_base32f", fx["loss"])
+
+
 def gen_vit_base1l():
     """The reference plugin's real width (videomae-base: d768, 12 heads, videomae.py:7-8; C3's
     n=512) with one layer, full 1568 tokens, B=1: trainable forward+backward, and a 3-step curve in
@@ -366,7 +419,7 @@ def gen_metrics():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "vit_tiny12", "vit_base1l", "k0",
-                             "metrics"]
+    which = sys.argv[1:] or ["configs", "linear", "vit_small", "vit_tiny1l", "vit_tiny12", "vit_tiny12_b16",
+                             "vit_base1l", "vit_base32f", "k0", "metrics"]
     for w in which:
         globals()["gen_" + w]()

@@ -25,3 +25,17 @@ def golden():
         with np.load(os.path.join(GOLDEN, name)) as f:      # allow_pickle=False (default)
             return {k: f[k] for k in f.files}
     return load
+
+
+@pytest.fixture
+def knobs():
+    """Set libvspike A/B knobs (vspike.h VS_KNOB_*, read once from the environment at load) for one
+    test: `knobs("no_wres", 1)`; every knob is restored afterwards."""
+    from vspike import _lib as L
+    saved = []
+
+    def set_(name, value):
+        saved.append((name, L.knob_set(name, value)))
+    yield set_
+    for name, prev in reversed(saved):
+        L.knob_set(name, prev)

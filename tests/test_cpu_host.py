@@ -40,8 +40,40 @@ def test_library_exports_every_header_symbol(built_lib):
 def test_abi_struct_mirrors_and_version(built_lib):
     from vspike import _lib
     lib = _lib.lib()                       # verifies struct sizes against the C side
-    assert lib.vs_version() >= 1
+    assert lib.vs_version() >= 4
     assert lib.vs_struct_size(99) == -1
+
+
+def test_build_id_matches_sources(built_lib):
+    """vs_build_id() is the hash of the sources the loaded library was compiled from."""
+    from vspike import _lib, build
+    assert _lib.build_id() == build.source_hash()
+
+
+def test_knobs_and_dispatch_counters_without_gpu(built_lib):
+    """Knob overrides round-trip (read once from the environment, no getenv on launch paths);
+    dispatch counters read and reset; unknown ids are rejected."""
+    from vspike import _lib
+    lib = _lib.lib()
+    assert len(_lib.KNOB_NAMES) <= _lib.KNOB_COUNT and len(_lib.PATH_NAMES) <= _lib.PATH_COUNT
+    prev = _lib.knob_set("wslab_g", 256)
+    assert _lib.knob_get("wslab_g") == 256
+    with _lib.knob("wslab_g", 128):
+        assert _lib.knob_get("wslab_g") == 128
+    assert _lib.knob_get("wslab_g") == 256
+    _lib.knob_set("wslab_g", prev)
+    assert lib.vs_knob_get(999) == -1 and lib.vs_knob_set(-1, 0) == -1
+    _lib.dispatch_reset()
+    assert set(_lib.dispatch_counts().values()) == {0}
+
+
+def test_mse_criterion_selection():
+    from vspike import make_criterion, mse_mean, poisson_nll_mean
+    assert make_criterion(None) is poisson_nll_mean
+    assert make_criterion({"training": {"loss": "mse"}}) is mse_mean
+    assert make_criterion({"training": {}}) is poisson_nll_mean
+    with pytest.raises(ValueError):
+        make_criterion({"training": {"loss": "huber"}})
 
 
 def test_gpu_only_entry_points_reject_bad_args_without_launching(built_lib):

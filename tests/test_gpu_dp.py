@@ -13,8 +13,11 @@
 Two ranks share cuda:0 (RCCL refuses two ranks on one device, so these use gloo; the RCCL path is
 the same code with backend "nccl", exercised by bench.py --gpus N).
 """
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -84,16 +87,27 @@ def _worker(rank, world, port, mode, layers, dtype, out):
     else:
         from torch.nn.parallel import DistributedDataParallel as DDP
         net = DDP(m, device_ids=[0])
-        ex = attach_ddp(net, bucket_mb=0.25) if mode == "ddp_attach" else None
+        ex = attach_ddp(net, bucket_mb=0.25) if mode.startswith("ddp_attach") else None
     for step in range(2):                           # DDP rebuilds its buckets after the first step
         px, y = _batch(cfg, step=step)
         m.zero_grad(set_to_none=True)
-        loss = poisson_nll_mean(net(px[rank * per:(rank + 1) * per].to(DEV)), y[rank * per:(rank + 1) * per].to(DEV))
+        xs, ys = px[rank * per:(rank + 1) * per].to(DEV), y[rank * per:(rank + 1) * per].to(DEV)
+        if mode == "ddp_attach_accum":
+            # gradient accumulation: one clip per micro-batch, the first under no_sync (local only)
+            for j in range(per):
+                if j < per - 1:
+                    with net.no_sync():
+                        poisson_nll_mean(net(xs[j:j + 1]), ys[j:j + 1]).backward()
+                else:
+                    poisson_nll_mean(net(xs[j:j + 1]), ys[j:j + 1]).backward()
+            continue
+        loss = poisson_nll_mean(net(xs), ys)
         loss.backward()
         if mode == "exchange":
             ex.finish()
     torch.cuda.synchronize()
-    scale = 1.0 / world if mode == "exchange" else 1.0           # DDP averages; the exchange sums
+    # DDP averages over ranks; the exchange sums; accumulation sums `per` one-clip mean losses
+    scale = 1.0 / world if mode == "exchange" else (1.0 / per if mode == "ddp_attach_accum" else 1.0)
     out[rank] = (m.enc_flat.grad.detach().cpu() * scale, m.head_flat.grad.detach().cpu() * scale)
     dist.destroy_process_group()
 
@@ -116,6 +130,7 @@ def _single_process_grads(layers, dtype):
     ("ddp", 4, "bf16", 1e-4),
     ("ddp_attach", 2, "fp32", 1e-5),
     ("ddp_attach", 4, "bf16", 1e-4),
+    ("ddp_attach_accum", 2, "fp32", 1e-5),   # DDP no_sync micro-steps + attach_ddp
 ])
 def test_two_ranks_equal_single_process_batch(mode, layers, dtype, tol):
     import torch.multiprocessing as mp
@@ -165,3 +180,20 @@ def test_accelerate_prepare_backward_and_checkpoint(golden, tmp_path):
     with torch.no_grad():
         a, b = module(px), back(px)
     assert (a - b).abs().max().item() <= 1e-6 * a.abs().max().item()
+
+
+def test_bench_gpus_2_launches_two_ranks_in_sync():
+    """`bench.py --gpus 2` started WITHOUT a launcher spawns two ranks itself (the driver's scaling
+    run calls it either way); gloo lets both share this box's one GPU.  Rank 0 prints the one JSON
+    line with n_gpus = 2, the whole-job batch, and the replicas' weights equal after the steps."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--profile-steps", "0", "--batch", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = lines[0]
+    print("\n", {k: line[k] for k in ("n_gpus", "value", "ms_per_step", "replicas_equal", "backend")})
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 4 and line["config"]["parallelism"] == "dp2"
+    assert line["replicas_equal"] is True and line["value"] > 0

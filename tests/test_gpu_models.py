@@ -105,6 +105,28 @@ def test_vit_small_loss_curve_matches_reference(golden, frozen):
     np.testing.assert_allclose(losses, ref, rtol=1e-3)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_mse_head_trains_like_torch_reference(dtype):
+    """`training.loss: mse` through the Trainer loop (base.py:144-159 with MSELoss as criterion):
+    3 steps of the small ViT (trainable encoder) against the CPU oracle's forward + MSE mean +
+    torch AdamW / OneCycleLR on the same seeded batches and weights."""
+    from vspike import FusedAdamW
+    from vspike.trainer import Trainer
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n, dtype=dtype)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-5, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=3, max_lr=1e-5, pct_start=0.15, div_factor=10)
+    trainer = Trainer(m, opt, sched, config={"training": {"loss": "mse"}})
+    batches = [(cpu_ref.make_pixels(cfg, B, seed=800 + s), prng.spike_targets(850 + s, (B, 100, n))) for s in range(3)]
+    losses = [float(trainer.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))) for x, y in batches]
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    fwd = lambda x, PP: cpu_ref.videomae_plugin_forward(x, PP, cfg, freeze_encoder=False)  # noqa: E731
+    ref = cpu_ref.train_curve(fwd, P, [(torch.from_numpy(x), torch.from_numpy(y)) for x, y in batches], lr=1e-5,
+                              criterion=cpu_ref.mse_mean)
+    print(f"\n[{dtype}] mse curve {losses} ref {ref}")
+    np.testing.assert_allclose(losses, ref, rtol=1e-3 if dtype == "fp32" else 1e-2)
+
+
 def test_linear_plugin_matches_reference(golden):
     from vspike import Linear, poisson_nll_mean
     fx = golden("linear_f.npz")

@@ -216,13 +216,13 @@ def test_gemm_wide_row_slab_path(bkc, shape, epi):
 @pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape", [(8269, 384, 192), (25093, 576, 192), (25088, 768, 192)])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none", "gelu_grad", "mul_aux"])
-def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
+def test_gemm_w_resident_path(knobs, bkc, shape, epi):
     """K = 192, N a multiple of 192 (qkv, fc1 + GELU, the GELU' product) run on the W-resident kernel
     (W part in LDS once per workgroup, permuted rows so a lane stores 8 consecutive columns, ragged
     row ranges / token blocks): fp64 reference on the same bf16 inputs (tolerances as the wide
-    row-slab test), and the same values as the tile kernels (VSPIKE_NO_WRES=1) to bf16 rounding."""
+    row-slab test), and the same values as the tile kernels (knob no_wres) to bf16 rounding."""
     from vspike import ops, _lib as L
-    monkeypatch.setenv("VSPIKE_WRES_GBWD", "1")   # the GELU' product too (off by default)
+    knobs("wres_gbwd", 1)   # the GELU' product too (off by default)
     M, N, K = shape
     x = _rand(M, K, seed=41).to(torch.bfloat16).to(DEV)
     w = _rand(N, K, seed=42, scale=0.1).to(torch.bfloat16).to(DEV)
@@ -270,7 +270,7 @@ def test_gemm_w_resident_path(monkeypatch, bkc, shape, epi):
         ref = ref * torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
         tol = 1.5e-2
     assert rel(out.float(), ref) < tol
-    monkeypatch.setenv("VSPIKE_NO_WRES", "1")
+    knobs("no_wres", 1)
     out2, pre2 = run()
     assert (out.float() - out2.float()).abs().max() <= 1e-2 * out2.float().abs().max()
     if epi in ("gelu", "gelu_grad"):
@@ -442,16 +442,44 @@ def test_gemm_splitk_atomic_accumulates(dtype, ws, shape):
         assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("shape", [(192, 768, 25088), (768, 192, 25088), (192, 192, 25088), (576, 192, 25088),
+                                   (192, 1536, 25088)])
+def test_dw_bench_split_plan(shape):
+    """The weight gradients of the ViT-Tiny block (dW2, dW1, dWproj, dWqkv) and of the patch
+    embedding at the bench's 25,088 tokens (B=16): the dW-tile kernel with the PLANNED split (the
+    timed step's plan) and its fixed-order reduce, against fp64 with the fused bias row sums;
+    reruns are bit-identical and the dispatch counter shows the dW kernel ran."""
+    from vspike import ops, _lib as L
+    M, N, K = shape
+    dy = _rand(K, M, seed=58).to(torch.bfloat16).to(DEV)
+    x = _rand(K, N, seed=59).to(torch.bfloat16).to(DEV)
+    nb = ops.splitk_workspace_bytes(torch.bfloat16, M, N, K)
+    ws = torch.empty(nb // 4 + 64, device=DEV)
+    outs = []
+    L.dispatch_reset()
+    for _ in range(2):
+        c = torch.full((M, N), 0.25, device=DEV)
+        db = torch.full((M,), 1.5, device=DEV)
+        ops.linear_dw(dy, x, c, db=db, workspace=ws)
+        outs.append((c, db))
+    torch.cuda.synchronize()
+    assert L.dispatch_counts()["gemm_dw"] == 2
+    ref = dy.double().t() @ x.double() + 0.25
+    assert rel(outs[0][0], ref) < 2e-5
+    assert rel(outs[0][1], dy.double().sum(0) + 1.5) < 2e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("bn", [64, 128])
 @pytest.mark.parametrize("bm", [64, 128, 192])
 @pytest.mark.parametrize("shape", [(192, 768, 3136 + 40), (576, 192, 1568), (200, 72, 999)])
-def test_dw_kernel_every_tile_height(monkeypatch, bm, bn, shape):
+def test_dw_kernel_every_tile_height(knobs, bm, bn, shape):
     """The token-reduction dW kernel (gemm_dw.hip) at every tile shape, with ragged tiles, a
     partial last token step, swapped operands (M > N: C stored transposed, bias = column sums of
     the swapped B) and the fixed-order split reduce: bit-identical reruns."""
     from vspike import ops
-    monkeypatch.setenv("VSPIKE_DW_BM", str(bm))
-    monkeypatch.setenv("VSPIKE_DW_BN", str(bn))
+    knobs("dw_bm", bm)
+    knobs("dw_bn", bn)
     M, N, K = shape
     dy = _rand(K, M, seed=18).to(torch.bfloat16).to(DEV)
     x = _rand(K, N, seed=19).to(torch.bfloat16).to(DEV)
@@ -705,6 +733,31 @@ def test_poisson_nll_and_grad():
     (gr,) = torch.autograd.grad(lr, xr)
     assert abs(loss.item() - lr.item()) < 1e-6 * abs(lr.item())
     assert rel(dx, gr) < 1e-6
+
+
+def test_mse_loss_and_grad():
+    """The MSE head option (vs_mse_loss) against torch.nn.MSELoss() in fp64: loss, gradient, the
+    upstream-scaled backward entry point, and a ragged size (n not a multiple of the block)."""
+    from vspike import ops, mse_mean
+    for shape in ((4, 100, 128), (3, 7, 11)):
+        x = _rand(*shape, seed=61, scale=0.7)
+        y = _rand(*shape, seed=62).abs() * 3.0
+        loss = torch.empty((), device=DEV)
+        dx = torch.empty_like(x, device=DEV)
+        ops.mse_loss(x.to(DEV), y.to(DEV), loss, dx=dx)
+        xr = x.double().requires_grad_()
+        lr = torch.nn.MSELoss()(xr, y.double())
+        (gr,) = torch.autograd.grad(lr, xr)
+        assert abs(loss.item() - lr.item()) < 1e-6 * abs(lr.item())
+        assert rel(dx, gr) < 1e-6
+        g = torch.tensor([0.5], device=DEV)
+        dx2 = torch.empty_like(dx)
+        ops.mse_loss_bwd(x.to(DEV), y.to(DEV), g, dx2)
+        assert rel(dx2, 0.5 * gr) < 1e-6
+        xa = x.to(DEV).requires_grad_()
+        la = mse_mean(xa, y.to(DEV))
+        (la * 3.0).backward()
+        assert rel(xa.grad, 3.0 * gr) < 1e-6
 
 
 def test_fused_adamw_matches_torch():

@@ -26,10 +26,10 @@ DEV = "cuda"
 
 # measured on MI355X (r02, HEAD cab4b27): tiny12 log-rates 2.4e-3, loss 6.3e-6, worst gradient
 # 1.8e-2 (layer 10 query.weight), curve 2.7e-4; base1l log-rates 3.5e-3, loss 2.1e-5, worst
-# gradient 9.9e-3 (layer 0 value.weight), frozen curve 2.0e-4
-BF16_OUT = 1e-2      # log-rates, relative to max|ref|
+# gradient 9.9e-3 (layer 0 value.weight), frozen curve 2.0e-4.  Bars: ~2x the worst measured.
+BF16_OUT = 7e-3      # log-rates, relative to max|ref|
 BF16_LOSS = 1e-3     # loss and loss-curve steps, relative: the north star's 1e-3 holds in bf16 too
-BF16_GRAD = 4e-2     # norm-relative gradient error
+BF16_GRAD = 3.7e-2   # norm-relative gradient error
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -66,11 +66,11 @@ def _named_grads(m):
     return out
 
 
-def _fwd_bwd_case(fx, cfg, B, n, dtype):
+def _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=0, y_seed=1):
     from vspike import poisson_nll_mean
     m = _vit_model(cfg, 64, n, dtype)
-    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
-    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=px_seed)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(y_seed, (B, 100, n))).to(DEV)
     out = m(px)
     loss = poisson_nll_mean(out, y)
     loss.backward()
@@ -128,6 +128,82 @@ def test_vit_tiny12_bench_geometry_loss_curve(golden, dtype):
     assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
 
 
+# kernel paths the benched bf16 step takes at M = B * 1568 = 25,088 token rows (vspike.h VS_PATH_*):
+# W-resident qkv / fc1, proj + LayerNorm2 fused, row-slab N <= 192 products (fc2, dX, patch
+# embedding), the wide row-slab GELU' product, the dW tiles, the skinny head, flash attention
+BENCH_PATHS_BF16 = ("gemm_wres", "gemm_ln_fwd", "gemm_slab", "gemm_wslab", "gemm_dw", "gemm_skinny", "attn_fwd",
+                    "attn_bwd")
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_tiny12_b16_benched_dispatch_forward_backward(golden, dtype):
+    """The bench's exact workload (C2, 12 layers, B=16 -> M = 25,088) against the reference's own
+    forward/backward at that batch (fixture vit_tiny12_b16 from HF VideoMAEModel): log-rates, loss and
+    all 183 gradients; in bf16 the dispatch counters prove the benched kernel paths ran."""
+    from vspike import _lib as L
+    fx = golden("vit_tiny12_b16.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 16, 128
+    L.dispatch_reset()
+    m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=16, y_seed=16)
+    counts = {k: v for k, v in L.dispatch_counts().items() if v}
+    print(f"[{dtype}] dispatch {counts}")
+    if dtype == "fp32":
+        assert out_err < 1e-4 and loss_err < 1e-5
+        shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+        for k, v in g.items():
+            ok, msg = cpu_ref.compare_summary(k, v.reshape(shapes[k]), fx, rtol=1e-3, atol=1e-8)
+            assert ok, msg
+    else:
+        missing = [p for p in BENCH_PATHS_BF16 if not counts.get(p)]
+        assert not missing, (missing, counts)
+        assert out_err < BF16_OUT and loss_err < BF16_LOSS
+        bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
+        assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_tiny12_b16_benched_dispatch_loss_curve(golden, dtype):
+    """3 optimiser steps of the reference loop (base.py:144-159) at the bench batch (B=16)."""
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_tiny12_b16.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 16, 128
+    m = _vit_model(cfg, 64, n, dtype)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-6, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=3, max_lr=1e-6, pct_start=0.15, div_factor=10)
+    losses = []
+    for s in range(3):
+        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=600 + s)).to(DEV)
+        y = torch.from_numpy(prng.spike_targets(650 + s, (B, 100, n))).to(DEV)
+        loss = poisson_nll_mean(m(px), y)
+        loss.backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        losses.append(loss.item())
+    rel = np.abs(np.array(losses) - fx["curve_train"]) / np.abs(fx["curve_train"])
+    print(f"\n[{dtype}] B=16 curve {losses} ref {fx['curve_train'].tolist()} max rel {rel.max():.3e}")
+    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_base_32_frames_c5_encoder_geometry(golden, dtype):
+    """BASELINE C5's encoder geometry: videomae-base width at 32 frames -> 3,136 tokens (24 * 128 + 64:
+    a 64-row tail tile), n = 1024, one layer, B=1, trainable — against the reference's HF encoder."""
+    fx = golden("vit_base32f.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_frames=32, num_hidden_layers=1), 1, 1024
+    m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=32, y_seed=32)
+    if dtype == "fp32":
+        assert out_err < 1e-4 and loss_err < 1e-5
+        shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+        for k, v in g.items():
+            ok, msg = cpu_ref.compare_summary(k, v.reshape(shapes[k]), fx, rtol=1e-3, atol=1e-8)
+            assert ok, msg
+    else:
+        assert out_err < BF16_OUT and loss_err < BF16_LOSS
+        bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
+        assert not bad, bad
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_vit_base_one_layer_forward_backward(golden, dtype):
     """C3 width (d768, 12 heads -> B*H = 12 attention heads per clip), full tokens, n=512."""
@@ -172,6 +248,12 @@ def test_vit_base_frozen_encoder_loss_curve(golden, dtype):
     assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
 
 
+def test_loaded_library_is_built_from_these_sources():
+    """The libvspike.so this GPU run loaded carries the hash of the sources in this tree."""
+    from vspike import _lib, build
+    assert _lib.build_id() == build.source_hash()
+
+
 # ------------------------------------------------------------------------ attention, bench grids
 def _attn_ref64(qkv, do, B, N, H, scale=0.125):
     """fp64 reference on the device (the CPU would take minutes at B*H = 192), in head chunks."""
@@ -198,12 +280,12 @@ def _rel(a, b):
     return float((a.double() - b).norm() / b.norm())
 
 
-@pytest.mark.parametrize("H", [3, 12])
-def test_attention_bf16_at_bench_grid(H):
+@pytest.mark.parametrize("B,N,H", [(16, 1568, 3), (16, 1568, 12), (2, 3136, 12)])
+def test_attention_bf16_at_bench_grid(B, N, H):
     """B=16, N=1568: the grids the bench (H=3, 624 workgroups per pass, XCD-remapped) and C3
-    (H=12, 2496) launch; the row prep + fused dK/dV / dQ backward on the forward's own O and LSE."""
+    (H=12, 2496) launch; N=3136 (C5's 32 frames, tail 64); the row prep + fused dK/dV / dQ backward
+    on the forward's own O and LSE."""
     from vspike import ops
-    B, N = 16, 1568
     D = H * 64
     g = torch.Generator(device=DEV).manual_seed(1234 + H)
     # activations of the scale a trained ViT shows: |scores| up to ~20
@@ -219,7 +301,7 @@ def test_attention_bf16_at_bench_grid(H):
     o_ref, lse_ref, d_ref = _attn_ref64(qkv, do, B, N, H)
     eo, el = _rel(o.float(), o_ref), _rel(lse, lse_ref)
     parts = [_rel(dqkv[:, i * D:(i + 1) * D].float(), d_ref[:, i * D:(i + 1) * D]) for i in range(3)]
-    print(f"\n[attn B=16 H={H}] o {eo:.3e} lse {el:.3e} dq {parts[0]:.3e} dk {parts[1]:.3e} dv {parts[2]:.3e}")
+    print(f"\n[attn B={B} N={N} H={H}] o {eo:.3e} lse {el:.3e} dq {parts[0]:.3e} dk {parts[1]:.3e} dv {parts[2]:.3e}")
     assert eo < 1.5e-2 and el < 3e-3
     assert max(parts) < 3e-2, parts
     # every (batch, head) block covered: per-head errors, not only the global norm
@@ -233,7 +315,8 @@ def test_attention_bf16_at_bench_grid(H):
 def test_deferred_joins_four_layers_per_layer_grads(mode):
     """VS_BWD_DEFER_JOIN / _LAST with 4 layers (several deferred blocks in a row: alternating event
     parity, pending bits carried forward) over two steps: every layer's gradient slice equals the
-    join-every-block result (norm-relative 1e-5: the fused bias row sums add f32 atomics)."""
+    join-every-block result (every reduction is fixed-order, so this holds to the last bit; the bar
+    is norm-relative 1e-5)."""
     import vspike.vit as V
     from vspike import poisson_nll_mean
     cfg = cpu_ref.ViTCfg(image_size=112, num_frames=8, hidden_size=128, num_hidden_layers=4,

@@ -129,6 +129,52 @@ def test_vit_tiny12_bench_geometry_matches_reference(golden):
     np.testing.assert_allclose(curve, fx["curve_train"], rtol=1e-4)
 
 
+def test_vit_tiny12_bench_batch_matches_reference(golden):
+    """The bench's exact batch (C2, 12 layers, B=16 -> 25,088 token rows, fixture vit_tiny12_b16):
+    log-rates, loss, every gradient and the 3-step train curve."""
+    fx = golden("vit_tiny12_b16.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 16, 128
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=16))
+    y = torch.from_numpy(prng.spike_targets(16, (B, 100, n)))
+    out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-5 * abs(fx["loss"][0])
+    loss.backward()
+    for k, p in P.items():
+        if ".key.bias" in k:
+            continue
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=5e-4, atol=1e-7)
+        assert ok, msg
+    del out, loss
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    batches = [(torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=600 + s)),
+                torch.from_numpy(prng.spike_targets(650 + s, (B, 100, n)))) for s in range(3)]
+    fwd = lambda x, PP: cpu_ref.videomae_plugin_forward(x, PP, cfg, freeze_encoder=False)  # noqa: E731
+    curve = cpu_ref.train_curve(fwd, P, batches, lr=1e-6)
+    np.testing.assert_allclose(curve, fx["curve_train"], rtol=1e-4)
+
+
+def test_vit_base_32_frames_matches_reference(golden):
+    """BASELINE C5's encoder geometry (videomae-base, 32 frames -> 3,136 tokens, n=1024), 1 layer, B=1."""
+    fx = golden("vit_base32f.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_frames=32, num_hidden_layers=1), 1, 1024
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n))
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=32))
+    y = torch.from_numpy(prng.spike_targets(32, (B, 100, n)))
+    out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    np.testing.assert_allclose(out.detach().numpy(), fx["log_rates"], rtol=1e-4, atol=1e-5)
+    loss = cpu_ref.poisson_nll_mean(out, y)
+    assert abs(loss.item() - fx["loss"][0]) <= 1e-5 * abs(fx["loss"][0])
+    loss.backward()
+    for k, p in P.items():
+        if ".key.bias" in k:
+            continue
+        ok, msg = cpu_ref.compare_summary(k, p.grad.numpy(), fx, rtol=5e-4, atol=1e-7)
+        assert ok, msg
+
+
 def test_vit_base_one_layer_matches_reference(golden):
     """The reference plugin's real width (videomae-base d768 / 12 heads, C3's n=512), 1 layer, B=1:
     trainable fwd+bwd, and the default frozen-encoder curve."""

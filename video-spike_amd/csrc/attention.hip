@@ -1097,10 +1097,12 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
+    count_path(VS_PATH_ATTN_FWD);
     hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse,
                        (int)N, (int)H, scale * kLog2e);
   } else if (dtype == VS_F32) {
     dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);
+    count_path(VS_PATH_ATTN_F32);
     hipLaunchKernelGGL(attn_fwd_f32_kernel, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, (float*)o, ld_o, lse,
                        (int)N, (int)H, scale);
   } else {
@@ -1139,6 +1141,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     const int64_t npad = attn_npad(N);
     float* nlse2 = (float*)workspace;
     float* ndel = nlse2 + B * H * npad;
+    count_path(VS_PATH_ATTN_BWD);
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
@@ -1146,6 +1149,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
                        (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
                        scale, (int)grid.x);
   } else if (dtype == VS_F32) {
+    count_path(VS_PATH_ATTN_F32);
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,
                        (const float*)dout, ld_do, delta, rows, (int)N, (int)H);
     dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);

@@ -38,6 +38,11 @@ void set_error(const char* msg);
     if (_r != VS_OK) return _r;     \
   } while (0)
 
+// A/B and test knobs (VS_KNOB_*): read from the environment once, overridable by vs_knob_set
+int knob(int id);
+// dispatch counters (VS_PATH_*): one relaxed host-side add per launch of a path
+void count_path(int id);
+
 inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t esize(int dtype) { return dtype == VS_BF16 ? 2 : 4; }

@@ -150,21 +150,36 @@ __global__ void cast_bf16_f32(const bf16_t* __restrict__ in, float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// PoissonNLLLoss(log_input=True), mean reduction, fused with its gradient.
+// PoissonNLLLoss(log_input=True) or MSELoss, mean reduction, fused with its gradient.
 // Stage 1: per-block partial sums (fixed order) + dx.  Stage 2: one block sums the partials in a
 // fixed order -> deterministic loss.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPoissonBlocks = 256;
+enum { kLossPoisson = 0, kLossMse = 1 };
 
-__global__ void poisson_stage1(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ dx,
-                               float gscale, int64_t n, float* __restrict__ partial) {
+// the loss term and its derivative in x: Poisson exp(x) - y x, (exp(x) - y); MSE (x - y)^2, 2 (x - y)
+template <int KIND>
+__device__ __forceinline__ float loss_term(float x, float y, float& grad) {
+  if constexpr (KIND == kLossPoisson) {
+    const float ex = expf(x);
+    grad = ex - y;
+    return ex - y * x;
+  } else {
+    const float d = x - y;
+    grad = 2.0f * d;
+    return d * d;
+  }
+}
+
+template <int KIND>
+__global__ void loss_stage1(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ dx,
+                            float gscale, int64_t n, float* __restrict__ partial) {
   __shared__ float red[4];
   float s = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float xi = x[i], yi = y[i];
-    const float ex = expf(xi);
-    s += ex - yi * xi;
-    if (dx) dx[i] = gscale * (ex - yi);
+    float g;
+    s += loss_term<KIND>(x[i], y[i], g);
+    if (dx) dx[i] = gscale * g;
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -180,11 +195,15 @@ __global__ void poisson_stage2(const float* __restrict__ partial, int nb, float 
   __syncthreads();
   if (threadIdx.x == 0) loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) * inv_n;
 }
-__global__ void poisson_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                   const float* __restrict__ g, float* __restrict__ dx, int64_t n) {
+template <int KIND>
+__global__ void loss_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ g,
+                                float* __restrict__ dx, int64_t n) {
   const float s = g[0] / (float)n;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dx[i] = s * (expf(x[i]) - y[i]);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gr;
+    (void)loss_term<KIND>(x[i], y[i], gr);
+    dx[i] = s * gr;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -321,24 +340,44 @@ extern "C" size_t vs_poisson_workspace_bytes(int64_t n) {
   return kPoissonBlocks * sizeof(float);
 }
 
-extern "C" int vs_poisson_nll(int64_t n, const float* log_rate, const float* target, float* loss_out, float* dx,
-                              float grad_scale, void* workspace, void* stream) {
-  VS_REQUIRE(n > 0 && log_rate && target && loss_out && workspace, "vs_poisson_nll: bad args");
-  hipStream_t s = (hipStream_t)stream;
+template <int KIND>
+static int loss_fwd(int64_t n, const float* x, const float* y, float* loss_out, float* dx, float grad_scale,
+                    void* workspace, hipStream_t s) {
   ScopedTimer timer(VS_TIMER_MISC, s, (double)n * (dx ? 12.0 : 8.0));
   int nb = (int)cdiv(n, 256);
   if (nb > kPoissonBlocks) nb = kPoissonBlocks;
-  hipLaunchKernelGGL(poisson_stage1, dim3(nb), dim3(256), 0, s, log_rate, target, dx, grad_scale / (float)n, n,
+  hipLaunchKernelGGL((loss_stage1<KIND>), dim3(nb), dim3(256), 0, s, x, y, dx, grad_scale / (float)n, n,
                      (float*)workspace);
   hipLaunchKernelGGL(poisson_stage2, dim3(1), dim3(256), 0, s, (const float*)workspace, nb, 1.0f / (float)n, loss_out);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
 
+extern "C" int vs_poisson_nll(int64_t n, const float* log_rate, const float* target, float* loss_out, float* dx,
+                              float grad_scale, void* workspace, void* stream) {
+  VS_REQUIRE(n > 0 && log_rate && target && loss_out && workspace, "vs_poisson_nll: bad args");
+  return loss_fwd<kLossPoisson>(n, log_rate, target, loss_out, dx, grad_scale, workspace, (hipStream_t)stream);
+}
+
 extern "C" int vs_poisson_nll_bwd(int64_t n, const float* log_rate, const float* target, const float* grad_out,
                                   float* dx, void* stream) {
   VS_REQUIRE(n > 0 && log_rate && target && grad_out && dx, "vs_poisson_nll_bwd: bad args");
-  hipLaunchKernelGGL(poisson_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, log_rate, target,
+  hipLaunchKernelGGL((loss_bwd_kernel<kLossPoisson>), dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, log_rate,
+                     target, grad_out, dx, n);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_mse_loss(int64_t n, const float* pred, const float* target, float* loss_out, float* dx,
+                           float grad_scale, void* workspace, void* stream) {
+  VS_REQUIRE(n > 0 && pred && target && loss_out && workspace, "vs_mse_loss: bad args");
+  return loss_fwd<kLossMse>(n, pred, target, loss_out, dx, grad_scale, workspace, (hipStream_t)stream);
+}
+
+extern "C" int vs_mse_loss_bwd(int64_t n, const float* pred, const float* target, const float* grad_out, float* dx,
+                               void* stream) {
+  VS_REQUIRE(n > 0 && pred && target && grad_out && dx, "vs_mse_loss_bwd: bad args");
+  hipLaunchKernelGGL((loss_bwd_kernel<kLossMse>), dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, pred, target,
                      grad_out, dx, n);
   VS_LAUNCH_CHECK();
   return VS_OK;

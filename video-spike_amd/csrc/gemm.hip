@@ -1985,47 +1985,6 @@ static GemmPlan plan_gemm(int dtype, int64_t M, int64_t N, int64_t K, int want_s
   return p;
 }
 
-static int getenv_flag(const char* name) {  // A/B switch for benchmarking, read once
-  static int cached = -1;
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached;
-}
-
-static int getenv_flag2(const char* name) {
-  static int cached = -1;
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached;
-}
-
-static int getenv_flag4(const char* name) {
-  static int cached = -1;
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached;
-}
-
-static int getenv_flag3(const char* name) {
-  static int cached = -1;
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached;
-}
-
-static int getenv_flag5(const char* name) {
-  const char* v = getenv(name);
-  return (v && v[0] && v[0] != '0') ? 1 : 0;
-}
-
 static bool vec_ok(const vs_gemm_desc* d) {
   const uint32_t f = d->epilogue;
   const int ovec = d->out_dtype == VS_BF16 ? 8 : 4;
@@ -2112,20 +2071,19 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
   const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
   // token-reduction weight gradients (dW = dY^T X, both operands token-major): the dedicated
   // split-K kernel with a fixed-order reduce (gemm_dw.hip)
-  static const int no_dw = getenv_flag5("VSPIKE_DW_OLD");
-  if (!no_dw && d->dtype == VS_BF16 && d->out_dtype == VS_F32 && f == VS_EPI_ATOMIC && !d->a_kcontig &&
+  if (!knob(VS_KNOB_DW_OLD) && d->dtype == VS_BF16 && d->out_dtype == VS_F32 && f == VS_EPI_ATOMIC && !d->a_kcontig &&
       !d->b_kcontig && d->split_k <= 0 && use_ws && d->K >= 1 && d->M % 8 == 0 && d->N % 8 == 0 &&
       d->lda % 8 == 0 && d->ldb % 8 == 0 && (size_t)d->workspace_bytes >= dw_workspace_bytes(d->M, d->N, d->K))
-    return launch_dw(d, s);
+    return count_path(VS_PATH_GEMM_DW), launch_dw(d, s);
   // skinny split-K with K-contiguous operands (the head forward): fragments straight from HBM
-  static const int no_skinny = getenv_flag5("VSPIKE_NO_SKINNY");
   const bool dense_c = d->ldc == d->N && aligned16(d->c) && (!(f & VS_EPI_BIAS) || aligned16(d->bias));
-  const bool skinny = !no_skinny && use_ws && dense_c && skinny_ok(d) &&
+  const bool skinny = !knob(VS_KNOB_NO_SKINNY) && use_ws && dense_c && skinny_ok(d) &&
                       (size_t)d->workspace_bytes >= skinny_workspace_bytes(d->dtype, d->M, d->N, d->K);
   VS_REQUIRE(skinny || !((f & VS_EPI_ATOMIC) && (f & VS_EPI_RELU)),
              "vs_gemm: ATOMIC|RELU needs the skinny split-K path (M <= 64, N <= 256, K-contiguous, workspace)");
   if (skinny) {
     int S = 0;
+    count_path(VS_PATH_GEMM_SKINNY);
     VS_CALL(launch_skinny(d, s, &S));
     const int64_t n4 = d->M * d->N / 4;
     hipLaunchKernelGGL(gemm_splitk_reduce_wide, dim3((unsigned)n4), dim3(256), 0, s, (const float*)d->workspace, S, d->M,
@@ -2134,11 +2092,11 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     return VS_OK;
   }
   // row-slab path: N <= 192 outputs of a large-M, K-contiguous-A product, no split / reduction
-  static const int no_slab = getenv_flag5("VSPIKE_NO_SLAB");
-  if (!no_slab && d->dtype == VS_BF16 && d->a_kcontig && (d->N == 64 || d->N == 128 || d->N == 192) &&
+  if (!knob(VS_KNOB_NO_SLAB) && d->dtype == VS_BF16 && d->a_kcontig && (d->N == 64 || d->N == 128 || d->N == 192) &&
       d->K % 64 == 0 && d->K >= 64 && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
       (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_RESIDUAL) || f == (VS_EPI_BIAS | VS_EPI_POS))) {
     const int64_t G = d->M / 16 < 512 ? d->M / 16 : 512;
+    count_path(VS_PATH_GEMM_SLAB);
     if (d->N == 64) launch_bf16_slab<1>(d, (unsigned)G, e, s);
     else if (d->N == 128) launch_bf16_slab<2>(d, (unsigned)G, e, s);
     else launch_bf16_slab<3>(d, (unsigned)G, e, s);
@@ -2146,8 +2104,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     return VS_OK;
   }
   // big-tile path: MFMA-heavy products (K >= 512, N >= 512, N % 128 == 0: the ViT-Base block)
-  static const int no_big = getenv_flag5("VSPIKE_NO_BIG");
-  if (!no_big && d->dtype == VS_BF16 && d->a_kcontig && d->M >= 4096 && d->N >= 512 && d->N % 128 == 0 &&
+  if (!knob(VS_KNOB_NO_BIG) && d->dtype == VS_BF16 && d->a_kcontig && d->M >= 4096 && d->N >= 512 && d->N % 128 == 0 &&
       d->K >= 512 && d->K % 64 == 0 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
       !(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM))) {
     GridMap g;
@@ -2155,19 +2112,18 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     g.tiles_n = (int)(d->N / 128);
     g.splits = 1;
     g.k_per_split = d->K;
+    count_path(VS_PATH_GEMM_BIG);
     launch_bf16_big(d, (unsigned)((int64_t)g.tiles_m * g.tiles_n), g, e, s);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
   // W-resident path: K = 192, N a multiple of 192 (>= 384): qkv, fc1 + GELU, the GELU' product
   {
-    const char* nv = getenv("VSPIKE_NO_WRES");  // A/B knob (read per call: tests toggle it)
-    const bool no_wres = nv && nv[0] && nv[0] != '0';
+    const bool no_wres = knob(VS_KNOB_NO_WRES) != 0;
     // the GELU' product (GELU_BWD, or MUL_AUX on the stored gelu') stays on the wide row-slab kernel
     // unless VSPIKE_WRES_GBWD=1: 35.7 vs 41.2 us (GELU_BWD), 27.8 vs 32.6 us (MUL_AUX) there — its
     // operand stream (a 16-B aux read per 8 outputs) overlaps better with the row-slab schedule
-    const char* gv = getenv("VSPIKE_WRES_GBWD");
-    const bool gbwd = gv && gv[0] && gv[0] != '0';
+    const bool gbwd = knob(VS_KNOB_WRES_GBWD) != 0;
     const bool ef_ok = (f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU) || f == 0 ||
                         f == (VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD) ||
                         (gbwd && (f == VS_EPI_GELU_BWD || f == VS_EPI_MUL_AUX))) &&
@@ -2175,6 +2131,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     if (!no_wres && ef_ok && d->dtype == VS_BF16 && d->a_kcontig && d->K == 192 && d->N % kWresNH == 0 &&
         d->N >= 2 * kWresNH && d->N <= 64 * kWresNH && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->lda % 8 == 0 &&
         d->ldb % 8 == 0 && aligned16(d->a) && aligned16(d->b)) {
+      count_path(VS_PATH_GEMM_WRES);
       if (f == VS_EPI_BIAS) launch_bf16_wres_ef<(uint32_t)VS_EPI_BIAS>(d, e, s);
       else if (f == (VS_EPI_BIAS | VS_EPI_GELU)) launch_bf16_wres_ef<(uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, e, s);
       else if (f == 0) launch_bf16_wres_ef<0u>(d, e, s);
@@ -2187,17 +2144,17 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     }
   }
   // wide row-slab path: K <= 192, N > 192 (qkv, fc1 + GELU, the GELU' dX product)
-  static const int no_wslab = getenv_flag5("VSPIKE_NO_WSLAB");
   // Measured (scripts/microbench.py, bench shapes): faster than the panel kernel for the GELU'
   // product (39.7 -> 36.8 us), slower than the whole-K tile kernel for the store-bound forward
   // products (qkv 19.0 -> 22.2, fc1 + GELU 37.9 -> 41.2 us), which therefore stay on it unless
   // VSPIKE_WSLAB=1 forces this path for every eligible epilogue.
-  static const int all_wslab = getenv_flag5("VSPIKE_WSLAB");
-  if (!no_wslab && d->dtype == VS_BF16 && d->a_kcontig && d->N % 64 == 0 && d->N > 192 &&
+  const int all_wslab = knob(VS_KNOB_WSLAB);
+  if (!knob(VS_KNOB_NO_WSLAB) && d->dtype == VS_BF16 && d->a_kcontig && d->N % 64 == 0 && d->N > 192 &&
       (d->K == 64 || d->K == 128 || d->K == 192) && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok &&
       (f == VS_EPI_GELU_BWD || (f == VS_EPI_MUL_AUX && e.op_bf16) ||
        (all_wslab && (f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_GELU))))) {
-    static const int gw = getenv("VSPIKE_WSLAB_G") ? atoi(getenv("VSPIKE_WSLAB_G")) : 512;  // A/B knob
+    const int gw = knob(VS_KNOB_WSLAB_G) > 0 ? knob(VS_KNOB_WSLAB_G) : 512;
+    count_path(VS_PATH_GEMM_WSLAB);
     const int64_t G = d->M / 16 < gw ? d->M / 16 : gw;
     if (d->K == 64) launch_bf16_wslab<1>(d, (unsigned)G, e, s);
     else if (d->K == 128) launch_bf16_wslab<2>(d, (unsigned)G, e, s);
@@ -2219,16 +2176,13 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     // GELU' product (da: 43.2 -> 38.7 us); the per-tile whole-K kernel wins on the others (its
     // 2352 short tiles balance better than 512 persistent workgroups that each load a 48-KB A panel
     // before their first MFMA).  VSPIKE_PANEL=1 forces it for every eligible shape.
-    const bool panel = ((f & VS_EPI_GELU_BWD) || getenv_flag4("VSPIKE_PANEL")) && d->a_kcontig && g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 &&
+    const bool panel = ((f & VS_EPI_GELU_BWD) || knob(VS_KNOB_PANEL)) && d->a_kcontig && g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 &&
                        d->N % 64 == 0 && !d->a_rowsum && !(f & (VS_EPI_ATOMIC | VS_EPI_ACCUM)) && e.vec_ok &&
-                       getenv_flag3("VSPIKE_NO_PANEL") == 0;
+                       knob(VS_KNOB_NO_PANEL) == 0;
     if (panel) {
       const int64_t items = cdiv(d->M, 128) * (d->N / 64);
-      static int gcap = -1;  // A/B knob: VSPIKE_PANEL_GRID overrides the 512-workgroup cap
-      if (gcap < 0) {
-        const char* v = getenv("VSPIKE_PANEL_GRID");
-        gcap = v && atoi(v) > 0 ? atoi(v) : 512;
-      }
+      const int gcap = knob(VS_KNOB_PANEL_GRID) > 0 ? knob(VS_KNOB_PANEL_GRID) : 512;
+      count_path(VS_PATH_GEMM_PANEL);
       const unsigned grid = (unsigned)(items < gcap ? items : gcap);
       const int KT = (int)(d->K / 64);
       if (KT == 1) launch_bf16_panel<1>(d, grid, items, e, s);
@@ -2238,28 +2192,34 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       return VS_OK;
     }
     const bool fullk = g.splits == 1 && d->K % 64 == 0 && d->K >= 64 && d->K <= 192 && BM == 128 && !d->a_rowsum &&
-                       !(f & VS_EPI_ATOMIC) && getenv_flag("VSPIKE_NO_FULLK") == 0;
+                       !(f & VS_EPI_ATOMIC) && knob(VS_KNOB_NO_FULLK) == 0;
     if (fullk) {
       GridMap gf = g;
       gf.tiles_n = (int)cdiv(d->N, 64);
       const int64_t nbf = (int64_t)gf.tiles_n * gf.tiles_m;
       const int KT = (int)(d->K / 64);
+      count_path(VS_PATH_GEMM_FULLK);
       if (KT == 1) launch_bf16_fullk<128, 64, 1>(d, (unsigned)nbf, gf, e, s);
       else if (KT == 2) launch_bf16_fullk<128, 64, 2>(d, (unsigned)nbf, gf, e, s);
       else launch_bf16_fullk<128, 64, 3>(d, (unsigned)nbf, gf, e, s);
-    } else if (d->K % 64 == 0 && getenv_flag2("VSPIKE_NO_RING") == 0) {
+    } else if (d->K % 64 == 0 && knob(VS_KNOB_NO_RING) == 0) {
+      count_path(VS_PATH_GEMM_RING);
       // long K: 3-stage DMA ring, BN = 64 tiles (72 KB of LDS at BM = 128: 2 blocks per CU)
       GridMap gr = plan_gemm_bn64(d, g);
       const int64_t nbr = (int64_t)gr.tiles_n * gr.tiles_m * gr.splits;
       if (BM == 128) launch_bf16_ring<128, 64>(d, (unsigned)nbr, gr, e, s);
       else launch_bf16_ring<64, 64>(d, (unsigned)nbr, gr, e, s);
     } else if (BM == 128 && BN == 128) {
+      count_path(VS_PATH_GEMM_TILE);
       launch_bf16<128, 128>(d, (unsigned)nblk, g, e, s);
     } else if (BM == 128) {
+      count_path(VS_PATH_GEMM_TILE);
       launch_bf16<128, 64>(d, (unsigned)nblk, g, e, s);
     } else if (BN == 128) {
+      count_path(VS_PATH_GEMM_TILE);
       launch_bf16<64, 128>(d, (unsigned)nblk, g, e, s);
     } else {
+      count_path(VS_PATH_GEMM_TILE);
       launch_bf16<64, 64>(d, (unsigned)nblk, g, e, s);
     }
   } else {
@@ -2268,6 +2228,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     const float* a = (const float*)d->a;
     const float* b = (const float*)d->b;
     dim3 grid((unsigned)nblk);
+    count_path(VS_PATH_GEMM_F32);
     if (d->a_kcontig && d->b_kcontig)
       hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
     else if (d->a_kcontig)
@@ -2301,8 +2262,10 @@ extern "C" int vs_gemm_ln_fwd(const vs_gemm_desc* d, const float* gamma, const f
   if (d->M == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
   const int64_t M = d->M, N = d->N;
-  static const int no_fuse = getenv_flag5("VSPIKE_NO_LNF_FUSE");
-  const bool fused = !no_fuse && d->dtype == VS_BF16 && d->a_kcontig && N == 192 && d->K % 64 == 0 && d->K >= 64 &&
+  VS_REQUIRE(d->a && d->b && d->c && d->residual, "vs_gemm_ln_fwd: null operand");
+  VS_REQUIRE(d->ldc >= N && d->ld_residual >= N && ldh >= N, "vs_gemm_ln_fwd: ldc / ld_residual / ldh < N");
+  VS_REQUIRE(!(d->epilogue & VS_EPI_BIAS) || d->bias, "vs_gemm_ln_fwd: BIAS needs bias");
+  const bool fused = !knob(VS_KNOB_NO_LNF_FUSE) && d->dtype == VS_BF16 && d->a_kcontig && N == 192 && d->K % 64 == 0 && d->K >= 64 &&
                      M >= 8192 && aligned16(d->a) && aligned16(d->b) && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
                      d->lda >= d->K && (d->b_kcontig ? d->ldb >= d->K : d->ldb >= N) && aligned16(d->c) &&
                      d->ldc % 4 == 0 && aligned16(d->residual) && d->ld_residual % 4 == 0 &&
@@ -2323,6 +2286,7 @@ extern "C" int vs_gemm_ln_fwd(const vs_gemm_desc* d, const float* gamma, const f
   LnBwdParams ln = {};
   ln.gamma = gamma; ln.beta = beta; ln.eps = eps; ln.h = (bf16_t*)h; ln.ldh = ldh; ln.mean_out = mean; ln.rstd_out = rstd;
   const int64_t G = M / 16 < 512 ? M / 16 : 512;
+  count_path(VS_PATH_GEMM_LN_FWD);
   if (d->epilogue & VS_EPI_BIAS) launch_bf16_slab_ef<3, (uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL), false, true>(d, (unsigned)G, e, s, ln);
   else launch_bf16_slab_ef<3, (uint32_t)VS_EPI_RESIDUAL, false, true>(d, (unsigned)G, e, s, ln);
   VS_LAUNCH_CHECK();
@@ -2338,8 +2302,9 @@ extern "C" int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx
   if (d->M == 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
   const int64_t M = d->M, N = d->N;
-  static const int no_fuse = getenv_flag5("VSPIKE_NO_LN_FUSE");
-  const bool fused = !no_fuse && d->dtype == VS_BF16 && d->a_kcontig && (N == 64 || N == 128 || N == 192) &&
+  VS_REQUIRE(d->a && d->b, "vs_gemm_ln_bwd: null operand");
+  VS_REQUIRE(ldx >= N && lddx >= N && (!dres || lddres >= N), "vs_gemm_ln_bwd: ldx / lddx / lddres < N");
+  const bool fused = !knob(VS_KNOB_NO_LN_FUSE) && d->dtype == VS_BF16 && d->a_kcontig && (N == 64 || N == 128 || N == 192) &&
                      d->K % 64 == 0 && d->K >= 64 && M >= 8192 && workspace &&
                      aligned16(d->a) && aligned16(d->b) && d->lda % 8 == 0 && d->ldb % 8 == 0 && d->lda >= d->K &&
                      (d->b_kcontig ? d->ldb >= d->K : d->ldb >= N) && aligned16(x) && ldx % 4 == 0 && aligned16(dx) &&
@@ -2361,6 +2326,7 @@ extern "C" int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx
   ln.x = x; ln.ldx = ldx; ln.mean = mean; ln.rstd = rstd; ln.gamma = gamma; ln.dres = dres; ln.ldr = lddres;
   ln.dx = dx; ln.lddx = lddx; ln.dx_lp = (bf16_t*)dx_lp; ln.part = (float*)workspace;
   const int64_t G = M / 16 < 512 ? M / 16 : 512;  // <= the 1024 partial rows of the LN workspace
+  count_path(VS_PATH_GEMM_LN_BWD);
   if (N == 64) launch_bf16_slab_ef<1, 0u, true>(d, (unsigned)G, e, s, ln);
   else if (N == 128) launch_bf16_slab_ef<2, 0u, true>(d, (unsigned)G, e, s, ln);
   else launch_bf16_slab_ef<3, 0u, true>(d, (unsigned)G, e, s, ln);

@@ -570,16 +570,11 @@ int launch_skinny(const vs_gemm_desc* d, hipStream_t s, int* splits_out) {
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && v[0] ? atoi(v) : dflt;
-}
-
 // Cost model (microseconds), fitted to rocprof durations of the C2 shapes: a launch pays ~10 us of
 // fixed cost (dispatch, the prologue burst of every workgroup's first stages, the partial-tile store
 // burst at the end, the reduce launch); a 64-token step costs ~0.25 us + 0.02 us per MFMA of a wave
 // (0.49 us at 192 x 64, 0.73 us at 192 x 128), and the partial tiles cost ~0.3 us per MB (stored,
-// then re-read by the reduce).  Splits keep >= 8 token steps each.  VSPIKE_DW_BM / _BN / _SPLITS /
+// then re-read by the reduce).  Splits keep >= 8 token steps each.  VS_KNOB_DW_BM / _BN / _SPLITS /
 // _STAGES force a choice (A/B runs, tests).
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   DwPlan best = {};
@@ -587,8 +582,8 @@ DwPlan plan_dw(int64_t M, int64_t N, int64_t K) {
   const bool swap = M > N;
   const int64_t Ma = swap ? N : M, Nb = swap ? M : N;
   const int64_t nk = (K + 63) / 64;
-  const int force_bm = env_int("VSPIKE_DW_BM", 0), force_bn = env_int("VSPIKE_DW_BN", 0);
-  const int force_s = env_int("VSPIKE_DW_SPLITS", 0), force_stg = env_int("VSPIKE_DW_STAGES", 0);
+  const int force_bm = knob(VS_KNOB_DW_BM), force_bn = knob(VS_KNOB_DW_BN);
+  const int force_s = knob(VS_KNOB_DW_SPLITS), force_stg = knob(VS_KNOB_DW_STAGES);
   double best_t = 1e30;
   for (int BN : {64, 128}) {
     if (force_bn && BN != force_bn) continue;

@@ -479,11 +479,8 @@ static int layernorm_bwd_t(int64_t rows, int64_t cols, const TD* dy, int64_t ldd
   if (lpr && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && (!dres || (lddres % 4 == 0 && aligned16(dres))) &&
       (((uintptr_t)dy) & (BF ? 7 : 15)) == 0 && aligned16(x) && aligned16(dx) && aligned16(gamma) &&
       (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {
-    static const int cap = [] {  // A/B knob: VSPIKE_LN_BLOCKS caps the grid (= partial rows) below 1024
-      const char* v = getenv("VSPIKE_LN_BLOCKS");
-      const int c = v ? atoi(v) : 0;
-      return c > 0 && c <= kLnBwdBlocks ? c : kLnBwdBlocks;
-    }();
+    const int kc = knob(VS_KNOB_LN_BLOCKS);  // A/B knob: caps the grid (= partial rows) below 1024
+    const int cap = kc > 0 && kc <= kLnBwdBlocks ? kc : kLnBwdBlocks;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), cap);
     float* part = (float*)workspace;
 #define BV_(L)                                                                                                       \

@@ -1,9 +1,15 @@
-// runtime.hip — error reporting, version, kernel timers (bench instrumentation).
+// runtime.hip — error reporting, version / build id, knobs, dispatch counters, kernel timers.
+#include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <string.h>
 #include <vector>
 
 #include "common.h"
+
+#ifndef VS_BUILD_ID
+#define VS_BUILD_ID "unknown"
+#endif
 
 namespace vs {
 
@@ -14,6 +20,40 @@ void set_error(const char* msg) {
   strncpy(g_err, msg, sizeof(g_err) - 1);
   g_err[sizeof(g_err) - 1] = 0;
 }
+
+// ---- knobs: environment read once (first use), then vs_knob_set overrides -------------------
+struct KnobDef {
+  const char* env;
+  int dflt;
+};
+static const KnobDef kKnobs[VS_KNOB_COUNT] = {
+    {"VSPIKE_DW_OLD", 0},      {"VSPIKE_NO_SKINNY", 0},    {"VSPIKE_NO_SLAB", 0},      {"VSPIKE_NO_BIG", 0},
+    {"VSPIKE_NO_WRES", 0},     {"VSPIKE_WRES_GBWD", 0},    {"VSPIKE_NO_WSLAB", 0},     {"VSPIKE_WSLAB", 0},
+    {"VSPIKE_WSLAB_G", 512},   {"VSPIKE_PANEL", 0},        {"VSPIKE_NO_PANEL", 0},     {"VSPIKE_PANEL_GRID", 512},
+    {"VSPIKE_NO_FULLK", 0},    {"VSPIKE_NO_RING", 0},      {"VSPIKE_NO_LNF_FUSE", 0},  {"VSPIKE_NO_LN_FUSE", 0},
+    {"VSPIKE_DW_BM", 0},       {"VSPIKE_DW_BN", 0},        {"VSPIKE_DW_SPLITS", 0},    {"VSPIKE_DW_STAGES", 0},
+    {"VSPIKE_LN_BLOCKS", 0},   {"VSPIKE_DH_F32", 0},       {"VSPIKE_NO_PATCH_FUSED", 0}, {"VSPIKE_NO_DW_GROUP", 0},
+    {"VSPIKE_ATTN_VARIANT", 0}, {nullptr, 0}, {nullptr, 0}, {nullptr, 0}, {nullptr, 0}, {nullptr, 0}, {nullptr, 0},
+    {nullptr, 0}};
+static std::atomic<int> g_knob[VS_KNOB_COUNT];
+static std::once_flag g_knob_once;
+static void knob_init() {
+  for (int i = 0; i < VS_KNOB_COUNT; ++i) {
+    int v = kKnobs[i].dflt;
+    if (kKnobs[i].env) {
+      const char* e = getenv(kKnobs[i].env);
+      if (e && e[0]) v = atoi(e);
+    }
+    g_knob[i].store(v, std::memory_order_relaxed);
+  }
+}
+int knob(int id) {
+  std::call_once(g_knob_once, knob_init);
+  return g_knob[id].load(std::memory_order_relaxed);
+}
+
+static std::atomic<int64_t> g_dispatch[VS_PATH_COUNT];
+void count_path(int id) { g_dispatch[id].fetch_add(1, std::memory_order_relaxed); }
 
 // Event pairs recorded around tracked launches while timing is enabled.  Events are pooled and
 // only read back in vs_timing_collect(), so recording never synchronises the stream.
@@ -51,7 +91,29 @@ ScopedTimer::~ScopedTimer() {
 
 }  // namespace vs
 
-extern "C" int vs_version(void) { return 3; }  // 2: vs_vit_layer_grad.flags; 3: .chain
+// 2: vs_vit_layer_grad.flags; 3: .chain; 4: bf16-mode a_pre holds gelu'(pre), d_h may be bf16,
+// knobs / dispatch counters / build id
+extern "C" int vs_version(void) { return 4; }
+extern "C" const char* vs_build_id(void) { return VS_BUILD_ID; }
+
+extern "C" int vs_knob_get(int k) {
+  VS_REQUIRE(k >= 0 && k < VS_KNOB_COUNT, "vs_knob_get: unknown knob");
+  return vs::knob(k);
+}
+extern "C" int vs_knob_set(int k, int value) {
+  VS_REQUIRE(k >= 0 && k < VS_KNOB_COUNT, "vs_knob_set: unknown knob");
+  const int prev = vs::knob(k);
+  vs::g_knob[k].store(value, std::memory_order_relaxed);
+  return prev;
+}
+extern "C" int vs_dispatch_counts(int64_t* out, int n) {
+  for (int i = 0; i < n && i < VS_PATH_COUNT; ++i) out[i] = vs::g_dispatch[i].load(std::memory_order_relaxed);
+  return VS_PATH_COUNT;
+}
+extern "C" int vs_dispatch_reset(void) {
+  for (auto& c : vs::g_dispatch) c.store(0, std::memory_order_relaxed);
+  return VS_OK;
+}
 
 extern "C" int vs_struct_size(int which) {
   switch (which) {

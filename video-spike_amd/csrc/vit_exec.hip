@@ -14,13 +14,7 @@
 
 namespace vs {
 
-static bool dh_f32() {
-  static const bool v = [] {
-    const char* e = getenv("VSPIKE_DH_F32");
-    return e && e[0] && e[0] != '0';
-  }();
-  return v;
-}
+static bool dh_f32() { return knob(VS_KNOB_DH_F32) != 0; }
 
 static vs_gemm_desc gdesc(int dtype, int out_dtype, bool akc, bool bkc, int64_t M, int64_t N, int64_t K, const void* a,
                           int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, uint32_t epi) {

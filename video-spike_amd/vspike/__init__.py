@@ -6,7 +6,7 @@ runs in libvspike.so (hand-written HIP, include/vspike.h) — there is no CPU fa
 """
 from .config import DictConfig, config_from_kwargs, load_run_config, update_config
 from .linear import Linear
-from .loss import PoissonNLLMeanLoss, poisson_nll_mean
+from .loss import MSEMeanLoss, PoissonNLLMeanLoss, make_criterion, mse_mean, poisson_nll_mean
 from .optim import FusedAdamW
 from .vit import VideoMAE
 
@@ -16,4 +16,5 @@ NAME2MODEL = {
 }
 
 __all__ = ["NAME2MODEL", "Linear", "VideoMAE", "FusedAdamW", "poisson_nll_mean", "PoissonNLLMeanLoss",
+           "mse_mean", "MSEMeanLoss", "make_criterion",
            "DictConfig", "update_config", "config_from_kwargs", "load_run_config"]

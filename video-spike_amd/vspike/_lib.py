@@ -26,6 +26,16 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
                "fwd_qkv", "fwd_proj", "fwd_fc1", "fwd_fc2", "dx_fc2", "dx_fc1", "dx_proj", "dx_qkv",
                "dw_fc2", "dw_fc1", "dw_proj", "dw_qkv")
 
+# vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
+PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
+              "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
+              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped")
+PATH_COUNT = 24
+KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
+              "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
+              "dw_splits", "dw_stages", "ln_blocks", "dh_f32", "no_patch_fused", "no_dw_group", "attn_variant")
+KNOB_COUNT = 32
+
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_size_t)
 
@@ -69,6 +79,13 @@ class VitLayerGrad(ctypes.Structure):
 # every entry point of include/vspike.h: name -> (restype, argtypes)
 PROTOTYPES = {
     "vs_version": (ctypes.c_int, []),
+    "vs_build_id": (ctypes.c_char_p, []),
+    "vs_dispatch_counts": (ctypes.c_int, [ctypes.POINTER(c_i64), ctypes.c_int]),
+    "vs_dispatch_reset": (ctypes.c_int, []),
+    "vs_knob_get": (ctypes.c_int, [ctypes.c_int]),
+    "vs_knob_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "vs_mse_loss": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_f32, c_p, c_p]),
+    "vs_mse_loss_bwd": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_last_error": (ctypes.c_char_p, []),
     "vs_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     "vs_struct_size": (ctypes.c_int, [ctypes.c_int]),
@@ -188,3 +205,43 @@ class BwdChain:
             self.close()
         except Exception:
             pass
+
+
+def build_id() -> str:
+    """vs_build_id() of the loaded library: the source hash it was compiled from (vspike.build.source_hash)."""
+    return lib().vs_build_id().decode()
+
+
+def dispatch_counts() -> dict:
+    """Launches per kernel path since the last dispatch_reset() (vspike.h VS_PATH_*)."""
+    buf = (c_i64 * PATH_COUNT)()
+    lib().vs_dispatch_counts(buf, PATH_COUNT)
+    return {name: int(buf[i]) for i, name in enumerate(PATH_NAMES)}
+
+
+def dispatch_reset() -> None:
+    lib().vs_dispatch_reset()
+
+
+def knob_get(name: str) -> int:
+    return int(lib().vs_knob_get(KNOB_NAMES.index(name)))
+
+
+def knob_set(name: str, value: int) -> int:
+    """Override an A/B knob (vspike.h VS_KNOB_*); returns the previous value."""
+    return int(lib().vs_knob_set(KNOB_NAMES.index(name), int(value)))
+
+
+class knob:
+    """Context manager: `with knob("no_wres", 1): ...` selects a kernel path for the block."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value, self.prev = name, int(value), None
+
+    def __enter__(self):
+        self.prev = knob_set(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        knob_set(self.name, self.prev)
+        return False

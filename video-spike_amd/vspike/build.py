@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -33,6 +34,27 @@ def _flags():
             "-Wno-unused-result", "-munsafe-fp-atomics"]
 
 
+def _sources():
+    srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip"))) + sorted(glob.glob(os.path.join(SRC_DIR, "*.cpp")))
+    headers = sorted(glob.glob(os.path.join(SRC_DIR, "*.h"))) + [os.path.join(INCLUDE, "vspike.h")]
+    return srcs, headers
+
+
+def source_hash(defines=()) -> str:
+    """sha256 prefix over every source and header the library is compiled from (by file name and
+    content, in name order) plus the target and any extra -D defines: the id `vs_build_id()` of a
+    library built from exactly these sources returns."""
+    h = hashlib.sha256()
+    srcs, headers = _sources()
+    for f in sorted(srcs + headers, key=os.path.basename):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(("|".join([ARCH] + sorted(defines))).encode())
+    return h.hexdigest()[:16]
+
+
 def _needs(obj: str, deps) -> bool:
     if not os.path.exists(obj):
         return True
@@ -48,13 +70,16 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8, variant: str
     os.makedirs(obj_dir, exist_ok=True)
     hipcc = _hipcc()
     dflags = [f"-D{d}" for d in defines]
-    srcs = sorted(glob.glob(os.path.join(SRC_DIR, "*.hip"))) + sorted(glob.glob(os.path.join(SRC_DIR, "*.cpp")))
-    headers = sorted(glob.glob(os.path.join(SRC_DIR, "*.h"))) + [os.path.join(INCLUDE, "vspike.h")]
+    srcs, headers = _sources()
+    bid = source_hash(defines)
+    stamp = os.path.join(obj_dir, "build_id")
+    old_bid = open(stamp).read().strip() if os.path.exists(stamp) else ""
     objs, todo = [], []
     for s in srcs:
         o = os.path.join(obj_dir, os.path.splitext(os.path.basename(s))[0] + ".o")
         objs.append(o)
-        if force or _needs(o, [s] + headers):
+        # runtime.hip carries the build id: recompiled whenever any source changed
+        if force or _needs(o, [s] + headers) or (os.path.basename(s) == "runtime.hip" and old_bid != bid):
             todo.append((s, o))
 
     def compile_one(so):
@@ -63,6 +88,8 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8, variant: str
             cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-I", INCLUDE, "-c", s, "-o", o]
         else:
             cmd = [hipcc, *_flags(), *dflags, "-c", s, "-o", o]
+            if os.path.basename(s) == "runtime.hip":
+                cmd.insert(-4, f'-DVS_BUILD_ID="{bid}"')
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed for {os.path.basename(s)}:\n{r.stderr[-6000:]}")
@@ -79,7 +106,9 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8, variant: str
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
         if verbose:
-            print(f"[vspike.build] linked {lib_path}", file=sys.stderr)
+            print(f"[vspike.build] linked {lib_path} (build id {bid})", file=sys.stderr)
+    with open(stamp, "w") as fh:
+        fh.write(bid + "\n")
     return lib_path
 
 

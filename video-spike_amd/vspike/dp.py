@@ -30,30 +30,61 @@ import torch.distributed as dist
 
 
 class GradExchange:
-    def __init__(self, model: torch.nn.Module, bucket_mb: float = 8.0, group=None, return_grads: bool = False):
+    def __init__(self, model: torch.nn.Module, bucket_mb: float = 8.0, group=None, return_grads: bool = False,
+                 ddp=None):
         """return_grads: the model's autograd Function hands the (being-reduced) sink buffers back
         to autograd as the gradients instead of installing them as `.grad` itself — the mode DDP
-        needs (its reducer fires on those gradients, `attach_ddp`)."""
+        needs (its reducer fires on those gradients, `attach_ddp`).  ddp: that DDP wrapper, whose
+        `no_sync()` state the sink follows (gradient accumulation, see `_mode`)."""
         self.model = model
         self.group = group
         self.return_grads = return_grads
+        self.ddp = ddp
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
         self._buffers: Dict[int, torch.Tensor] = {}
         self._pending: Dict[int, List[Tuple[int, int]]] = {}
         self._works = []
         self._sunk = set()
+        self._accumulating = False      # a no_sync micro-step ran since the last synchronised step
+        self._passthrough = set()       # ids whose gradient of this step DDP reduces itself
         if self.world > 1:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
-                    dist.broadcast(t.detach(), src=src, group=group)   # versioned write (bf16 shadows recast)
+                    dist.broadcast(t.detach(), src=src, group=group)
+        # a collective's write does not bump a tensor's version: re-cast low-precision weight
+        # shadows explicitly instead of trusting the version counter
+        if hasattr(model, "invalidate_lp"):
+            model.invalidate_lp()
         if hasattr(model, "grad_sink"):
             model.grad_sink = self
             self._sunk = {id(model.enc_flat), id(model.head_flat)} if hasattr(model, "enc_flat") else set()
 
+    def _mode(self) -> str:
+        """'overlap' (launch bucketed all-reduces during the backward), 'local' (DDP no_sync
+        micro-step: plain local gradients, no collective) or 'passthrough' (the synchronised step
+        that closes an accumulation window: DDP's bucket holds the ACCUMULATED local gradients, so
+        DDP's own all-reduce handles this step and nothing is launched early)."""
+        if self.ddp is None or self.world == 1:
+            return "overlap"
+        if not self.ddp.require_backward_grad_sync:
+            self._accumulating = True
+            return "local"
+        return "passthrough" if self._accumulating else "overlap"
+
     # ---- sink protocol (called from the model's backward) ---------------------------------------
     def grad_buffer(self, p: torch.Tensor) -> torch.Tensor:
+        mode = self._mode()
+        if mode != "overlap":
+            if mode == "passthrough":
+                self._passthrough.add(id(p))
+            buf = torch.zeros_like(p)
+            if not self.return_grads:
+                p.grad = buf
+            self._pending[id(p)] = None
+            return buf
+        self._passthrough.discard(id(p))
         buf = self._buffers.get(id(p))
         if buf is None or buf.device != p.device:
             buf = torch.zeros_like(p)
@@ -66,12 +97,15 @@ class GradExchange:
         return buf
 
     def reduced(self, p: torch.Tensor):
-        """The all-reduced (summed) gradient buffer of a sink parameter, or None."""
+        """The all-reduced (summed) gradient buffer of a sink parameter, or None (also when DDP
+        reduces this step's gradient itself: the step after no_sync micro-steps)."""
+        if id(p) in self._passthrough:
+            return None
         return self._buffers.get(id(p))
 
     def mark_ready(self, p: torch.Tensor, lo: int, hi: int) -> None:
-        if self.world == 1 or hi <= lo:
-            return
+        if self.world == 1 or hi <= lo or self._pending.get(id(p), []) is None:
+            return            # local / passthrough step: no early collective
         pend = self._pending.setdefault(id(p), [])
         pend.append((lo, hi))
         pend.sort()
@@ -98,6 +132,8 @@ class GradExchange:
         """Flush partial buckets, reduce the non-sink gradients, and make the current stream wait."""
         if self.world > 1:
             for pid, spans in self._pending.items():
+                if spans is None:
+                    continue
                 for a, b in spans:
                     self._launch(self._buffers[pid][a:b])
                 spans.clear()
@@ -133,6 +169,8 @@ def _overlap_hook(exchange: "GradExchange", bucket):
     import torch.distributed.algorithms.ddp_comm_hooks.default_hooks as dh
     params = bucket.parameters()
     if not all(exchange.reduced(p) is not None for p in params):
+        if any(id(p) in exchange._passthrough for p in params):
+            exchange._accumulating = False      # this synchronised step closes the no_sync window
         return dh.allreduce_hook(exchange.group, bucket)
     exchange.finish()                      # this step's early all-reduces have landed (stream order)
     buf = bucket.buffer()
@@ -149,9 +187,12 @@ def _overlap_hook(exchange: "GradExchange", bucket):
 def attach_ddp(ddp_model, bucket_mb: float = 8.0) -> "GradExchange":
     """Overlap the gradient all-reduce with the backward for a DDP-wrapped vspike plugin (e.g. the
     module `accelerator.prepare` returned).  Returns the exchange; nothing else changes in the
-    caller: DDP still averages, the optimizer keeps grad_scale 1."""
+    caller: DDP still averages, the optimizer keeps grad_scale 1.  Gradient accumulation with
+    `ddp_model.no_sync()` keeps DDP's semantics: no_sync micro-steps produce local gradients only,
+    and the synchronised step that follows is reduced by DDP itself (from the accumulated
+    gradients, without the early overlap); steps with no accumulation overlap as usual."""
     module = ddp_model.module
-    ex = GradExchange(module, bucket_mb=bucket_mb, group=ddp_model.process_group, return_grads=True)
+    ex = GradExchange(module, bucket_mb=bucket_mb, group=ddp_model.process_group, return_grads=True, ddp=ddp_model)
     if hasattr(module, "grad_sink"):
         module.grad_sink = ex
     ddp_model.register_comm_hook(ex, _overlap_hook)

@@ -226,6 +226,24 @@ def poisson_nll_bwd(log_rate, target, grad_out, dx):
     return dx
 
 
+def mse_loss(pred, target, loss_out, dx=None, grad_scale=1.0, workspace=None):
+    """mean((pred - target)^2) into loss_out (device scalar); dx = grad_scale * 2 (pred - target) / n."""
+    require_device(pred, target, loss_out)
+    n = pred.numel()
+    if workspace is None:
+        workspace = torch.empty(int(lib().vs_poisson_workspace_bytes(n)) // 4, dtype=torch.float32, device=pred.device)
+    check(lib().vs_mse_loss(n, pred.data_ptr(), target.data_ptr(), loss_out.data_ptr(), ptr(dx), grad_scale,
+                            workspace.data_ptr(), stream()), "vs_mse_loss")
+    return loss_out
+
+
+def mse_loss_bwd(pred, target, grad_out, dx):
+    require_device(pred, target, grad_out, dx)
+    check(lib().vs_mse_loss_bwd(pred.numel(), pred.data_ptr(), target.data_ptr(), grad_out.data_ptr(), dx.data_ptr(),
+                                stream()), "vs_mse_loss_bwd")
+    return dx
+
+
 def adamw(param, grad, exp_avg, exp_avg_sq, hyper, param_lp=None):
     require_device(param, grad, exp_avg, exp_avg_sq, hyper)
     check(lib().vs_adamw(param.numel(), param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),

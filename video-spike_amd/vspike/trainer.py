@@ -14,7 +14,7 @@ from typing import Iterable, List, Optional
 import torch
 
 from .dp import GradExchange
-from .loss import poisson_nll_mean
+from .loss import make_criterion
 from .metrics import eval_session
 from .optim import FusedAdamW
 
@@ -44,10 +44,13 @@ def build_optimizer(model, config, total_steps: int, world: int = 1):
 
 
 class Trainer:
-    def __init__(self, model, optimizer, lr_scheduler=None, config=None, criterion=poisson_nll_mean,
+    def __init__(self, model, optimizer, lr_scheduler=None, config=None, criterion=None,
                  exchange: Optional[GradExchange] = None):
+        """criterion: default = the config's `training.loss` (make_criterion: "poisson", the
+        reference's PoissonNLL of src/train.py:59, or "mse")."""
         self.model, self.optimizer, self.lr_scheduler = model, optimizer, lr_scheduler
-        self.config, self.criterion, self.exchange = config, criterion, exchange
+        self.config, self.exchange = config, exchange
+        self.criterion = criterion if criterion is not None else make_criterion(config)
 
     def step(self, inputs, target) -> torch.Tensor:
         outputs = self.model(inputs)
