@@ -317,6 +317,24 @@ int vs_bwd_chain_create(void** chain);   /* on the current device */
 int vs_bwd_chain_destroy(void* chain);
 
 /* ------------------------------------------------------------------------------------------
+ * Data-parallel gradient exchange over RCCL (xGMI), for hosts that do not run torch.distributed:
+ * replaces the implicit DDP all-reduce of accelerate (src/train.py:61-64 `accelerator.prepare`,
+ * src/trainer/base.py:150 `accelerator.backward`).  One communicator per process / GPU: rank 0
+ * makes an id (vs_comm_unique_id), the host ships its VS_COMM_ID_BYTES to every rank (any
+ * channel), each rank calls vs_comm_init on its device.  vs_comm_allreduce_bucket sums one gradient
+ * bucket in place across ranks, enqueued on the caller's stream (call it as each bucket's backward
+ * products finish: the collective overlaps the rest of the backward); fold 1/world into vs_adamw's
+ * grad_scale.  RCCL failures return VS_COMM_ERR_BASE + ncclResult_t.  The Python host uses
+ * torch.distributed (backend "nccl" = RCCL) through vspike/dp.py with the same bucketing.
+ * ------------------------------------------------------------------------------------------ */
+#define VS_COMM_ID_BYTES 128
+#define VS_COMM_ERR_BASE 1000
+int vs_comm_unique_id(void* id_out /* VS_COMM_ID_BYTES */);
+int vs_comm_init(void** comm, const void* id, int32_t world, int32_t rank);
+int vs_comm_allreduce_bucket(void* comm, void* buf, int64_t count, int32_t dtype, void* stream);
+int vs_comm_finalize(void* comm);
+
+/* ------------------------------------------------------------------------------------------
  * Trial shards (host side of the input path; replaces the per-trial webdataset tars of
  * src/prepare_data.py:210-235 read by src/loader/base.py:21-41).  Fixed-size records: raw uint8
  * frames (T, C, H, W) + f32 spike counts (ap_rows, ap_cols) + a 64-byte "<eid>_<trial>" key.

@@ -49,12 +49,13 @@ def main():
     ap.add_argument("--only", default="", help="gemm|attn|ln, or gemm:<name substring> for one GEMM")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--heads", type=int, default=3, help="attention heads (3: C2 ViT-Tiny, 12: C3 ViT-Base)")
     a = ap.parse_args()
     global SELECT
     if a.only.startswith("gemm:"):
         a.only, SELECT = "gemm", a.only[5:]
     dev = "cuda"
-    B, N, D, F, H = a.batch, 1568, 192, 768, 3
+    B, N, D, F, H = a.batch, 1568, 192, 768, a.heads
     M = B * N
     bf = torch.bfloat16
     r = lambda *s, dt=bf: (torch.randn(*s, device=dev) * 0.5).to(dt)  # noqa: E731
@@ -142,16 +143,23 @@ def main():
         report("copy 38.5 MB -> 38.5 MB (torch)", timeit(lambda: dst.copy_(src), a.reps), 2 * M * F * 2, 0)
         report("fill 77 MB (torch zero_)", timeit(lambda: big.zero_(), a.reps), 2 * M * F * 2, 0)
     if a.only in ("", "attn"):
-        qkv = r(M, 3 * D, dt=bf) * 3
-        o = torch.empty(M, D, dtype=bf, device=dev)
+        Da = H * 64
+        qkv = r(M, 3 * Da, dt=bf) * 3
+        o = torch.empty(M, Da, dtype=bf, device=dev)
         lse = torch.empty(B, H, N, device=dev)
-        do = r(M, D)
-        dq = torch.empty(M, 3 * D, dtype=bf, device=dev)
+        do = r(M, Da)
+        dq = torch.empty(M, 3 * Da, dtype=bf, device=dev)
         ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=dev)
         f = 4.0 * B * H * N * N * 64
-        report("attn fwd", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps), M * 4 * D * 2, f)
-        report("attn bwd (delta+dkdv+dq)", timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps),
-               M * 8 * D * 2, 2.5 * f)
+        for v in (0, 1, 2, 3):        # VS_KNOB_ATTN_VARIANT: bit 0 forward kernel, bit 1 backward kernel
+            with L.knob("attn_variant", v):
+                if v in (0, 1):
+                    report(f"attn fwd [variant {v}]", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps),
+                           M * 4 * Da * 2, f)
+                if v in (0, 2):
+                    report(f"attn bwd (delta+dkdv+dq) [variant {v}]",
+                           timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps), M * 8 * Da * 2,
+                           2.5 * f)
     if a.only in ("", "linear"):
         # Linear plugin first layer at the real linear_video geometry (K = 120*128*128), f32, B = 4
         Bn, K, Nout = 4, 120 * 128 * 128, 256

@@ -197,3 +197,19 @@ def test_bench_gpus_2_launches_two_ranks_in_sync():
     print("\n", {k: line[k] for k in ("n_gpus", "value", "ms_per_step", "replicas_equal", "backend")})
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 4 and line["config"]["parallelism"] == "dp2"
     assert line["replicas_equal"] is True and line["value"] > 0
+
+
+def test_rccl_comm_c_abi_single_rank():
+    """vs_comm_* (the C-ABI exchange for non-Python hosts): one rank on this box's GPU — id, init,
+    the in-place bucket all-reduce on the current stream (a sum over one rank is the identity,
+    f32 and bf16, a 0-length bucket is a no-op), finalize."""
+    from vspike.comm import RcclComm
+    comm = RcclComm(1, 0, RcclComm.unique_id())
+    for dt in (torch.float32, torch.bfloat16):
+        t = torch.randn(1 << 20, device=DEV).to(dt)
+        ref = t.clone()
+        comm.allreduce_(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, ref)
+    comm.allreduce_(torch.empty(0, device=DEV))
+    comm.close()

@@ -595,6 +595,30 @@ def _attn_ref(qkv, B, N, H, scale=0.125):
 ATTN_SHAPES = [(1, 100, 1), (2, 196, 2), (1, 1568, 3), (2, 130, 1)]
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1)])
+def test_attention_fwd_variants(knobs, variant, shape):
+    """Both bf16 forward kernels (VS_KNOB_ATTN_VARIANT bit 0: 0 = 3 waves/SIMD x 32 rows, 1 = one
+    wave per SIMD x 96 rows, 3-stage K/V ring) against fp64 on the same bf16 inputs, at tails of
+    every kind: N = 1 / 33 / 100 / 130 / 196 (partial 32-key block), 1568 (= 4 x 384 + 32: a
+    workgroup with one live q-block), 1600 (partial 64-key tile), 3136 (C5: 98 blocks)."""
+    from vspike import ops
+    knobs("attn_variant", variant)
+    B, N, H = shape
+    D = H * 64
+    qkv = _rand(B * N, 3 * D, seed=24, scale=1.5).to(torch.bfloat16)
+    o = torch.full((B * N, D), 7.0, dtype=torch.bfloat16, device=DEV)
+    lse = torch.full((B, H, N), 7.0, device=DEV)
+    ops.attn_fwd(qkv.to(DEV), o, lse, B, N, H)
+    torch.cuda.synchronize()
+    o_ref, lse_ref = _attn_ref(qkv.double(), B, N, H)
+    assert rel(o.float(), o_ref) < 1.5e-2
+    assert rel(lse, lse_ref) < 3e-3
+    per = ((o.float().double() - o_ref).view(B, N, H, 64).norm(dim=(1, 3)) /
+           o_ref.view(B, N, H, 64).norm(dim=(1, 3)))
+    assert float(per.max()) < 3e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", ATTN_SHAPES)
 def test_attention_fwd_bwd(dtype, shape):
@@ -641,9 +665,11 @@ def test_attention_bf16_matches_f32_kernel_on_same_inputs():
     assert rel(l16, l32) < 3e-3
 
 
-def test_attention_rescale_branch_forced():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_attention_rescale_branch_forced(knobs, variant):
     """A huge score late in the sequence forces the online-softmax rescale (guide rule 26)."""
     from vspike import ops
+    knobs("attn_variant", variant)
     B, N, H = 1, 700, 1
     qkv = _rand(N, 192, seed=40, scale=0.5)
     qkv[600, 64:128] = qkv[5, 0:64] * 40.0            # key 600 dominates query 5
@@ -657,11 +683,13 @@ def test_attention_rescale_branch_forced():
 
 
 @pytest.mark.gpu
-def test_attention_extreme_logits_move_reference():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_attention_extreme_logits_move_reference(knobs, variant):
     """Queries whose scores all lie far below / above 0 force the forward's softmax reference off
     its default 0 on the first block (m < -32 or > 32 in log2 units), then a late larger score
     moves it again; the rest of the wave stays on the unshifted fast path."""
     from vspike import ops
+    knobs("attn_variant", variant)
     B, N, H = 1, 900, 1
     qkv = _rand(N, 192, seed=41, scale=0.3)
     u = torch.ones(64) / 8.0

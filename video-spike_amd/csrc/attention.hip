@@ -663,6 +663,320 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 #endif
 }
 
+// ------------------------------------------------------------------ forward, one wave per SIMD
+// Workgroup = 4 waves = 4 x NQB x 32 query rows of one (batch, head); one workgroup per CU (the
+// whole register file per wave).  Each wave carries NQB independent 32-row query blocks through
+// the same K/V stream, so every K / V^T fragment it reads from LDS feeds NQB MFMAs, and the
+// softmax VALU of one 32-key block runs under the next block's QK^T MFMAs (software pipeline:
+// S(i+1) = QK(K(i+1)) is issued before softmax(S(i)), then O += PV(V(i), P(i))).  At C2 (B*H = 48
+// heads x 1568 queries) NQB = 3 gives 240 workgroups for 256 CUs: one round, 96 rows per SIMD
+// (the 32-row granularity of the problem allows no fewer than 73.5 on 1024 SIMDs).  K/V arrive by
+// LDS-DMA into a 3-stage ring of 64-key tiles issued two tiles ahead, one barrier per tile.
+// Numerics and the two passes (fast: p = exp2(s) against a fixed reference, row sums on the matrix
+// pipe; safe: online softmax, re-run when a row sum leaves [2^-60, 2^60]) as attn_fwd_bf16_kernel.
+template <int NQB>
+__global__ __launch_bounds__(256, 1) void attn_fwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                  bf16_t* __restrict__ o, int64_t ldo,
+                                                                  float* __restrict__ lse, int N, int H,
+                                                                  float scale_log2) {
+  constexpr int TILE = 64 * 128;      // bytes of one 64-key x 64-dh bf16 image
+  constexpr int STAGE = 2 * TILE;     // K image + V image
+  constexpr int NSTG = 3;
+  constexpr int ROWS = 4 * NQB * 32;  // query rows per workgroup
+  __shared__ __attribute__((aligned(16))) char smem[NSTG * STAGE];
+  __shared__ int redo_flag;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (N + ROWS - 1) / ROWS, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nqb;
+  const int h = (blk / nqb) % H, b = blk / nqb / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const int q0w = qb * ROWS + wid * NQB * 32;  // this wave's first query
+  const float c = scale_log2;
+  if (tid == 0) redo_flag = 0;
+
+  // Q fragments (B operand of S^T = K Q^T), pre-scaled by c; rows past N re-read row N-1
+  bf16x8 qf[NQB][4];
+#pragma unroll
+  for (int q = 0; q < NQB; ++q)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int qi = q0w + q * 32 + (lane & 31);
+      const int qr = qi < N ? qi : N - 1;
+      const bf16x8 x = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)x[j] * c;
+      qf[q][s] = __builtin_convertvector(v, bf16x8);
+    }
+  const bf16x8 sel = rowsum_selector(lane);
+  f32x16 oacc[NQB][2];
+  f32x4 lacc[NQB];
+  float m_run[NQB], l_half[NQB];
+
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
+  int kbase[4];
+  {
+    const int key = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kbase[s] = key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4);
+  }
+  int vbase[2];
+  {
+    const int k0 = 4 * hh + q4;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) vbase[dt] = TILE + off_halfswz(k0, dt * 32 + g16 + p4);
+  }
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  // DMA of one 64-key tile into stage `st`: wave w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1
+  // (8 rows x 128 B each, lane L loading the source chunk that belongs at position L & 7)
+  auto load_tile = [&](int kt, int st) {
+    const int prow0 = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const char* kb = (const char*)Kp + kt * tile_bytes;
+    const char* vb = kb + vdelta;
+    char* dk = smem + st * STAGE + wid * 2048;
+    char* dv = dk + TILE;
+    int r0 = prow0, r1 = prow0 + 8;
+    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (their scores are masked)
+      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
+      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
+    }
+    const uint32_t o0 = (uint32_t)r0 * (uint32_t)(2 * ldq), o1 = (uint32_t)r1 * (uint32_t)(2 * ldq);
+    glds16_asm_so(kb, o0 + ((ppos ^ swz_row(prow0)) << 4), dk);
+    glds16_asm_so(kb, o1 + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
+    glds16_asm_so(vb, o0 + ((ppos ^ swz_half(prow0)) << 4), dv);
+    glds16_asm_so(vb, o1 + ((ppos ^ swz_half(prow0 + 8)) << 4), dv + 1024);
+  };
+  struct KFrag {
+    bf16x8 k[4];
+  };
+  struct VFrag {
+    bf16x8 v[4];
+  };
+  auto kread = [&](int st, int kb) {
+    KFrag f;
+    const char* base = smem + st * STAGE + kb * 4096;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f.k[s] = *(const bf16x8*)(base + kbase[s]);
+    return f;
+  };
+  auto vread = [&](int st, int kb) {
+    VFrag f;
+    const char* base = smem + st * STAGE + kb * 4096;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) f.v[2 * s + dt] = tr_pair(base + s * 2048, vbase[dt], vbase[dt] + 1024);
+    return f;
+  };
+  auto qk = [&](const KFrag& k, f32x16 (&sacc)[NQB]) {
+#pragma unroll
+    for (int q = 0; q < NQB; ++q) {
+      f32x16 z;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) z[r] = 0.f;
+      sacc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k.k[0], qf[q][0], z, 0, 0, 0);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) sacc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k.k[s], qf[q][s], sacc[q], 0, 0, 0);
+    }
+  };
+  // wave-uniform barrier helpers with an immediate vmcnt (LDS-DMA pieces of younger tiles may stay
+  // in flight: 4 pieces per wave per tile)
+  auto wait_tile = [&](int younger_tiles) {
+    if (younger_tiles >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger_tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  const int ntile = (N + 63) / 64, nblk = (N + 31) / 32;
+  auto pass = [&](auto safec) {
+    constexpr bool SAFE = decltype(safec)::value;
+#pragma unroll
+    for (int q = 0; q < NQB; ++q) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        oacc[q][0][r] = 0.f;
+        oacc[q][1][r] = 0.f;
+      }
+      lacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      m_run[q] = 0.f;
+      l_half[q] = 0.f;
+    }
+    for (int t = 0; t < NSTG && t < ntile; ++t) load_tile(t, t);
+    wait_tile(ntile - 1 < 2 ? ntile - 1 : 2);
+    f32x16 sc[NQB];  // scores of the current 32-key block, replaced in place by the next block's
+    VFrag vA = vread(0, 0), vB;
+    {
+      const KFrag k0 = kread(0, 0);
+      qk(k0, sc);
+    }
+    // one 32-key block i, per q-block q: softmax(S(i, q)) -> P(i, q), then S(i+1, q) = QK(K(i+1), q)
+    // into the same registers (its MFMAs run under the next q-block's softmax VALU); then
+    // O += PV(V(i), P(i)), under which the next block's first softmax can issue.
+    // NEXT: a block i+1 exists.  OPEN: block i+1 opens tile tn (wait for it, DMA tile tn + 2 into
+    // tile tn - 1's stage; placed after the first softmax so the barrier overlaps the MFMAs in
+    // flight).  MASK: keys past N in this block.  Compile-time flags: one basic block per variant.
+    // stc: the LDS stage of block i+1's tile, ((i+1)/2) % NSTG — an IC<> in the unrolled main loop
+    // (every LDS address is then a lane base plus an immediate), a plain int in the remainder.
+    auto body = [&](int i, const VFrag& vcur, VFrag& vnxt, auto nextc, auto openc, auto maskc, auto stc) {
+      constexpr bool NEXT = decltype(nextc)::value, OPEN = decltype(openc)::value, MASK = decltype(maskc)::value;
+      const int tn = (i + 1) >> 1, hn = (i + 1) & 1;
+      const int stn = (int)stc;
+      const int key0 = i * 32;
+      bf16x8 pa[NQB], pb[NQB];
+      KFrag kf;
+#pragma unroll
+      for (int q = 0; q < NQB; ++q) {
+        f32x16& acc = sc[q];
+        if constexpr (MASK) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
+        }
+        float p[16];
+        if constexpr (!SAFE) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r]);
+        } else {
+          const float mx = max16(acc);
+          if (__any(i == 0 || mx > m_run[q] + kRefBand)) {
+            const float mxp = pair_max(mx);
+            const bool move = i == 0 || mxp > m_run[q] + kRefBand;
+            const float m_new = move ? mxp : m_run[q];
+            const float alpha = i == 0 ? 1.f : __builtin_amdgcn_exp2f(m_run[q] - m_new);
+            m_run[q] = m_new;
+            l_half[q] *= alpha;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              oacc[q][0][r] *= alpha;
+              oacc[q][1][r] *= alpha;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r] - m_run[q]);
+          l_half[q] += ((((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) +
+                        (((p[8] + p[9]) + (p[10] + p[11])) + ((p[12] + p[13]) + (p[14] + p[15]))));
+        }
+        pa[q] = pack8f(p);
+        pb[q] = pack8f(p + 8);
+        if constexpr (!SAFE) {
+          lacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pa[q], lacc[q], 0, 0, 0);
+          lacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb[q], lacc[q], 0, 0, 0);
+        }
+        if constexpr (NEXT) {
+          if (q == 0) {
+            if constexpr (OPEN) {
+              wait_tile(tn + 1 < ntile ? 1 : 0);
+              if (tn + 2 < ntile) load_tile(tn + 2, stn == 0 ? 2 : stn - 1);
+            }
+            kf = kread(stn, hn);
+          }
+          f32x16 z;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) z[r] = 0.f;
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf.k[0], qf[q][0], z, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf.k[s], qf[q][s], acc, 0, 0, 0);
+        }
+      }
+      if constexpr (NEXT) vnxt = vread(stn, hn);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int q = 0; q < NQB; ++q)
+            oacc[q][dt] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vcur.v[2 * s + dt], s == 0 ? pa[q] : pb[q], oacc[q][dt], 0, 0, 0);
+    };
+    // main loop: 6 blocks = 3 tiles per iteration, so block i+1's stage is static: blocks 6m+k have
+    // their next block in tile 3m + (k+1)/2 (stage (k+1)/2 % 3); k odd opens that tile
+    const bool tail_mask = (N & 31) != 0;
+    int i = 0;
+    for (; i + 6 < nblk; i += 6) {
+      body(i, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<0>{});
+      body(i + 1, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<1>{});
+      body(i + 2, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<1>{});
+      body(i + 3, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<2>{});
+      body(i + 4, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<2>{});
+      body(i + 5, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<0>{});
+    }
+    // remainder (1..6 blocks): dynamic stage; V alternates with the block parity (i is even here)
+    for (; i < nblk; ++i) {
+      const VFrag& vc = (i & 1) ? vB : vA;
+      VFrag& vn = (i & 1) ? vA : vB;
+      const int stn = ((i + 1) >> 1) % NSTG;
+      if (i + 1 < nblk) {
+        if (((i + 1) & 1) == 0) body(i, vc, vn, IC<1>{}, IC<1>{}, IC<0>{}, stn);
+        else body(i, vc, vn, IC<1>{}, IC<0>{}, IC<0>{}, stn);
+      } else if (tail_mask) {
+        body(i, vc, vn, IC<0>{}, IC<0>{}, IC<1>{}, stn);
+      } else {
+        body(i, vc, vn, IC<0>{}, IC<0>{}, IC<0>{}, stn);
+      }
+    }
+  };
+
+  pass(IC<0>{});
+  // row sum of this lane's query (lane & 31) per q-block: row (q >> 4) of lacc in lane (q & 15)
+  float l[NQB];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < NQB; ++q) {
+    const int qq = lane & 31, src = (qq & 15) << 2;
+    float l0, l1;
+    asm volatile(
+        "ds_bpermute_b32 %0, %2, %3\n\t"
+        "ds_bpermute_b32 %1, %2, %4\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(l0), "=&v"(l1)
+        : "v"(src), "v"(lacc[q][0]), "v"(lacc[q][1])
+        : "memory");
+    l[q] = qq < 16 ? l0 : l1;
+    const int qi = q0w + q * 32 + qq;
+    bad |= qi < N && !(l[q] >= 0x1p-60f && l[q] <= 0x1p60f);
+  }
+  __syncthreads();  // every wave is done with the last K/V tile; redo_flag = 0 is visible
+  if (__any(bad) && lane == 0) redo_flag = 1;
+  __syncthreads();
+  if (redo_flag) {  // workgroup-uniform: the whole workgroup streams K/V again, safe softmax
+    pass(IC<1>{});
+#pragma unroll
+    for (int q = 0; q < NQB; ++q) l[q] = pair_sum(l_half[q]);
+    __syncthreads();
+  }
+
+  // Epilogue: O^T accumulators -> normalised bf16 rows staged through LDS (wave-private, XOR-
+  // swizzled 16-B chunks), then whole 128-B rows (8 lanes per row)
+  char* so = smem + wid * (NQB * 4096);
+  const int oq = lane & 31;
+#pragma unroll
+  for (int q = 0; q < NQB; ++q) {
+    const float inv = 1.f / l[q];
+    const int r = q * 32 + oq;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int chunk = dt * 4 + g;
+        *(uint2*)(so + r * 128 + ((chunk ^ (r & 7)) << 4) + 8 * hh) =
+            pack4(oacc[q][dt][4 * g] * inv, oacc[q][dt][4 * g + 1] * inv, oacc[q][dt][4 * g + 2] * inv,
+                  oacc[q][dt][4 * g + 3] * inv);
+      }
+    const int qi = q0w + r;
+    if (hh == 0 && qi < N) lse[((int64_t)b * H + h) * N + qi] = (m_run[q] + __log2f(l[q])) * kLn2;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed (wave-private)
+#pragma unroll
+  for (int pss = 0; pss < 4 * NQB; ++pss) {
+    const int r = pss * 8 + (lane >> 3), ch = lane & 7;
+    const uint4 v = *(const uint4*)(so + r * 128 + ((ch ^ (r & 7)) << 4));
+    if (q0w + r < N) *(uint4*)(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8) = v;
+  }
+}
+
 // ------------------------------------------------------------------ backward: row constants
 // Per (batch, head, query): nlse2 = -LSE * log2(e) and ndel = -delta (delta = rowsum(dO * O)),
 // stored [B*H][Npad] with Npad = N rounded up to 64 and the padding set to (-inf, 0): the dK/dV
@@ -1096,10 +1410,16 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
   if (dtype == VS_BF16) {
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
-    dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     count_path(VS_PATH_ATTN_FWD);
-    hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse,
-                       (int)N, (int)H, scale * kLog2e);
+    if (knob(VS_KNOB_ATTN_VARIANT) & 1) {  // one wave per SIMD, 3 query blocks per wave
+      dim3 grid((unsigned)(cdiv(N, 384) * H * B));
+      hipLaunchKernelGGL(attn_fwd_bf16_w1_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o,
+                         ld_o, lse, (int)N, (int)H, scale * kLog2e);
+    } else {
+      dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o,
+                         lse, (int)N, (int)H, scale * kLog2e);
+    }
   } else if (dtype == VS_F32) {
     dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);
     count_path(VS_PATH_ATTN_F32);

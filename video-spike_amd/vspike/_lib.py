@@ -85,6 +85,10 @@ PROTOTYPES = {
     "vs_knob_get": (ctypes.c_int, [ctypes.c_int]),
     "vs_knob_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "vs_mse_loss": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_f32, c_p, c_p]),
+    "vs_comm_unique_id": (ctypes.c_int, [c_p]),
+    "vs_comm_init": (ctypes.c_int, [ctypes.POINTER(c_p), c_p, c_i32, c_i32]),
+    "vs_comm_allreduce_bucket": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p]),
+    "vs_comm_finalize": (ctypes.c_int, [c_p]),
     "vs_mse_loss_bwd": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_p]),
     "vs_last_error": (ctypes.c_char_p, []),
     "vs_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),

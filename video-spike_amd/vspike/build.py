@@ -101,7 +101,9 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 8, variant: str
                 if verbose:
                     print(f"[vspike.build] compiled {os.path.basename(s)}", file=sys.stderr)
     if force or todo or _needs(lib_path, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, "-lpthread"]
+        rocm_lib = os.path.join(os.path.dirname(os.path.dirname(hipcc)), "lib")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path, *objs, "-lpthread",
+               f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
