@@ -184,6 +184,18 @@ int vs_video_preprocess(int32_t in_dtype, int64_t B, int64_t T, int64_t H, int64
 int vs_patch_im2col(int32_t out_dtype, int64_t B, int64_t F, int64_t C, int64_t H, int64_t W,
                     int64_t tubelet, int64_t patch, const float* pixels, void* cols, void* stream);
 
+/* Patch embedding with the tubelet gather fused into the GEMM's operand load (mv:176-181, 194-195,
+ * + bias + the sinusoid table mv:135 in the epilogue): out[m, d] = sum_k X[m, k] W[d, k] + bias[d] +
+ * pos[m % n_tok, d], X[m, k] = pixels[b, 2 f' + t, c, 16 hp + i, 16 wp + j] for token m = (b, f', hp, wp)
+ * and k = (c, t, i, j) — the Conv3d weight's flatten order; no im2col tensor.  The f32 NCHW pixels
+ * are read once, coalesced along image rows, converted to bf16 in registers and staged in LDS.
+ * weight: [D, C*2*16*16] bf16; out: [B*n_tok, D] f32; cols (optional, [B*n_tok, C*512] bf16): the
+ * gathered rows as a side output (the weight gradient's operand, written only when given).
+ * Fused path: tubelet 2, patch 16, D in {64, 128, 192}. */
+int vs_patch_embed_fwd(int64_t B, int64_t F, int64_t C, int64_t H, int64_t W, int64_t tubelet, int64_t patch,
+                       const float* pixels, const void* weight, const float* bias, const float* pos, int64_t D,
+                       float* out, void* cols, void* stream);
+
 /* Fixed sinusoid position table (mv:101-112), f32 [n_pos, dim] (computed in f64, rounded). */
 int vs_sinusoid_table(int64_t n_pos, int64_t dim, float* out, void* stream);
 

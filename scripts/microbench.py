@@ -10,6 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "video-spike_amd"))
+sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
@@ -142,6 +143,33 @@ def main():
         big = torch.empty(2 * M, F, dtype=bf, device=dev)
         report("copy 38.5 MB -> 38.5 MB (torch)", timeit(lambda: dst.copy_(src), a.reps), 2 * M * F * 2, 0)
         report("fill 77 MB (torch zero_)", timeit(lambda: big.zero_(), a.reps), 2 * M * F * 2, 0)
+    if a.only in ("", "patch"):
+        # patch embedding (C2: 16 clips of 16 x 3 x 224^2 -> 25,088 tokens x 192): im2col + row-slab GEMM
+        # against the fused gather GEMM, with and without the bf16 cols side output (the dW operand)
+        from oracle import cpu_ref
+        px = torch.randn(B, 16, 3, 224, 224, device=dev)
+        Kp = 1536
+        wp = r(D, Kp)
+        bp = torch.zeros(D, device=dev)
+        pos = cpu_ref.sinusoid_table(N, D).to(dev)
+        cols = torch.empty(M, Kp, dtype=bf, device=dev)
+        x0 = torch.empty(M, D, device=dev)
+        report("patch im2col (bf16 cols)", timeit(lambda: ops.patch_im2col(px, cols, 2, 16), a.reps), px.numel() * 6, 0)
+        report("patch GEMM on cols (+bias+pos)", timeit(lambda: ops.linear(cols, wp, x0, bias=bp, epilogue=L.EPI_POS,
+                                                                         pos=pos, pos_rows=N), a.reps),
+               M * Kp * 2 + M * D * 4, 2 * M * D * Kp)
+        report("patch fused gather GEMM", timeit(lambda: ops.patch_embed_fwd(px, wp, bp, pos, x0, 2, 16), a.reps),
+               px.numel() * 4 + M * D * 4, 2 * M * D * Kp)
+        report("patch fused gather GEMM + cols", timeit(lambda: ops.patch_embed_fwd(px, wp, bp, pos, x0, 2, 16,
+                                                                                   cols=cols), a.reps),
+               px.numel() * 6 + M * D * 4, 2 * M * D * Kp)
+        dxp = r(M, D)
+        dwp = torch.zeros(D, Kp, device=dev)
+        dbp = torch.zeros(D, device=dev)
+        nbp = ops.splitk_workspace_bytes(bf, D, Kp, M)
+        wsp = torch.empty(nbp // 4 + 64, device=dev)
+        report("patch dW (dx0^T cols, + db)", timeit(lambda: ops.linear_dw(dxp, cols, dwp, db=dbp, workspace=wsp), a.reps),
+               M * (D + Kp) * 2 + D * Kp * 4, 2 * M * D * Kp)
     if a.only in ("", "attn"):
         Da = H * 64
         qkv = r(M, 3 * Da, dt=bf) * 3

@@ -614,9 +614,39 @@ def test_attention_fwd_variants(knobs, variant, shape):
     o_ref, lse_ref = _attn_ref(qkv.double(), B, N, H)
     assert rel(o.float(), o_ref) < 1.5e-2
     assert rel(lse, lse_ref) < 3e-3
-    per = ((o.float().double() - o_ref).view(B, N, H, 64).norm(dim=(1, 3)) /
+    per = ((o.float().cpu().double() - o_ref).view(B, N, H, 64).norm(dim=(1, 3)) /
            o_ref.view(B, N, H, 64).norm(dim=(1, 3)))
     assert float(per.max()) < 3e-2
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1), (1, 400, 1)])
+def test_attention_bwd_variants(knobs, variant, shape):
+    """Both bf16 backward kernels (VS_KNOB_ATTN_VARIANT bit 1: 0 = 3 waves/SIMD x 32 rows, 2 = one
+    wave per SIMD x 96 keys (dK/dV) / 64 queries (dQ), 3-stage ring) against the fp64 gradient of
+    the fp64 attention on the same bf16 inputs, O and LSE from the forward kernel (as in training),
+    at the tails of test_attention_fwd_variants."""
+    from vspike import ops
+    knobs("attn_variant", variant)
+    B, N, H = shape
+    D = H * 64
+    qkv = _rand(B * N, 3 * D, seed=25, scale=1.5).to(torch.bfloat16)
+    do = _rand(B * N, D, seed=26).to(torch.bfloat16)
+    qd = qkv.to(DEV)
+    o = torch.empty(B * N, D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qd, o, lse, B, N, H)
+    dqkv = torch.full((B * N, 3 * D), 7.0, dtype=torch.bfloat16, device=DEV)
+    ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=DEV)
+    ops.attn_bwd(qd, o, do.to(DEV), lse, dqkv, ws, B, N, H)
+    torch.cuda.synchronize()
+    ref_in = qkv.double().requires_grad_()
+    o_ref, _ = _attn_ref(ref_in, B, N, H)
+    (g_ref,) = torch.autograd.grad(o_ref, ref_in, do.double())
+    for part in range(3):
+        sl = slice(part * D, (part + 1) * D)
+        e = rel(dqkv[:, sl].float(), g_ref[:, sl])
+        assert e < 3e-2, ("qkv"[part], e)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -721,6 +751,47 @@ def test_im2col_matches_oracle():
         out = torch.empty(ref.shape, dtype=dtype, device=DEV)
         ops.patch_im2col(px.to(DEV), out, cfg.tubelet_size, cfg.patch_size)
         assert torch.equal(out.cpu(), ref.to(dtype))
+
+
+@pytest.mark.parametrize("D", [64, 128, 192])
+@pytest.mark.parametrize("geo", [(6, 16, 3, 224, 224), (3, 8, 3, 112, 112), (1, 4, 1, 32, 48)])
+def test_patch_embed_fused_matches_im2col_gemm(knobs, D, geo):
+    """vs_patch_embed_fwd (tubelet gather in the GEMM's A-load, bias + position table in the epilogue)
+    against the im2col + row-slab GEMM path on the same inputs: the same bf16 operands, MFMA tiles,
+    k order and epilogue, so the outputs agree to the last bit; the optional bf16 cols side output
+    equals im2col's.  Also against fp64 (Conv3d on the bf16-rounded pixels).  Geometries: the bench
+    clips (B=6 of 16 x 224^2: M = 9,408 rows, the row-slab GEMM's range), a ragged token count (3 clips x 4 x 7 x 7), 1 channel / non-square."""
+    from oracle import cpu_ref
+    from vspike import ops, _lib as L
+    B, F, C, H, W = geo
+    t, p = 2, 16
+    n_tok = (F // t) * (H // p) * (W // p)
+    M, K = B * n_tok, C * t * p * p
+    px = _rand(B, F, C, H, W, seed=90)
+    w = _rand(D, K, seed=91, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = _rand(D, seed=92).to(DEV)
+    pos = cpu_ref.sinusoid_table(n_tok, D).to(DEV)
+    out = torch.full((M, D), 3.0, device=DEV)
+    cols = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+    L.dispatch_reset()
+    ops.patch_embed_fwd(px.to(DEV), w, bias, pos, out, t, p, cols=cols)
+    out2 = torch.full((M, D), 5.0, device=DEV)
+    ops.patch_embed_fwd(px.to(DEV), w, bias, pos, out2, t, p)          # no side output
+    assert L.dispatch_counts()["patch_fused"] == 2
+    ref_cols = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+    ops.patch_im2col(px.to(DEV), ref_cols, t, p)
+    knobs("no_slab", 0)
+    ref = torch.empty(M, D, device=DEV)
+    ops.linear(ref_cols, w, ref, bias=bias, epilogue=L.EPI_POS, pos=pos, pos_rows=n_tok)
+    torch.cuda.synchronize()
+    assert torch.equal(cols, ref_cols)
+    assert torch.equal(out, out2)
+    r64 = ref_cols.double() @ w.double().t() + bias.double() + pos.double().repeat(B, 1)
+    assert rel(out, r64) < 1e-5
+    if M >= 8192:      # the row-slab kernel (the im2col path's GEMM at M >= 8192): the same bits
+        assert torch.equal(out, ref)
+    else:
+        assert rel(out, ref.double()) < 1e-5
 
 
 def test_sinusoid_table_matches_oracle():

@@ -1366,6 +1366,405 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
   }
 }
 
+// ------------------------------------------------------------------ backward, one wave per SIMD
+// The same two passes as attn_bwd_dkdv_body / attn_bwd_dq_body, re-tiled for one wave per SIMD
+// (launch_bounds(256, 1): the whole register file per wave): a wave carries NB = 3 key blocks
+// (dK/dV) or 3 query blocks (dQ), so each fragment it reads from LDS (Q / dO rows and their
+// transposes in the dK/dV pass; K / V rows and K^T in the dQ pass) feeds 3 MFMAs, and the three
+// independent chains give the scheduler MFMAs to issue under each block's exp / dS VALU.
+// Slices of 64 rows stream through a 3-stage LDS-DMA ring issued two slices ahead (one barrier per
+// slice); every wave issues 5 DMA pieces per slice (Q/dO or K/V rows + a quarter of the row
+// constants), so its counted vmcnt is wave-uniform.  Workgroup = 384 keys (or queries) of one
+// (batch, head): 240 + 240 workgroups at C2, dK/dV first.
+constexpr int kW1Stage = 2 * kBwdQT + 512;
+// query blocks per dQ wave: 2 (the per-lane -LSE / -delta splats that seed its S and dP chains cost
+// 32 registers per block, so 3 blocks overflow the register file into accumulator copies)
+constexpr int kW1DqBlocks = 2;
+
+template <int NB>
+__device__ __forceinline__ void attn_bwd_dkdv_w1(char* __restrict__ smem, int blk, const bf16_t* __restrict__ qkv,
+                                                 int64_t ldq, const bf16_t* __restrict__ dout, int64_t lddo,
+                                                 const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                                 bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                                 float scale) {
+  constexpr int QT = kBwdQT, STAGE = kW1Stage, NSTG = 3, ROWS = 4 * NB * 32;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkb = (N + ROWS - 1) / ROWS, kb = blk % nkb;
+  const int h = (blk / nkb) % H, b = blk / nkb / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Vp = Qp + 2 * D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const float* NL = nlse2 + ((int64_t)b * H + h) * Npad;
+  const float* ND = ndel + ((int64_t)b * H + h) * Npad;
+  const int k0w = kb * ROWS + wid * NB * 32;  // this wave's first key
+  const float c2 = scale * kLog2e;
+
+  bf16x8 kf[NB][4], vf[NB][4];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int ki = k0w + j * 32 + (lane & 31);
+    const int kr = ki < N ? ki : N - 1;  // rows past N: finite data, their dK/dV are not stored
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 k = *(const bf16x8*)(Kp + (int64_t)kr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (float)k[e] * c2;
+      kf[j][s] = __builtin_convertvector(v, bf16x8);
+      vf[j][s] = *(const bf16x8*)(Vp + (int64_t)kr * ldq + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 dkacc[NB][2], dvacc[NB][2];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dkacc[j][0][r] = 0.f;
+      dkacc[j][1][r] = 0.f;
+      dvacc[j][0][r] = 0.f;
+      dvacc[j][1][r] = 0.f;
+    }
+
+  // DMA of 64-query slice `it` into stage `st`: wave w fills Q pieces 2w, 2w+1, dO pieces 2w, 2w+1
+  // and one quarter (32 floats) of nlse2 | ndel (waves 0, 1: nlse2 halves; 2, 3: ndel halves)
+  auto load_slice = [&](int it, int st) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+    const int q0 = it * 64;
+    int r0 = prow, r1 = prow + 8;
+    if (q0 + 64 > N) {  // partial last slice: rows past N re-read row N-1 (their nlse2 = -inf zeroes them)
+      r0 = q0 + r0 < N ? r0 : N - 1 - q0;
+      r1 = q0 + r1 < N ? r1 : N - 1 - q0;
+    }
+    const char* qs = (const char*)(Qp + (int64_t)q0 * ldq);
+    const char* ds = (const char*)(Dp + (int64_t)q0 * lddo);
+    char* dst = smem + st * STAGE;
+    glds16_asm_so(qs, (uint32_t)r0 * (uint32_t)(2 * ldq) + cq0, dst + wid * 2048);
+    glds16_asm_so(qs, (uint32_t)r1 * (uint32_t)(2 * ldq) + cq1, dst + wid * 2048 + 1024);
+    glds16_asm_so(ds, (uint32_t)r0 * (uint32_t)(2 * lddo) + cq0, dst + QT + wid * 2048);
+    glds16_asm_so(ds, (uint32_t)r1 * (uint32_t)(2 * lddo) + cq1, dst + QT + wid * 2048 + 1024);
+    const float* src = (wid < 2 ? NL : ND) + q0 + (wid & 1) * 32;
+    const uint32_t lo = (uint32_t)(lane & 31) * 4;
+    if (lane < 32) glds4_asm_so(src, lo, dst + 2 * QT + (wid >> 1) * 256 + (wid & 1) * 128);
+  };
+  auto wait_slice = [&](int younger) {  // 5 pieces per wave per slice
+    if (younger >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  const int qrow = lane & 31;
+  int roff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) roff[s] = qrow * 128 + (((2 * s + hh) ^ swz_rt(qrow)) << 4);
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, qt = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(qt, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(qt + 8, dt * 32 + g16 + p4);
+  }
+
+  // one 32-query sub-slice of stage st: S = Q K^T (+ -LSE log2e) -> P -> dV^T += dO^T P;
+  // dP = dO V^T (- delta) -> dS = P dP -> dK^T += Q^T dS, for the wave's NB key blocks
+  auto sub_slice = [&](int st, int sub) {
+    const char* sQ = smem + st * STAGE;
+    const char* sD = sQ + QT;
+    const float* sL = (const float*)(sQ + 2 * QT) + sub * 32 + 4 * hh;
+    const float* sE = (const float*)(sQ + 2 * QT + 256) + sub * 32 + 4 * hh;
+    f32x16 init;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *(const float4*)(sL + 8 * g);
+      init[4 * g] = l4.x; init[4 * g + 1] = l4.y; init[4 * g + 2] = l4.z; init[4 * g + 3] = l4.w;
+    }
+    f32x16 sacc[NB];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 a = *(const bf16x8*)(sQ + sub * 4096 + roff[s]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[j][s], s == 0 ? init : sacc[j], 0, 0, 0);
+    }
+    float p[NB][16];
+    bf16x8 pb[NB][2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[j][r] = __builtin_amdgcn_exp2f(sacc[j][r]);
+      pb[j][0] = pack8f(p[j]);
+      pb[j][1] = pack8f(p[j] + 8);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = sub * 4096 + s2 * 2048;
+        const bf16x8 a = tr_pair(sD, o + toff[dt][0], o + toff[dt][1]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) dvacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[j][s2], dvacc[j][dt], 0, 0, 0);
+      }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 e4 = *(const float4*)(sE + 8 * g);
+      init[4 * g] = e4.x; init[4 * g + 1] = e4.y; init[4 * g + 2] = e4.z; init[4 * g + 3] = e4.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 a = *(const bf16x8*)(sD + sub * 4096 + roff[s]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, vf[j][s], s == 0 ? init : sacc[j], 0, 0, 0);
+    }
+    bf16x8 db[NB][2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] = p[j][r] * sacc[j][r];
+      db[j][0] = pack8f(ds);
+      db[j][1] = pack8f(ds + 8);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = sub * 4096 + s2 * 2048;
+        const bf16x8 a = tr_pair(sQ, o + toff[dt][0], o + toff[dt][1]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) dkacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, db[j][s2], dkacc[j][dt], 0, 0, 0);
+      }
+  };
+
+  const int nit = (N + 63) / 64;
+  load_slice(0, 0);
+  if (nit > 1) load_slice(1, 1);
+  // slice `it` in stage it % 3 (a compile-time constant in the unrolled loop): wait for it, DMA
+  // slice it + 2 into slice it - 1's stage, then its two 32-query sub-slices
+  auto iter = [&](int it, auto stc) {
+    constexpr int ST = decltype(stc)::value;
+    wait_slice(it + 1 < nit ? 1 : 0);
+    if (it + 2 < nit) load_slice(it + 2, (ST + 2) % NSTG);
+    sub_slice(ST, 0);
+    if (it * 64 + 32 < N) sub_slice(ST, 1);
+  };
+  int it = 0;
+  for (; it + 3 <= nit; it += 3) {
+    iter(it, IC<0>{});
+    iter(it + 1, IC<1>{});
+    iter(it + 2, IC<2>{});
+  }
+  if (it < nit) iter(it, IC<0>{});
+  if (it + 1 < nit) iter(it + 1, IC<1>{});
+
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int ki = k0w + j * 32 + (lane & 31);
+    if (ki < N) {
+      bf16_t* krow = dqkv + (row0 + ki) * ldd + D + h * 64;
+      bf16_t* vrow = krow + D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          *(uint2*)(krow + d) = pack4(dkacc[j][dt][4 * g] * scale, dkacc[j][dt][4 * g + 1] * scale,
+                                      dkacc[j][dt][4 * g + 2] * scale, dkacc[j][dt][4 * g + 3] * scale);
+          *(uint2*)(vrow + d) =
+              pack4(dvacc[j][dt][4 * g], dvacc[j][dt][4 * g + 1], dvacc[j][dt][4 * g + 2], dvacc[j][dt][4 * g + 3]);
+        }
+    }
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void attn_bwd_dq_w1(char* __restrict__ smem, int blk, const bf16_t* __restrict__ qkv,
+                                               int64_t ldq, const bf16_t* __restrict__ dout, int64_t lddo,
+                                               const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                               float scale) {
+  constexpr int TILE = kBwdQT, STAGE = kW1Stage, NSTG = 3, ROWS = 4 * NB * 32;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (N + ROWS - 1) / ROWS, qb = blk % nqb;
+  const int h = (blk / nqb) % H, b = blk / nqb / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const int q0w = qb * ROWS + wid * NB * 32;
+  const float c2 = scale * kLog2e;
+
+  bf16x8 qf[NB][4], df[NB][4];
+  f32x16 sinit[NB], dinit[NB], dqacc[NB][2];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int qi = q0w + j * 32 + (lane & 31);
+    const int qr = qi < N ? qi : N - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (float)q[e] * c2;
+      qf[j][s] = __builtin_convertvector(v, bf16x8);
+      df[j][s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
+    }
+    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
+    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
+    const float nd = qi < N ? ndel[w] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sinit[j][r] = nl;
+      dinit[j][r] = nd;
+      dqacc[j][0][r] = 0.f;
+      dqacc[j][1][r] = 0.f;
+    }
+  }
+
+  int roff[4];
+  {
+    const int key = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
+  }
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
+  }
+
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  // DMA of 64-key tile kt into stage st: wave w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1, plus
+  // one dummy-free 5th piece slot (a repeat of its first K piece) so every wave counts 5 per tile
+  auto load_tile = [&](int kt, int st) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const uint32_t cc0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cc1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+    const char* kb_ = (const char*)Kp + kt * tile_bytes;
+    const char* vb_ = kb_ + vdelta;
+    char* dk = smem + st * STAGE + wid * 2048;
+    char* dv = dk + TILE;
+    int r0 = prow, r1 = prow + 8;
+    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (masked below)
+      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
+      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
+    }
+    const uint32_t o0 = (uint32_t)r0 * (uint32_t)(2 * ldq) + cc0, o1 = (uint32_t)r1 * (uint32_t)(2 * ldq) + cc1;
+    glds16_asm_so(kb_, o0, dk);
+    glds16_asm_so(kb_, o1, dk + 1024);
+    glds16_asm_so(vb_, o0, dv);
+    glds16_asm_so(vb_, o1, dv + 1024);
+    glds16_asm_so(kb_, o0, dk);  // same bytes again: keeps the per-slice piece count at 5 (see dK/dV)
+  };
+  auto wait_tile = [&](int younger) {
+    if (younger >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  // one 32-key block (kb of stage st): S^T = K (cQ)^T - LSE, dP^T = V dO^T - delta (query on the
+  // lane), dS^T = exp2(S^T) dP^T -> dQ^T += K^T dS^T, for the wave's NB query blocks
+  auto block = [&](int st, int kbk, int key0, auto maskc) {
+    constexpr bool MASK = decltype(maskc)::value;
+    const char* sK = smem + st * STAGE;
+    const char* sV = sK + TILE;
+    f32x16 sacc[NB], dpacc[NB];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(sK + kbk * 4096 + roff[s]);
+      const bf16x8 va = *(const bf16x8*)(sV + kbk * 4096 + roff[s]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[j][s], s == 0 ? sinit[j] : sacc[j], 0, 0, 0);
+        dpacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[j][s], s == 0 ? dinit[j] : dpacc[j], 0, 0, 0);
+      }
+    }
+    bf16x8 db[NB][2];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[j][r] = -INFINITY;
+      }
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[j][r]) * dpacc[j][r];
+      db[j][0] = pack8f(ds);
+      db[j][1] = pack8f(ds + 8);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = kbk * 4096 + s2 * 2048;
+        const bf16x8 ka = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) dqacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db[j][s2], dqacc[j][dt], 0, 0, 0);
+      }
+  };
+
+  const int nkt = (N + 63) / 64;
+  load_tile(0, 0);
+  if (nkt > 1) load_tile(1, 1);
+  auto iter = [&](int kt, auto stc) {
+    constexpr int ST = decltype(stc)::value;
+    wait_tile(kt + 1 < nkt ? 1 : 0);
+    if (kt + 2 < nkt) load_tile(kt + 2, (ST + 2) % NSTG);
+    if ((kt + 1) * 64 <= N) {
+      block(ST, 0, kt * 64, IC<0>{});
+      block(ST, 1, kt * 64 + 32, IC<0>{});
+    } else {  // the partial last tile
+      block(ST, 0, kt * 64, IC<1>{});
+      if (kt * 64 + 32 < N) block(ST, 1, kt * 64 + 32, IC<1>{});
+    }
+  };
+  int kt = 0;
+  for (; kt + 3 <= nkt; kt += 3) {
+    iter(kt, IC<0>{});
+    iter(kt + 1, IC<1>{});
+    iter(kt + 2, IC<2>{});
+  }
+  if (kt < nkt) iter(kt, IC<0>{});
+  if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int qi = q0w + j * 32 + (lane & 31);
+    if (qi < N) {
+      bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hh;
+          *(uint2*)(qrow + d) = pack4(dqacc[j][dt][4 * g] * scale, dqacc[j][dt][4 * g + 1] * scale,
+                                      dqacc[j][dt][4 * g + 2] * scale, dqacc[j][dt][4 * g + 3] * scale);
+        }
+    }
+  }
+}
+
+// dK/dV workgroups [0, nkv), dQ workgroups [nkv, nkv + nq): the longer dK/dV ones dispatch first and
+// the dQ ones fill the CUs they free
+__global__ __launch_bounds__(256, 1) void attn_bwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                  const bf16_t* __restrict__ dout, int64_t lddo,
+                                                                  const float* __restrict__ nlse2,
+                                                                  const float* __restrict__ ndel,
+                                                                  bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
+                                                                  int Npad, float scale, int nkv) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * kW1Stage];
+  const int id = blockIdx.x;
+  if (id < nkv)
+    attn_bwd_dkdv_w1<3>(smem, xcd_remap(id, nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
+  else
+    attn_bwd_dq_w1<kW1DqBlocks>(smem, xcd_remap(id - nkv, (int)gridDim.x - nkv), qkv, ldq, dout, lddo, nlse2, ndel,
+                                dqkv, ldd, N, H, Npad, scale);
+}
+
 // ------------------------------------------------------------------ backward: one launch
 // The dK/dV and dQ passes run as ONE grid: blocks [0, nblk) are dK/dV workgroups, [nblk, 2 nblk)
 // dQ workgroups, sharing the same two LDS stages.  Each pass alone puts 2496 waves on 3072 wave
@@ -1464,10 +1863,17 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     count_path(VS_PATH_ATTN_BWD);
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
-    dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-    hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
-                       (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                       scale, (int)grid.x);
+    if (knob(VS_KNOB_ATTN_VARIANT) & 2) {  // one wave per SIMD, 3 key / query blocks per wave
+      const unsigned nkv = (unsigned)(cdiv(N, 384) * H * B), nq = (unsigned)(cdiv(N, 128 * kW1DqBlocks) * H * B);
+      hipLaunchKernelGGL(attn_bwd_bf16_w1_kernel, dim3(nkv + nq), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+                         (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
+                         scale, (int)nkv);
+    } else {
+      dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
+      hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+                         (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
+                         scale, (int)grid.x);
+    }
   } else if (dtype == VS_F32) {
     count_path(VS_PATH_ATTN_F32);
     hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(dgrid), dim3(256), 0, s, (const float*)o, ld_o,

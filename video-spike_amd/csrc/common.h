@@ -191,6 +191,21 @@ __device__ __forceinline__ void glds16_asm_so(const void* sbase, uint32_t voff, 
       : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds))
       : "memory");
 }
+// 4 bytes per lane (64 lanes -> 256 B), SGPR base + per-lane 32-bit offset, invisible to hipcc's
+// waitcnt tracking like glds16_asm_so
+__device__ __forceinline__ void glds4_asm_so(const void* sbase, uint32_t voff, void* dst) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(VS_LDS void*)dst;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
+}
 __device__ __forceinline__ void glds4(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src, (VS_LDS void*)dst, 4, 0, 0);
 }

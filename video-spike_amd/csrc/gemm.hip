@@ -1144,6 +1144,177 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
 }
 
 // ----------------------------------------------------------------------------------------------
+// Patch embedding with the tubelet gather in the A-operand load (mv:176-181, 194-195 + the sinusoid
+// table, mv:135): x0[m, n] = sum_k X[m, k] W[n, k] + bias[n] + pos[m % n_tok, n], where X[m, k] is the
+// pixel of token m = (b, f', hp, wp) at k = (c, t, i, j) — no im2col tensor.  The row-slab structure
+// of gemm_bf16_slab_kernel (workgroup = contiguous token rows, all N <= 192 columns, 64-deep k
+// steps, W tiles by LDS-DMA into a 2-stage ring); the A tile of a k step (64 tokens x (c, t, 4 image
+// rows, 16 pixels)) is read from the f32 NCHW pixels — a wave's load instruction covers 4 adjacent
+// tokens x 4 image rows, i.e. 4 contiguous 256-B row segments — NR steps ahead into registers,
+// converted to bf16 and written into the same swizzled LDS image the MFMA fragments read.  Optionally
+// the bf16 gathered rows are also stored (cols, the operand the weight gradient reads).
+// Geometry compile-time: tubelet 2, patch 16 (the VideoMAE tubelet), K = C * 512.
+// ----------------------------------------------------------------------------------------------
+struct PatchGeo {
+  int F, C, H, W;       // pixels (B, F, C, H, W)
+  int n_tok, HpWp, Wp;  // tokens per clip, per frame pair, per patch row
+};
+
+template <int NT, bool COLS>
+__global__ __launch_bounds__(256, 2) void patch_embed_fwd_kernel(const float* __restrict__ px, PatchGeo g,
+                                                                 const bf16_t* __restrict__ B, int64_t K,
+                                                                 EpiParams e, bf16_t* __restrict__ cols) {
+  using OA = OperandBf16<64, true>;
+  using OB = OperandBf16<64, true>;
+  constexpr int N = 64 * NT, TM = 2, TN = NT * 2, WN = N / 2, NR = 3;
+  constexpr int STAGE = OA::BYTES + NT * OB::BYTES;
+  constexpr int LDT = N + 4;
+  static_assert(64 * LDT * 4 <= 2 * STAGE, "epilogue staging fits the ring");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int64_t G = gridDim.x;
+  const int64_t r_begin = (int64_t)blockIdx.x * e.M / G, r_end = ((int64_t)blockIdx.x + 1) * e.M / G;
+  const int nk = (int)(K / 64);  // 8 steps per channel: (t, 4-row group of the patch)
+  // this thread's part of every A tile: image row ii of the 4, pixels 4 jq .. 4 jq + 3 of the 16, for
+  // the tokens rows (tid >> 4) + 16 s, s < 4
+  const int ii = (tid >> 2) & 3, jq = tid & 3;
+  const int64_t plane = (int64_t)g.H * g.W;
+
+  for (int64_t m0 = r_begin; m0 < r_end; m0 += 64) {
+    const int64_t m_end = m0 + 64 < r_end ? m0 + 64 : r_end;
+    int64_t base[4];  // pixel index of (token, c = 0, t = 0, i = ii, j = 4 jq)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      int64_t m = m0 + (tid >> 4) + 16 * s;
+      m = m < m_end ? m : m_end - 1;
+      const int64_t b = m / g.n_tok;
+      const int n = (int)(m - b * g.n_tok);
+      const int fp = n / g.HpWp, r = n - fp * g.HpWp, hp = r / g.Wp, wp = r - hp * g.Wp;
+      base[s] = ((b * g.F + 2 * fp) * g.C) * plane + (int64_t)(hp * 16 + ii) * g.W + wp * 16 + 4 * jq;
+    }
+    auto step_off = [&](int t) {  // k step t = (c, tt, i0): c = t / 8, tt = (t / 4) & 1, i0 = 4 (t & 3)
+      return ((int64_t)((t >> 2) & 1) * g.C + (t >> 3)) * plane + (int64_t)(4 * (t & 3)) * g.W;
+    };
+    float4 ra[NR][4];
+    auto gload = [&](int t, float4 (&r)[4]) {
+      const int64_t o = step_off(t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) r[s] = *(const float4*)(px + base[s] + o);
+    };
+    // bf16 of this thread's 4 pixels -> A image row (token) rr, k = 16 ii + 4 jq: 8-B half of chunk 2 ii + jq / 2
+    auto awrite = [&](char* st, const float4 (&r)[4], int t) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int rr = (tid >> 4) + 16 * s;
+        uint2 u;
+        u.x = (uint32_t)f2bf(r[s].x) | ((uint32_t)f2bf(r[s].y) << 16);
+        u.y = (uint32_t)f2bf(r[s].z) | ((uint32_t)f2bf(r[s].w) << 16);
+        const int c8 = 2 * ii + (jq >> 1);
+        *(uint2*)(st + rr * 128 + ((c8 ^ swz_kc(rr)) << 4) + (jq & 1) * 8) = u;
+      }
+      (void)t;
+    };
+    // the bf16 rows of a completed A image as whole 128-B segments of cols (8 lanes per token row)
+    auto cols_store = [&](const char* st, int t) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ci = tid + 256 * q, rr = ci >> 3, c = ci & 7;
+        const int64_t m = m0 + rr;
+        const uint4 v = *(const uint4*)(st + rr * 128 + ((c ^ swz_kc(rr)) << 4));
+        if (m < m_end) *(uint4*)(cols + m * K + (int64_t)t * 64 + c * 8) = v;
+      }
+    };
+    auto bdma = [&](int t, char* st) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) OB::template dma<true>(st + OA::BYTES + j * OB::BYTES, B, K, j * 64, N, (int64_t)t * 64, wid, lane);
+    };
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const char* sa) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = OA::frag(sa, wr * 32 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wc * WN + j * 16;
+          bfr[j] = OB::frag(sa + OA::BYTES + (col >> 6) * OB::BYTES, col & 63, kk, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    __syncthreads();  // a previous tile's epilogue reads of the staging area are done
+    // prologue: A of steps 0 .. NR-1 in flight, step 0 staged
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+      if (t < nk) gload(t, ra[t]);
+    bdma(0, smem);
+    awrite(smem, ra[0], 0);
+    if (NR < nk) gload(NR, ra[0]);
+    // step t: [B DMA of t+1 into the other stage] compute(t) [A of t+1 -> LDS, loads of t+1+NR] barrier
+    auto step = [&](int t, auto rc) {
+      constexpr int R = decltype(rc)::value;  // register set of step t+1 = (t + 1) % NR
+      char* cur = smem + (t & 1) * STAGE;
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      // this wave's B pieces of step t landed; the 4 A loads of step t + NR (issued after them) may
+      // stay in flight (vmcnt counts in issue order)
+      if (t + NR < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // stage t complete (A written, B landed); every wave is done with stage t-1
+      if (t + 1 < nk) bdma(t + 1, nxt);
+      if constexpr (COLS) cols_store(cur, t);
+      compute(cur);
+      if (t + 1 < nk) {
+        awrite(nxt, ra[R], t + 1);
+        if (t + 1 + NR < nk) gload(t + 1 + NR, ra[R]);
+      }
+    };
+    int t = 0;
+    for (; t + NR <= nk; t += NR) {
+      step(t, IC<1 % NR>{});
+      step(t + 1, IC<2 % NR>{});
+      step(t + 2, IC<3 % NR>{});
+    }
+    static_assert(NR == 3, "the unrolled step sequence assumes NR = 3");
+    if (t < nk) step(t, IC<1 % NR>{});
+    if (t + 1 < nk) step(t + 1, IC<2 % NR>{});
+    // epilogue: stage the f32 tile over the ring, then 8-column groups per thread (bias + position)
+    __syncthreads();
+    float* stg = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stg[(wr * 32 + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    constexpr int CPR = N / 8, ITEMS = 64 * CPR / 256;
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+      const int idx = tid + 256 * it, rr = idx / CPR, cg = idx % CPR;
+      const int64_t m = m0 + rr;
+      if (m < m_end) {
+        const float* src = stg + rr * LDT + cg * 8;
+        float v[8];
+        const float4 a = *(const float4*)src;
+        const float4 b = *(const float4*)(src + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_eight<(uint32_t)(VS_EPI_BIAS | VS_EPI_POS)>(e, m, (int64_t)cg * 8, v, false);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
 // bf16 W-resident kernel for the wide K = 192 products of the ViT block: qkv (N = 576), fc1 + GELU
 // (N = 768, two bf16 outputs) and the GELU' dX product da = (dx' W2) * gelu'(a_pre) (N = 768).
 // Outputs are 3-4x the input, so the bound is the output stream; the per-tile kernels re-read
@@ -2248,6 +2419,44 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)cdiv(n_items, vec ? 64 : 256)), dim3(256), 0, s, e.part, g.splits,
                        d->M, d->N, (float*)d->c, d->ldc, (f & VS_EPI_BIAS) ? d->bias : nullptr, vec);
   }
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_patch_embed_fwd(int64_t B, int64_t F, int64_t C, int64_t H, int64_t W, int64_t tubelet,
+                                  int64_t patch, const float* pixels, const void* weight, const float* bias,
+                                  const float* pos, int64_t D, float* out, void* cols, void* stream) {
+  using namespace vs;
+  VS_REQUIRE(pixels && weight && bias && pos && out, "vs_patch_embed_fwd: null pointer");
+  VS_REQUIRE(tubelet == 2 && patch == 16, "vs_patch_embed_fwd: the fused path is built for tubelet 2, patch 16");
+  VS_REQUIRE(B > 0 && F % 2 == 0 && H % 16 == 0 && W % 16 == 0 && C >= 1 && C <= 8,
+             "vs_patch_embed_fwd: frames / size must divide by the tubelet / patch");
+  VS_REQUIRE(D == 64 || D == 128 || D == 192, "vs_patch_embed_fwd: D must be 64, 128 or 192 (one row slab)");
+  VS_REQUIRE(aligned16(pixels) && aligned16(weight) && aligned16(bias) && aligned16(pos) && aligned16(out) &&
+                 (!cols || aligned16(cols)),
+             "vs_patch_embed_fwd: pointers must be 16-byte aligned");
+  const int64_t n_tok = (F / 2) * (H / 16) * (W / 16), M = B * n_tok, K = C * 512;
+  VS_REQUIRE(B * F * C * H * W < (1ll << 40), "vs_patch_embed_fwd: batch too large");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_MISC, s,
+                    (double)M * (double)K * (4.0 + (cols ? 2.0 : 0.0)) + (double)D * (double)K * 2.0 +
+                        (double)M * (double)D * 4.0 + (double)n_tok * (double)D * 4.0);
+  EpiParams e = {};
+  e.M = M; e.N = D; e.c = out; e.ldc = D; e.out_bf16 = 0; e.op_bf16 = 1; e.flags = VS_EPI_BIAS | VS_EPI_POS;
+  e.alpha = 1.0f; e.bias = bias; e.pos = pos; e.pos_rows = n_tok; e.vec_ok = 1;
+  PatchGeo g;
+  g.F = (int)F; g.C = (int)C; g.H = (int)H; g.W = (int)W;
+  g.n_tok = (int)n_tok; g.HpWp = (int)((H / 16) * (W / 16)); g.Wp = (int)(W / 16);
+  const int64_t G = M / 16 < 512 ? (M / 16 > 0 ? M / 16 : 1) : 512;
+  count_path(VS_PATH_PATCH_FUSED);
+  const bf16_t* w = (const bf16_t*)weight;
+#define PF_(NT_, CO_)                                                                                        \
+  hipLaunchKernelGGL((patch_embed_fwd_kernel<NT_, CO_>), dim3((unsigned)G), dim3(256), 0, s, pixels, g, w, K, e, \
+                     (bf16_t*)cols)
+  if (D == 64) { if (cols) PF_(1, true); else PF_(1, false); }
+  else if (D == 128) { if (cols) PF_(2, true); else PF_(2, false); }
+  else { if (cols) PF_(3, true); else PF_(3, false); }
+#undef PF_
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

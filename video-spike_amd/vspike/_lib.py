@@ -113,6 +113,8 @@ PROTOTYPES = {
                                    c_p, c_i64, c_p, c_f32, c_p]),
     "vs_patch_im2col": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "vs_sinusoid_table": (ctypes.c_int, [c_i64, c_i64, c_p, c_p]),
+    "vs_patch_embed_fwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                          c_p, c_p, c_p]),
     "vs_colsum": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
     "vs_cast": (ctypes.c_int, [c_i32, c_i32, c_i64, c_p, c_p, c_p]),
     "vs_poisson_workspace_bytes": (c_sz, [c_i64]),

@@ -185,6 +185,24 @@ def patch_im2col(pixels, cols, tubelet, patch):
     return cols
 
 
+def patch_embed_fwd(pixels, weight, bias, pos, out, tubelet, patch, cols=None):
+    """out[B*n_tok, D] f32 = Conv3d patch embedding of pixels (B, F, C, H, W) f32 + bias + pos, with the
+    tubelet gather inside the GEMM (vs_patch_embed_fwd); cols (optional bf16 [B*n_tok, C*t*p*p])
+    receives the gathered rows for the weight gradient."""
+    require_device(pixels, weight, bias, pos, out)
+    B, F, C, H, W = pixels.shape
+    check(lib().vs_patch_embed_fwd(B, F, C, H, W, tubelet, patch, pixels.data_ptr(), weight.data_ptr(), bias.data_ptr(),
+                                   pos.data_ptr(), out.shape[1], out.data_ptr(), ptr(cols), stream()),
+          "vs_patch_embed_fwd")
+    return out
+
+
+def patch_embed_fused_ok(cfg, dtype) -> bool:
+    """Shapes the fused patch embedding covers (else im2col + GEMM)."""
+    return (dtype == torch.bfloat16 and cfg.tubelet_size == 2 and cfg.patch_size == 16 and
+            cfg.hidden_size in (64, 128, 192) and cfg.num_channels <= 8 and L.knob_get("no_patch_fused") == 0)
+
+
 def sinusoid_table(n_pos, dim, device):
     out = torch.empty(n_pos, dim, dtype=torch.float32, device=device)
     check(lib().vs_sinusoid_table(n_pos, dim, out.data_ptr(), stream()), "vs_sinusoid_table")

@@ -306,7 +306,11 @@ class VideoMAE(nn.Module):
         M = B * N
         lp = dt != torch.float32
         ar = Arena()
-        ar.add("cols", (M, cfg.patch_dim), dt)
+        # the gathered tubelet rows: the patch GEMM's operand when im2col runs, and the weight
+        # gradient's operand (a side output of the fused patch embedding) when the encoder trains
+        fused = ops.patch_embed_fused_ok(cfg, dt)
+        if save_encoder or not fused:
+            ar.add("cols", (M, cfg.patch_dim), dt)
         ar.add("x0", (M, D), torch.float32)
         for j in range(Lyr if save_encoder else 1):
             self._plan_layer(ar, f"L{j}.", B)
@@ -331,7 +335,7 @@ class VideoMAE(nn.Module):
             x_out = act[f"X{i}"] if save_encoder else act[f"X{i % 2}"]
             structs.append(self._layer_struct(i, B, x, x_out, act, f"L{j}.", enc_lp, enc32))
             x = x_out
-        new = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_final": x,
+        new = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_final": x, "fused": fused,
                "x_flat_lp": act["x_lp"] if lp else x.view(B, N * D), "head_ws": act.get("head_ws"),
                "sig": sig, "owner": None}
         if ent is None or ent["sig"] != sig:
@@ -356,9 +360,13 @@ class VideoMAE(nn.Module):
                     ops.cast(p.detach(), shadow)
                     stamp["key"] = lp_key(p)
 
-        ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
-        ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
-                   epilogue=L.EPI_POS, pos=self._pos_table(dev), pos_rows=N)
+        if ent["fused"]:   # tubelet gather inside the GEMM's operand load (no im2col pass)
+            ops.patch_embed_fwd(pixels, le.view(enc_lp, "patch_w"), le.view(enc32, "patch_b"), self._pos_table(dev),
+                                act["x0"], cfg.tubelet_size, cfg.patch_size, cols=act.get("cols"))
+        else:
+            ops.patch_im2col(pixels, act["cols"], cfg.tubelet_size, cfg.patch_size)
+            ops.linear(act["cols"], le.view(enc_lp, "patch_w"), act["x0"], bias=le.view(enc32, "patch_b"),
+                       epilogue=L.EPI_POS, pos=self._pos_table(dev), pos_rows=N)
         for s in ent["structs"]:
             ops.vit_layer_fwd(s)
         x_flat_lp = ent["x_flat_lp"]
