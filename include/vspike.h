@@ -278,7 +278,9 @@ typedef struct vs_vit_layer {
   void* qkv; void* attn_o; float* lse;       /* [M, 3D]; [M, D]; [B, H, N] */
   float* y;                                  /* [M, D] f32 (after attention residual) */
   void* h2;  float* mean2; float* rstd2;
-  void* a_pre; void* a_act;                  /* [M, F] dtype */
+  void* a_pre; void* a_act;                  /* [M, F] dtype.  bf16 mode (ABI v4): a_pre holds gelu'(pre),
+                                                the factor the backward's GELU' product multiplies by
+                                                (VS_EPI_GELU_GRAD / VS_EPI_MUL_AUX), not pre itself */
   float* x_out;                              /* [M, D] f32 */
 } vs_vit_layer;
 
@@ -291,7 +293,8 @@ typedef struct vs_vit_layer_grad {
   float* dx_in;         void* dx_in_lp;          /* outputs, same shapes */
   /* scratch (caller-owned): */
   void* d_a;            /* [M, F] dtype: d(pre-activation of fc1) */
-  float* d_h;           /* [M, D] f32: grad wrt LN outputs */
+  float* d_h;           /* [M, D]: grad wrt LN outputs; f32 in fp32 mode, written as bf16 in bf16
+                           mode (ABI v4) unless VS_KNOB_DH_F32 or VS_BWD_FUSE_LN is set — size it for f32 */
   float* dy;  void* dy_lp;                       /* [M, D] f32 + dtype copy */
   void* d_o;            /* [M, D] dtype */
   void* d_qkv;          /* [M, 3D] dtype */

@@ -11,7 +11,7 @@ want = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
-starts = [i for i, r in enumerate(rows) if "im2col" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "im2col" in r["Kernel_Name"] or "patch_embed_fwd" in r["Kernel_Name"]]
 starts = starts[-want:]
 def short(n):
     n = re.sub(r"\(.*", "", n)

@@ -2179,7 +2179,7 @@ static double gemm_algorithmic_bytes(const vs_gemm_desc* d) {
   if (f & VS_EPI_BIAS) b += (double)d->N * 4.0;
   if (f & VS_EPI_RESIDUAL) b += mn * 4.0;
   if (f & VS_EPI_POS) b += (double)(d->pos_rows < d->M ? d->pos_rows : d->M) * (double)d->N * 4.0;
-  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) b += mn * ea;
+  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD | VS_EPI_MUL_AUX)) b += mn * ea;
   if (f & VS_EPI_GELU) b += mn * ea;
   if (d->a_rowsum) b += (double)d->M * 8.0;
   return b;

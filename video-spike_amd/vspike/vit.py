@@ -306,10 +306,12 @@ class VideoMAE(nn.Module):
         M = B * N
         lp = dt != torch.float32
         ar = Arena()
-        # the gathered tubelet rows: the patch GEMM's operand when im2col runs, and the weight
-        # gradient's operand (a side output of the fused patch embedding) when the encoder trains
-        fused = ops.patch_embed_fused_ok(cfg, dt)
-        if save_encoder or not fused:
+        # patch embedding: the fused gather GEMM when no weight gradient follows (frozen encoder /
+        # inference: 49.9 us vs 61.8 us for im2col + GEMM at C2); when the encoder trains the dW
+        # product needs the gathered rows, and im2col + GEMM (61.8 us) beats the fused kernel with its
+        # cols side output (79.9 us) — profiles/r03_v2_microbench_patch.txt
+        fused = ops.patch_embed_fused_ok(cfg, dt) and not save_encoder
+        if not fused:
             ar.add("cols", (M, cfg.patch_dim), dt)
         ar.add("x0", (M, D), torch.float32)
         for j in range(Lyr if save_encoder else 1):
