@@ -70,6 +70,9 @@ def parse():
                          "(scripts/c3_curve.py), and non-finite scores send attention down its safe-softmax redo")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="budget of the CPU-oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the step as a hipGraph replay (vspike.graph.GraphedStep; N=1 only).  Off by default: "
+                         "on MI355X the replay measured 6.20 vs 5.62 ms/step eager (DESIGN.md section 7)")
     return ap.parse_args()
 
 
@@ -317,10 +320,18 @@ def main():
         trainer.step(pixels, target)
     barrier_sync()
     L.dispatch_reset()
+    step_fn = trainer.step
+    if args.graph:
+        if world > 1:
+            raise SystemExit("bench.py --graph: the data-parallel exchange is not captured (N=1 only)")
+        from vspike.graph import GraphedStep
+        graphed = GraphedStep(trainer, pixels, target)     # the capture counts one step's dispatch
+        step_fn = graphed.step
+        barrier_sync()
     t0 = time.perf_counter()
     losses = []
     for _ in range(args.steps):
-        losses.append(trainer.step(pixels, target))
+        losses.append(step_fn(pixels, target))
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -328,7 +339,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(losses[-1].item())
-    dispatch = {k: round(v / args.steps, 2) for k, v in L.dispatch_counts().items() if v}
+    dispatch = {k: round(v / (1 if args.graph else args.steps), 2) for k, v in L.dispatch_counts().items() if v}
     replicas_equal = None
     if world > 1:   # every rank ends with the same weights (the exchange kept the replicas in sync)
         hi = _param_digest(model, dev)
@@ -427,6 +438,8 @@ def main():
             "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
             "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
         }
+        if args.graph:
+            line["step_mode"] = "hipGraph replay (vspike.graph.GraphedStep)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

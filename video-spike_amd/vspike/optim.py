@@ -47,12 +47,9 @@ class FusedAdamW(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
         super().__init__(params, defaults)
 
-    @torch.no_grad()
-    def step(self, closure=None):
-        loss = None
-        if closure is not None:
-            with torch.enable_grad():
-                loss = closure()
+    def _work(self, advance: bool):
+        """device -> [(param, state, hyper row)] of the parameters that have a gradient; `advance`
+        counts this update in each parameter's step (the row carries the new count)."""
         work = {}
         for group in self.param_groups:
             b1, b2 = group["betas"]
@@ -64,23 +61,67 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                row = [group["lr"], b1, b2, group["eps"], group["weight_decay"], float(st["step"]),
-                       group["grad_scale"], 0.0]
+                step = st["step"] + 1
+                if advance:
+                    st["step"] = step
+                row = [group["lr"], b1, b2, group["eps"], group["weight_decay"], float(step), group["grad_scale"], 0.0]
                 work.setdefault(p.device, []).append((p, st, row))
-        for dev, items in work.items():
-            host = torch.tensor([r for _, _, r in items], dtype=torch.float32)
-            if dev.type != "cpu":
-                # the caching host allocator keeps the pinned block alive until the copy has run
-                host = host.pin_memory()
-            hyper = host.to(dev, non_blocking=True)
-            for k, (p, st, _) in enumerate(items):
-                g = p.grad
-                if g.dtype != torch.float32 or not g.is_contiguous():
-                    g = g.float().contiguous()
-                ent = lp_shadow(p)
-                lp = ent[0] if ent is not None and ent[0].device == p.device and ent[0].numel() == p.numel() else None
-                ops.adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], hyper[k], param_lp=lp)
-                if lp is not None:
-                    ent[1]["key"] = lp_key(p)
+        return work
+
+    @staticmethod
+    def _upload(items, dev, out=None):
+        host = torch.tensor([r for _, _, r in items], dtype=torch.float32)
+        if dev.type != "cpu":
+            # the caching host allocator keeps the pinned block alive until the copy has run
+            host = host.pin_memory()
+        if out is None:
+            return host.to(dev, non_blocking=True)
+        out[:len(items)].copy_(host, non_blocking=True)
+        return out
+
+    @staticmethod
+    def _launch(items, hyper):
+        for k, (p, st, _) in enumerate(items):
+            g = p.grad
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                g = g.float().contiguous()
+            ent = lp_shadow(p)
+            lp = ent[0] if ent is not None and ent[0].device == p.device and ent[0].numel() == p.numel() else None
+            ops.adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], hyper[k], param_lp=lp)
+            if lp is not None:
+                ent[1]["key"] = lp_key(p)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for dev, items in self._work(advance=True).items():
+            self._launch(items, self._upload(items, dev))
         return loss
+
+    # ---- hipGraph capture (vspike.graph.GraphedStep) -------------------------------------------
+    @torch.no_grad()
+    def static_hyper(self):
+        """device -> hyper-parameter block with a row for every parameter of the groups (those with
+        a gradient use the first rows, in `_work` order), to be captured: the launches of
+        `launch_static` read it, `stage` rewrites it before every replay."""
+        rows = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                rows[p.device] = rows.get(p.device, 0) + 1
+        return {dev: torch.zeros(n, 8, dtype=torch.float32, device=dev) for dev, n in rows.items()}
+
+    @torch.no_grad()
+    def launch_static(self, hyper):
+        """The update launches of `step` reading `hyper` (inside a capture; no host-side state moves)."""
+        for dev, items in self._work(advance=False).items():
+            self._launch(items, hyper[dev])
+
+    @torch.no_grad()
+    def stage(self, hyper):
+        """Host half of one captured update: count the step and send this step's rows (lr from the
+        scheduler, bias-correction step) into `hyper` on the current stream, ahead of the replay."""
+        for dev, items in self._work(advance=True).items():
+            self._upload(items, dev, out=hyper[dev])
