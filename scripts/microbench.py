@@ -20,11 +20,25 @@ HBM = 6.3e12
 MFMA = 2.5e15
 
 
+COLD = None
+
+
 def timeit(fn, reps):
     if fn is None:
         return float("nan")
     for _ in range(3):
         fn()
+    if COLD is not None:  # every rep from cold caches: a 512-MB fill evicts L2 and the Infinity Cache first
+        tot = 0.0
+        for _ in range(reps):
+            COLD.fill_(1.0)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            torch.cuda.synchronize()
+            tot += s.elapsed_time(e)
+        return tot / reps * 1e3
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
@@ -51,7 +65,13 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--heads", type=int, default=3, help="attention heads (3: C2 ViT-Tiny, 12: C3 ViT-Base)")
+    ap.add_argument("--attn-variants", default="0",
+                    help="VS_KNOB_ATTN_VARIANT values, comma-separated (low nibble: forward kernel, bits 4-7: backward)")
+    ap.add_argument("--cold", action="store_true", help="evict L2 / Infinity Cache before every timed launch")
     a = ap.parse_args()
+    global COLD
+    if a.cold:
+        COLD = torch.empty(128 * 1024 * 1024, device="cuda")
     global SELECT
     if a.only.startswith("gemm:"):
         a.only, SELECT = "gemm", a.only[5:]
@@ -179,13 +199,16 @@ def main():
         dq = torch.empty(M, 3 * Da, dtype=bf, device=dev)
         ws = torch.empty(ops.attn_bwd_workspace_bytes(B, N, H) // 4 + 64, device=dev)
         f = 4.0 * B * H * N * N * 64
-        for v in (0, 1, 2, 3):        # VS_KNOB_ATTN_VARIANT: bit 0 forward kernel, bit 1 backward kernel
+        done_f, done_b = set(), set()
+        for v in [int(t, 0) for t in a.attn_variants.split(",")]:
             with L.knob("attn_variant", v):
-                if v in (0, 1):
-                    report(f"attn fwd [variant {v}]", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps),
+                if (v & 15) not in done_f:
+                    done_f.add(v & 15)
+                    report(f"attn fwd [variant {v:#x}]", timeit(lambda: ops.attn_fwd(qkv, o, lse, B, N, H), a.reps),
                            M * 4 * Da * 2, f)
-                if v in (0, 2):
-                    report(f"attn bwd (delta+dkdv+dq) [variant {v}]",
+                if (v >> 4) not in done_b:
+                    done_b.add(v >> 4)
+                    report(f"attn bwd (rowprep+dkdv+dq) [variant {v:#x}]",
                            timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps), M * 8 * Da * 2,
                            2.5 * f)
     if a.only in ("", "linear"):
@@ -217,6 +240,10 @@ def main():
         ops.layernorm_fwd(x, g, b, 1e-12, y, mu, rs)
         report("ln bwd (+dres, + bf16 copy)", timeit(lambda: ops.layernorm_bwd(x, x, mu, rs, g, dx, dg, dbb, dres=x,
                                                                                dx_lp=dxl), a.reps), M * D * 18, 0)
+        dyl = y.clone()
+        report("ln bwd (bf16 dy, +dres, + bf16 copy)", timeit(lambda: ops.layernorm_bwd(dyl, x, mu, rs, g, dx, dg, dbb,
+                                                                                        dres=x, dx_lp=dxl), a.reps),
+               M * D * 16, 0)
 
 
 if __name__ == "__main__":

@@ -595,11 +595,12 @@ def _attn_ref(qkv, B, N, H, scale=0.125):
 ATTN_SHAPES = [(1, 100, 1), (2, 196, 2), (1, 1568, 3), (2, 130, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 4])
 @pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1)])
 def test_attention_fwd_variants(knobs, variant, shape):
-    """Both bf16 forward kernels (VS_KNOB_ATTN_VARIANT bit 0: 0 = 3 waves/SIMD x 32 rows, 1 = one
-    wave per SIMD x 96 rows, 3-stage K/V ring) against fp64 on the same bf16 inputs, at tails of
+    """The bf16 forward kernels (VS_KNOB_ATTN_VARIANT low nibble: 0 = 3 waves/SIMD x 32 rows; 1 = one
+    wave per SIMD x 96 rows, 3-stage K/V ring, S(i+1) issued before softmax(i); 4 = that body at 32
+    rows per wave and 2 waves per SIMD) against fp64 on the same bf16 inputs, at tails of
     every kind: N = 1 / 33 / 100 / 130 / 196 (partial 32-key block), 1568 (= 4 x 384 + 32: a
     workgroup with one live q-block), 1600 (partial 64-key tile), 3136 (C5: 98 blocks)."""
     from vspike import ops
@@ -619,11 +620,12 @@ def test_attention_fwd_variants(knobs, variant, shape):
     assert float(per.max()) < 3e-2
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 0x10, 0x50])
 @pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1), (1, 400, 1)])
 def test_attention_bwd_variants(knobs, variant, shape):
-    """Both bf16 backward kernels (VS_KNOB_ATTN_VARIANT bit 1: 0 = 3 waves/SIMD x 32 rows, 2 = one
-    wave per SIMD x 96 keys (dK/dV) / 64 queries (dQ), 3-stage ring) against the fp64 gradient of
+    """The bf16 backward kernels (VS_KNOB_ATTN_VARIANT bits 4-7: 0 = 3 waves/SIMD x 32 rows; 1 = one
+    wave per SIMD x 96 keys (dK/dV) / 64 queries (dQ), 3-stage ring; 5 = the same body at 32 rows
+    and 2 waves per SIMD) against the fp64 gradient of
     the fp64 attention on the same bf16 inputs, O and LSE from the forward kernel (as in training),
     at the tails of test_attention_fwd_variants."""
     from vspike import ops

@@ -674,8 +674,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 // LDS-DMA into a 3-stage ring of 64-key tiles issued two tiles ahead, one barrier per tile.
 // Numerics and the two passes (fast: p = exp2(s) against a fixed reference, row sums on the matrix
 // pipe; safe: online softmax, re-run when a row sum leaves [2^-60, 2^60]) as attn_fwd_bf16_kernel.
-template <int NQB>
-__global__ __launch_bounds__(256, 1) void attn_fwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+template <int NQB, int WPS>
+__global__ __launch_bounds__(256, WPS) void attn_fwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                   bf16_t* __restrict__ o, int64_t ldo,
                                                                   float* __restrict__ lse, int N, int H,
                                                                   float scale_log2) {
@@ -1749,20 +1749,22 @@ __device__ __forceinline__ void attn_bwd_dq_w1(char* __restrict__ smem, int blk,
 }
 
 // dK/dV workgroups [0, nkv), dQ workgroups [nkv, nkv + nq): the longer dK/dV ones dispatch first and
-// the dQ ones fill the CUs they free
-__global__ __launch_bounds__(256, 1) void attn_bwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                                  const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                  const float* __restrict__ nlse2,
-                                                                  const float* __restrict__ ndel,
-                                                                  bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
-                                                                  int Npad, float scale, int nkv) {
+// the dQ ones fill the CUs they free.  NBKV key blocks per dK/dV wave, NBQ query blocks per dQ wave,
+// WPS waves per SIMD (the register budget: 512 / WPS per lane).
+template <int NBKV, int NBQ, int WPS>
+__global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                    const bf16_t* __restrict__ dout, int64_t lddo,
+                                                                    const float* __restrict__ nlse2,
+                                                                    const float* __restrict__ ndel,
+                                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N,
+                                                                    int H, int Npad, float scale, int nkv) {
   __shared__ __attribute__((aligned(16))) char smem[3 * kW1Stage];
   const int id = blockIdx.x;
   if (id < nkv)
-    attn_bwd_dkdv_w1<3>(smem, xcd_remap(id, nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
+    attn_bwd_dkdv_w1<NBKV>(smem, xcd_remap(id, nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
   else
-    attn_bwd_dq_w1<kW1DqBlocks>(smem, xcd_remap(id - nkv, (int)gridDim.x - nkv), qkv, ldq, dout, lddo, nlse2, ndel,
-                                dqkv, ldd, N, H, Npad, scale);
+    attn_bwd_dq_w1<NBQ>(smem, xcd_remap(id - nkv, (int)gridDim.x - nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv,
+                        ldd, N, H, Npad, scale);
 }
 
 // ------------------------------------------------------------------ backward: one launch
@@ -1810,10 +1812,22 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
     count_path(VS_PATH_ATTN_FWD);
-    if (knob(VS_KNOB_ATTN_VARIANT) & 1) {  // one wave per SIMD, 3 query blocks per wave
-      dim3 grid((unsigned)(cdiv(N, 384) * H * B));
-      hipLaunchKernelGGL(attn_fwd_bf16_w1_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o,
-                         ld_o, lse, (int)N, (int)H, scale * kLog2e);
+    // VS_KNOB_ATTN_VARIANT low nibble: 0 the default kernel; 1..3 the software-pipelined kernel with
+    // (query blocks per wave, waves per SIMD) = (3, 1), (1, 3), (2, 2), (1, 2)
+    const int fv = knob(VS_KNOB_ATTN_VARIANT) & 15;
+    auto w1 = [&](auto kern, int nqb) {
+      dim3 grid((unsigned)(cdiv(N, 128 * nqb) * H * B));
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse, (int)N,
+                         (int)H, scale * kLog2e);
+    };
+    if (fv == 1) {
+      w1(attn_fwd_bf16_w1_kernel<3, 1>, 3);
+    } else if (fv == 2) {
+      w1(attn_fwd_bf16_w1_kernel<1, 3>, 1);
+    } else if (fv == 3) {
+      w1(attn_fwd_bf16_w1_kernel<2, 2>, 2);
+    } else if (fv == 4) {
+      w1(attn_fwd_bf16_w1_kernel<1, 2>, 1);
     } else {
       dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
       hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o,
@@ -1863,11 +1877,25 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     count_path(VS_PATH_ATTN_BWD);
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
-    if (knob(VS_KNOB_ATTN_VARIANT) & 2) {  // one wave per SIMD, 3 key / query blocks per wave
-      const unsigned nkv = (unsigned)(cdiv(N, 384) * H * B), nq = (unsigned)(cdiv(N, 128 * kW1DqBlocks) * H * B);
-      hipLaunchKernelGGL(attn_bwd_bf16_w1_kernel, dim3(nkv + nq), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
-                         (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                         scale, (int)nkv);
+    // VS_KNOB_ATTN_VARIANT bits 4..7: 0 the default kernel; 1..5 the multi-block kernel with (key
+    // blocks per dK/dV wave, query blocks per dQ wave, waves per SIMD) = (3, 2, 1), (1, 1, 3),
+    // (2, 2, 2), (2, 1, 2), (1, 1, 2)
+    const int bv = (knob(VS_KNOB_ATTN_VARIANT) >> 4) & 15;
+    auto w1 = [&](auto kern, int nbkv, int nbq) {
+      const unsigned nkv = (unsigned)(cdiv(N, 128 * nbkv) * H * B), nq = (unsigned)(cdiv(N, 128 * nbq) * H * B);
+      hipLaunchKernelGGL(kern, dim3(nkv + nq), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout,
+                         ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad, scale, (int)nkv);
+    };
+    if (bv == 1) {
+      w1(attn_bwd_bf16_w1_kernel<3, kW1DqBlocks, 1>, 3, kW1DqBlocks);
+    } else if (bv == 2) {
+      w1(attn_bwd_bf16_w1_kernel<1, 1, 3>, 1, 1);
+    } else if (bv == 3) {
+      w1(attn_bwd_bf16_w1_kernel<2, 2, 2>, 2, 2);
+    } else if (bv == 4) {
+      w1(attn_bwd_bf16_w1_kernel<2, 1, 2>, 2, 1);
+    } else if (bv == 5) {
+      w1(attn_bwd_bf16_w1_kernel<1, 1, 2>, 1, 1);
     } else {
       dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
       hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,

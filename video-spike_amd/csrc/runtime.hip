@@ -42,7 +42,7 @@ static void knob_init() {
     int v = kKnobs[i].dflt;
     if (kKnobs[i].env) {
       const char* e = getenv(kKnobs[i].env);
-      if (e && e[0]) v = atoi(e);
+      if (e && e[0]) v = (int)strtol(e, nullptr, 0);  // decimal or 0x hex
     }
     g_knob[i].store(v, std::memory_order_relaxed);
   }
