@@ -204,14 +204,15 @@ def _pmc_lookup(kind):
     """MFMA-busy fraction of an attention kernel from the newest committed PMC summary
     (scripts/pmc_attn.sh passes -> scripts/pmc_json.py: SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
     GRBM_GUI_ACTIVE / 8), the executed-MFMA cross-check of the hipEvent roofline."""
-    kern = {"attn_fwd": "attn_fwd_bf16_kernel", "attn_bwd": "attn_bwd_bf16_kernel"}.get(kind)
+    kern = {"attn_fwd": ("attn_fwd_bf16_kernel",),
+            "attn_bwd": ("attn_bwd_bf16_pp_kernel<2, true, true>", "attn_bwd_bf16_kernel")}.get(kind)
     if kern is None:
         return None
     for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_attn.json")))):
         try:
             d = json.load(open(f))
             for name, e in d["kernels"].items():
-                if name.endswith(kern) and "mfma_busy_frac" in e:
+                if name.endswith(kern[0]) and "mfma_busy_frac" in e:
                     return {"mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
                             "note": "executed MFMA cycles (the backward's dQ pass recomputes S and dP: 7 products "
                                     "executed for the 5 credited)" if kind == "attn_bwd" else "executed MFMA cycles "

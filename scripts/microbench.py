@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--heads", type=int, default=3, help="attention heads (3: C2 ViT-Tiny, 12: C3 ViT-Base)")
     ap.add_argument("--attn-variants", default="0",
                     help="VS_KNOB_ATTN_VARIANT values, comma-separated (low nibble: forward kernel, bits 4-7: backward)")
+    ap.add_argument("--attn-scale", type=float, default=3.0, help="q, k, v ~ N(0, scale^2)")
     ap.add_argument("--cold", action="store_true", help="evict L2 / Infinity Cache before every timed launch")
     a = ap.parse_args()
     global COLD
@@ -192,7 +193,7 @@ def main():
                M * (D + Kp) * 2 + D * Kp * 4, 2 * M * D * Kp)
     if a.only in ("", "attn"):
         Da = H * 64
-        qkv = r(M, 3 * Da, dt=bf) * 3
+        qkv = r(M, 3 * Da, dt=bf) * a.attn_scale
         o = torch.empty(M, Da, dtype=bf, device=dev)
         lse = torch.empty(B, H, N, device=dev)
         do = r(M, Da)
@@ -208,6 +209,8 @@ def main():
                            M * 4 * Da * 2, f)
                 if (v >> 4) not in done_b:
                     done_b.add(v >> 4)
+                    if v >> 8:
+                        print("  (bits 8 / 9: the dK/dV or the dQ pass skipped: timing only)")
                     report(f"attn bwd (rowprep+dkdv+dq) [variant {v:#x}]",
                            timeit(lambda: ops.attn_bwd(qkv, o, do, lse, dq, ws, B, N, H), a.reps), M * 8 * Da * 2,
                            2.5 * f)

@@ -23,7 +23,8 @@ def main(d, out, steps):
         kern[name.split("(")[0]] = {"fetch_bytes_x2": 2 * fetch, "write_bytes": write, "traffic_bytes": 2 * fetch + write,
                                     "launches": len(c["FETCH_SIZE"])}
     # the bench's timer classes (libvspike VS_TIMER_*): which kernels one timed call launches
-    groups = {"attn_bwd": ["attn_rowprep_kernel", "attn_bwd_bf16_kernel", "attn_bwd_dkdv_bf16_kernel", "attn_bwd_dq_bf16_kernel"],
+    groups = {"attn_bwd": ["attn_rowprep_kernel", "attn_bwd_bf16_kernel", "attn_bwd_bf16_pp_kernel", "attn_bwd_dkdv_bf16_kernel",
+                           "attn_bwd_dq_bf16_kernel"],
               "attn_fwd": ["attn_fwd_bf16_kernel"],
               "gemm_dw": ["gemm_dw_kernel", "gemm_dw_reg_kernel", "gemm_dw_reduce"],
               "gemm": ["gemm_bf16_kernel", "gemm_bf16_ring_kernel", "gemm_bf16_fullk_kernel", "gemm_bf16_panel_kernel",

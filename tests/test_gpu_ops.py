@@ -620,11 +620,12 @@ def test_attention_fwd_variants(knobs, variant, shape):
     assert float(per.max()) < 3e-2
 
 
-@pytest.mark.parametrize("variant", [0, 0x10, 0x50])
+@pytest.mark.parametrize("variant", [0, 0x10, 0x50, 0x70, 0x80, 0x90])
 @pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1), (1, 400, 1)])
 def test_attention_bwd_variants(knobs, variant, shape):
-    """The bf16 backward kernels (VS_KNOB_ATTN_VARIANT bits 4-7: 0 = 3 waves/SIMD x 32 rows; 1 = one
-    wave per SIMD x 96 keys (dK/dV) / 64 queries (dQ), 3-stage ring; 5 = the same body at 32 rows
+    """The bf16 backward kernels (VS_KNOB_ATTN_VARIANT bits 4-7: 0 = software-pipelined pairs of 32-row
+    units, 2 waves/SIMD (7 / 8: only the dK/dV / dQ pass pipelined); 9 = 3 waves/SIMD x 32 rows; 1 =
+    one wave per SIMD x 96 keys (dK/dV) / 64 queries (dQ), 3-stage ring; 5 = that body at 32 rows
     and 2 waves per SIMD) against the fp64 gradient of
     the fp64 attention on the same bf16 inputs, O and LSE from the forward kernel (as in training),
     at the tails of test_attention_fwd_variants."""

@@ -1366,6 +1366,387 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
   }
 }
 
+// ------------------------------------------------------------------ backward, software-pipelined pairs
+// The 3-wave bodies above rely on the other waves of the SIMD to fill the gap between a chain's
+// MFMAs and the VALU that consumes them (exp after S, dS after dP).  These bodies pipeline two
+// independent 32-row units inside the wave instead (2 waves per SIMD: the register file of two
+// units): the dK/dV body runs a 64-query slice as S(a), S(b) (interleaved chains) -> P(a) under
+// S(b)'s MFMAs -> dV(a), dP(a) -> P(b) under them -> dV(b), dP(b) -> dS(a) under them -> dK(a) ->
+// dS(b) under dK(a) -> dK(b); the dQ body runs a 64-key tile as S, dP of keys a and b (interleaved
+// chains) -> dS(a) under b's MFMAs -> dQ(a) -> dS(b) under dQ(a) -> dQ(b).  P stays f32 between the
+// dV and dK products (no bf16 unpack).  Same LDS images, DMA and numerics as the 3-wave bodies.
+__device__ __forceinline__ void attn_bwd_dkdv_pp(char* __restrict__ stg0, char* __restrict__ stg1, int blk,
+                                                 const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                 const bf16_t* __restrict__ dout, int64_t lddo,
+                                                 const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                                 bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                                 float scale) {
+  constexpr int QT = kBwdQT;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb128 = (N + 127) / 128, kb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Vp = Qp + 2 * D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const float* NL = nlse2 + ((int64_t)b * H + h) * Npad;
+  const float* ND = ndel + ((int64_t)b * H + h) * Npad;
+  const int ki = kb * 128 + wid * 32 + (lane & 31);
+  const float c2 = scale * kLog2e;
+
+  bf16x8 kf[4], vf[4];
+  {
+    const int kr = ki < N ? ki : N - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 k = *(const bf16x8*)(Kp + (int64_t)kr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)k[j] * c2;
+      kf[s] = __builtin_convertvector(v, bf16x8);
+      vf[s] = *(const bf16x8*)(Vp + (int64_t)kr * ldq + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 dkacc[2], dvacc[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dkacc[0][r] = 0.f;
+    dkacc[1][r] = 0.f;
+    dvacc[0][r] = 0.f;
+    dvacc[1][r] = 0.f;
+  }
+  auto load_stage = [&](int it, char* dst) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+    const int q0 = it * 64;
+    int r0 = prow, r1 = prow + 8;
+    if (q0 + 64 > N) {
+      r0 = q0 + r0 < N ? r0 : N - 1 - q0;
+      r1 = q0 + r1 < N ? r1 : N - 1 - q0;
+    }
+    const char* qs = (const char*)(Qp + (int64_t)q0 * ldq);
+    const char* ds = (const char*)(Dp + (int64_t)q0 * lddo);
+    glds16_asm_so(qs, (uint32_t)r0 * (uint32_t)(2 * ldq) + cq0, dst + wid * 2048);
+    glds16_asm_so(qs, (uint32_t)r1 * (uint32_t)(2 * ldq) + cq1, dst + wid * 2048 + 1024);
+    glds16_asm_so(ds, (uint32_t)r0 * (uint32_t)(2 * lddo) + cq0, dst + QT + wid * 2048);
+    glds16_asm_so(ds, (uint32_t)r1 * (uint32_t)(2 * lddo) + cq1, dst + QT + wid * 2048 + 1024);
+    const float* src = (wid < 2 ? NL : ND) + q0 + (wid & 1) * 32;
+    if (lane < 32) glds4_asm_so(src, (uint32_t)(lane & 31) * 4, dst + 2 * QT + (wid >> 1) * 256 + (wid & 1) * 128);
+  };
+  const int qrow = lane & 31;
+  int roff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) roff[s] = qrow * 128 + (((2 * s + hh) ^ swz_rt(qrow)) << 4);
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, qt = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(qt, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(qt + 8, dt * 32 + g16 + p4);
+  }
+  auto rowc = [&](const float* base, int sub, f32x16& acc) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *(const float4*)(base + sub * 32 + 4 * hh + 8 * g);
+      acc[4 * g] = l4.x; acc[4 * g + 1] = l4.y; acc[4 * g + 2] = l4.z; acc[4 * g + 3] = l4.w;
+    }
+  };
+  // one 64-query slice: sub-slices a (queries 0..31) and b (32..63).  A sub-slice past N runs on
+  // padded rows (nlse2 = -inf: P = 0, dS = 0), so every slice is branch-free.  Each phase's LDS
+  // operand reads are issued ahead of its MFMAs (pinned by sched_barriers; the compiler otherwise
+  // sinks every read next to its MFMA behind an lgkmcnt(0)).
+  auto rows4 = [&](const char* img, int sub, bf16x8 (&f)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f[s] = *(const bf16x8*)(img + sub * 4096 + roff[s]);
+  };
+  auto tr4 = [&](const char* img, int sub, bf16x8 (&f)[4]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = sub * 4096 + s2 * 2048;
+        f[2 * s2 + dt] = tr_pair(img, o + toff[dt][0], o + toff[dt][1]);
+      }
+  };
+  auto mma_p = [&](const bf16x8 (&f)[4], const float (&pv)[16], f32x16 (&acc)[2]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = pack8f(pv + 8 * s2);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 * s2 + dt], pb, acc[dt], 0, 0, 0);
+    }
+  };
+  auto slice = [&](const char* st) {
+    const char* sQ = st;
+    const char* sD = st + QT;
+    const float* sL = (const float*)(st + 2 * QT);
+    const float* sE = (const float*)(st + 2 * QT + 256);
+    f32x16 xa, xb;
+    bf16x8 fa[4], fb[4];
+    rowc(sL, 0, xa);
+    rows4(sQ, 0, fa);
+    rowc(sL, 1, xb);
+    rows4(sQ, 1, fb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {  // S(a), S(b): two independent chains, interleaved
+      xa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s], kf[s], xa, 0, 0, 0);
+      xb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], kf[s], xb, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    tr4(sD, 0, fa);  // dO(a)^T for dV(a)
+    rows4(sD, 0, fb);  // dO(a) rows for dP(a)
+    __builtin_amdgcn_sched_barrier(0);
+    float pa[16], pb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pa[r] = __builtin_amdgcn_exp2f(xa[r]);
+    rowc(sE, 0, xa);
+    mma_p(fa, pa, dvacc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], vf[s], xa, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    tr4(sD, 1, fa);  // dO(b)^T
+    rows4(sD, 1, fb);  // dO(b) rows
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pb[r] = __builtin_amdgcn_exp2f(xb[r]);
+    rowc(sE, 1, xb);
+    mma_p(fa, pb, dvacc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], vf[s], xb, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    tr4(sQ, 0, fa);  // Q(a)^T, Q(b)^T for dK
+    tr4(sQ, 1, fb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pa[r] *= xa[r];
+    mma_p(fa, pa, dkacc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pb[r] *= xb[r];
+    mma_p(fb, pb, dkacc);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int nit = (N + 63) / 64;
+  load_stage(0, stg0);
+  auto iter = [&](int it, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (it + 1 < nit) load_stage(it + 1, BUF ? stg0 : stg1);
+    slice(BUF ? stg1 : stg0);
+  };
+  for (int it = 0; it < nit; it += 2) {
+    iter(it, IC<0>{});
+    if (it + 1 < nit) iter(it + 1, IC<1>{});
+  }
+  if (ki < N) {
+    bf16_t* krow = dqkv + (row0 + ki) * ldd + D + h * 64;
+    bf16_t* vrow = krow + D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(krow + d) = pack4(dkacc[dt][4 * g] * scale, dkacc[dt][4 * g + 1] * scale,
+                                    dkacc[dt][4 * g + 2] * scale, dkacc[dt][4 * g + 3] * scale);
+        *(uint2*)(vrow + d) = pack4(dvacc[dt][4 * g], dvacc[dt][4 * g + 1], dvacc[dt][4 * g + 2], dvacc[dt][4 * g + 3]);
+      }
+  }
+}
+
+__device__ __forceinline__ void attn_bwd_dq_pp(char* __restrict__ kv0, char* __restrict__ kv1, int blk,
+                                               const bf16_t* __restrict__ qkv, int64_t ldq,
+                                               const bf16_t* __restrict__ dout, int64_t lddo,
+                                               const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                               float scale) {
+  constexpr int TILE = 64 * 128;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb128 = (N + 127) / 128, qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const int qi = qb * 128 + wid * 32 + (lane & 31);
+  const float c2 = scale * kLog2e;
+  bf16x8 qf[4], df[4];
+  {
+    const int qr = qi < N ? qi : N - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c2;
+      qf[s] = __builtin_convertvector(v, bf16x8);
+      df[s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 sinit, dinit, dqacc[2];
+  {
+    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
+    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
+    const float nd = qi < N ? ndel[w] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sinit[r] = nl;
+      dinit[r] = nd;
+      dqacc[0][r] = 0.f;
+      dqacc[1][r] = 0.f;
+    }
+  }
+  int roff[4];
+  {
+    const int key = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
+  }
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
+  }
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  auto load_tile = [&](int kt, char* buf) {
+    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+    const uint32_t cc0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cc1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+    const char* kb_ = (const char*)Kp + kt * tile_bytes;
+    int r0 = prow, r1 = prow + 8;
+    if ((kt + 1) * 64 > N) {
+      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
+      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
+    }
+    const uint32_t o0 = (uint32_t)r0 * (uint32_t)(2 * ldq) + cc0, o1 = (uint32_t)r1 * (uint32_t)(2 * ldq) + cc1;
+    glds16_asm_so(kb_, o0, buf + wid * 2048);
+    glds16_asm_so(kb_, o1, buf + wid * 2048 + 1024);
+    glds16_asm_so(kb_ + vdelta, o0, buf + TILE + wid * 2048);
+    glds16_asm_so(kb_ + vdelta, o1, buf + TILE + wid * 2048 + 1024);
+  };
+  auto mask = [&](f32x16& acc, int key0) {
+    if (key0 + 32 > N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
+    }
+  };
+  auto ktr4 = [&](const char* sK, int kb, bf16x8 (&f)[4]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = kb * 4096 + s2 * 2048;
+        f[2 * s2 + dt] = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
+      }
+  };
+  auto dq_mma = [&](const bf16x8 (&f)[4], const f32x16& sacc, const f32x16& dpacc) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float ds[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[8 * s2 + r]) * dpacc[8 * s2 + r];
+      const bf16x8 db = pack8f(ds);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 * s2 + dt], db, dqacc[dt], 0, 0, 0);
+    }
+  };
+  // one 64-key tile: key blocks a (0..31) and b (32..63; keys past N masked to p = 0, so every tile
+  // is branch-free but the last one's mask).  Operand reads one phase ahead of their MFMAs.
+  auto tile = [&](const char* sK, int key0) {
+    const char* sV = sK + TILE;
+    f32x16 sa, da, sb, db;
+    bf16x8 ka[4], va[4], kb_[4], vb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ka[s] = *(const bf16x8*)(sK + roff[s]);
+      va[s] = *(const bf16x8*)(sV + roff[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kb_[s] = *(const bf16x8*)(sK + 4096 + roff[s]);
+      vb[s] = *(const bf16x8*)(sV + 4096 + roff[s]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[s], s == 0 ? sinit : sa, 0, 0, 0);
+      da = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], df[s], s == 0 ? dinit : da, 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb_[s], qf[s], s == 0 ? sinit : sb, 0, 0, 0);
+      db = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb[s], df[s], s == 0 ? dinit : db, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ktr4(sK, 0, ka);
+    ktr4(sK, 1, kb_);
+    __builtin_amdgcn_sched_barrier(0);
+    if (key0 + 64 > N) {
+      mask(sa, key0);
+      mask(sb, key0 + 32);
+    }
+    dq_mma(ka, sa, da);
+    dq_mma(kb_, sb, db);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const int nkt = (N + 63) / 64;
+  load_tile(0, kv0);
+  auto iter = [&](int kt, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nkt) load_tile(kt + 1, BUF ? kv0 : kv1);
+    tile(BUF ? kv1 : kv0, kt * 64);
+  };
+  for (int kt = 0; kt < nkt; kt += 2) {
+    iter(kt, IC<0>{});
+    if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+  }
+  if (qi < N) {
+    bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(qrow + d) = pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
+                                    dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale);
+      }
+  }
+}
+
+// PKV / PQ: the pipelined (true) or the 3-wave (false) dK/dV / dQ body
+template <int WPS, bool PKV, bool PQ>
+__global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                    const bf16_t* __restrict__ dout, int64_t lddo,
+                                                                    const float* __restrict__ nlse2,
+                                                                    const float* __restrict__ ndel,
+                                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N,
+                                                                    int H, int Npad, float scale, int nblk, int skip) {
+  __shared__ __attribute__((aligned(16))) char st0[kBwdStage];
+  __shared__ __attribute__((aligned(16))) char st1[kBwdStage];
+  const int id = blockIdx.x;
+  if (skip & (id < nblk ? 1 : 2)) return;
+  if (id < nblk) {
+    if constexpr (PKV)
+      attn_bwd_dkdv_pp(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
+    else
+      attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
+  } else {
+    if constexpr (PQ)
+      attn_bwd_dq_pp(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
+                     scale);
+    else
+      attn_bwd_dq_body(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
+                       scale);
+  }
+}
+
 // ------------------------------------------------------------------ backward, one wave per SIMD
 // The same two passes as attn_bwd_dkdv_body / attn_bwd_dq_body, re-tiled for one wave per SIMD
 // (launch_bounds(256, 1): the whole register file per wave): a wave carries NB = 3 key blocks
@@ -1778,10 +2159,11 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(const bf16_t* __r
                                                                const float* __restrict__ nlse2,
                                                                const float* __restrict__ ndel,
                                                                bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H,
-                                                               int Npad, float scale, int nblk) {
+                                                               int Npad, float scale, int nblk, int skip) {
   __shared__ __attribute__((aligned(16))) char st0[kBwdStage];  // two objects: see attn_fwd_bf16_kernel
   __shared__ __attribute__((aligned(16))) char st1[kBwdStage];
   const int id = blockIdx.x;
+  if (skip & (id < nblk ? 1 : 2)) return;  // timing of one pass alone (VS_KNOB_ATTN_VARIANT bits 8, 9)
   if (id < nblk)
     attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
   else
@@ -1877,9 +2259,10 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     count_path(VS_PATH_ATTN_BWD);
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
-    // VS_KNOB_ATTN_VARIANT bits 4..7: 0 the default kernel; 1..5 the multi-block kernel with (key
+    // VS_KNOB_ATTN_VARIANT bits 4..7: 0 (default) the software-pipelined pair kernel, 9 the 3-wave kernel
+    // (3 waves per SIMD, one 32-row unit per wave: 5 % slower in the step); 1..5 the multi-block kernel with (key
     // blocks per dK/dV wave, query blocks per dQ wave, waves per SIMD) = (3, 2, 1), (1, 1, 3),
-    // (2, 2, 2), (2, 1, 2), (1, 1, 2)
+    // (2, 2, 2), (2, 1, 2), (1, 1, 2); 6: the software-pipelined pair bodies (2 waves per SIMD)
     const int bv = (knob(VS_KNOB_ATTN_VARIANT) >> 4) & 15;
     auto w1 = [&](auto kern, int nbkv, int nbq) {
       const unsigned nkv = (unsigned)(cdiv(N, 128 * nbkv) * H * B), nq = (unsigned)(cdiv(N, 128 * nbq) * H * B);
@@ -1896,11 +2279,19 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
       w1(attn_bwd_bf16_w1_kernel<2, 1, 2>, 2, 1);
     } else if (bv == 5) {
       w1(attn_bwd_bf16_w1_kernel<1, 1, 2>, 1, 1);
-    } else {
+    } else if (bv <= 0 || (bv >= 6 && bv <= 8)) {  // software-pipelined pairs (0, 6: both passes, 7: dK/dV only, 8: dQ only)
+      const unsigned g = (unsigned)(cdiv(N, 128) * H * B);
+      auto kern = attn_bwd_bf16_pp_kernel<2, true, true>;
+      if (bv == 7) kern = attn_bwd_bf16_pp_kernel<2, true, false>;
+      if (bv == 8) kern = attn_bwd_bf16_pp_kernel<2, false, true>;
+      hipLaunchKernelGGL(kern, dim3(2 * g), dim3(256), 0, s,
+                         (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv,
+                         (int)N, (int)H, (int)npad, scale, (int)g, (knob(VS_KNOB_ATTN_VARIANT) >> 8) & 3);
+    } else {  // 9: the 3-wave kernel (round-2 default)
       dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
       hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                          (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                         scale, (int)grid.x);
+                         scale, (int)grid.x, (knob(VS_KNOB_ATTN_VARIANT) >> 8) & 3);
     }
   } else if (dtype == VS_F32) {
     count_path(VS_PATH_ATTN_F32);
