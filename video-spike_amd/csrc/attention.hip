@@ -2259,11 +2259,23 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     count_path(VS_PATH_ATTN_BWD);
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
-    // VS_KNOB_ATTN_VARIANT bits 4..7: 0 (default) the software-pipelined pair kernel, 9 the 3-wave kernel
-    // (3 waves per SIMD, one 32-row unit per wave: 5 % slower in the step); 1..5 the multi-block kernel with (key
+    // VS_KNOB_ATTN_VARIANT bits 4..7: 0 (default) picks 6 or 9 by grid size; 6 the software-pipelined
+    // pair kernel, 9 the 3-wave kernel (3 waves per SIMD, one 32-row unit per wave); 1..5 the multi-block kernel with (key
     // blocks per dK/dV wave, query blocks per dQ wave, waves per SIMD) = (3, 2, 1), (1, 1, 3),
     // (2, 2, 2), (2, 1, 2), (1, 1, 2); 6: the software-pipelined pair bodies (2 waves per SIMD)
-    const int bv = (knob(VS_KNOB_ATTN_VARIANT) >> 4) & 15;
+    int bv = (knob(VS_KNOB_ATTN_VARIANT) >> 4) & 15;
+    if (bv == 0) {
+      // default by grid size: the pipelined pairs (2 waves/SIMD) when both passes fit in about two
+      // rounds of the 3-wave kernel's slots (C2 at 16 clips: 624 + 624 workgroups, 122.3 -> 116.6 us),
+      // the 3-wave kernel beyond (128 clips: 4,992 + 4,992 workgroups, 1,026 vs 924 us in
+      // profiles/r03_v5_microbench_b128.txt)
+      static const int slots = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 3 * cus;
+      }();
+      bv = cdiv(N, 128) * H * B <= slots ? 6 : 9;
+    }
     auto w1 = [&](auto kern, int nbkv, int nbq) {
       const unsigned nkv = (unsigned)(cdiv(N, 128 * nbkv) * H * B), nq = (unsigned)(cdiv(N, 128 * nbq) * H * B);
       hipLaunchKernelGGL(kern, dim3(nkv + nq), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout,
@@ -2279,7 +2291,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
       w1(attn_bwd_bf16_w1_kernel<2, 1, 2>, 2, 1);
     } else if (bv == 5) {
       w1(attn_bwd_bf16_w1_kernel<1, 1, 2>, 1, 1);
-    } else if (bv <= 0 || (bv >= 6 && bv <= 8)) {  // software-pipelined pairs (0, 6: both passes, 7: dK/dV only, 8: dQ only)
+    } else if (bv >= 6 && bv <= 8) {  // software-pipelined pairs (6: both passes, 7: dK/dV only, 8: dQ only)
       const unsigned g = (unsigned)(cdiv(N, 128) * H * B);
       auto kern = attn_bwd_bf16_pp_kernel<2, true, true>;
       if (bv == 7) kern = attn_bwd_bf16_pp_kernel<2, true, false>;

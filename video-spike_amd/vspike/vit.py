@@ -39,8 +39,12 @@ from .optim import lp_key, register_lp_shadow
 _DEFER = {"0": 0, "1": 1, "last": 2}.get(os.environ.get("VSPIKE_DEFER", "last"), 2)
 # VSPIKE_SIDE=0: no side stream (every dW product in order on the main stream), for A/B runs
 _SIDE = os.environ.get("VSPIKE_SIDE", "1") != "0"
-# VSPIKE_LN_FUSE=1: fuse the dX products with the LayerNorm backwards (VS_BWD_FUSE_LN, see vspike.h)
-_LN_FUSE = os.environ.get("VSPIKE_LN_FUSE", "0") == "1"
+# VS_BWD_FUSE_LN (the dX products fused with the LayerNorm backwards, see vspike.h): on by default from
+# _LN_FUSE_ROWS token rows (128 clips: 33.97 -> 33.70 ms/step, profiles/r03_v5_ab_b128_knobs.txt), off
+# below (16 clips: 90 us/step slower beside the side-stream dW products);
+# VSPIKE_LN_FUSE=1 / 0 forces it either way
+_LN_FUSE = {"1": True, "0": False}.get(os.environ.get("VSPIKE_LN_FUSE", ""), None)
+_LN_FUSE_ROWS = 65536
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -491,7 +495,8 @@ class VideoMAE(nn.Module):
                 gs.gemm_ws, gs.gemm_ws_bytes = g["gemm_ws"].data_ptr(), g["gemm_ws"].numel() * 4
                 # opt-in: every block but the last one defers its side-stream join to the next
                 gs.flags = ({1: L.BWD_DEFER_JOIN, 2: L.BWD_DEFER_LAST}[_DEFER] if i > 0 and _DEFER and side else 0)
-                gs.flags |= L.BWD_FUSE_LN if _LN_FUSE else 0
+                fuse_ln = _LN_FUSE if _LN_FUSE is not None else B * N >= _LN_FUSE_ROWS
+                gs.flags |= L.BWD_FUSE_LN if fuse_ln else 0
                 grads[i] = (gs, nxt)
                 cur = nxt
             gs_cache[gkey] = grads
