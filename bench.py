@@ -226,7 +226,7 @@ def _pmc_lookup(kind):
         try:
             d = json.load(open(f))
             for name, e in d["kernels"].items():
-                if name.endswith(kern[0]) and "mfma_busy_frac" in e:
+                if name.endswith(kern) and "mfma_busy_frac" in e:
                     return {"mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
                             "note": "executed MFMA cycles (the backward's dQ pass recomputes S and dP: 7 products "
                                     "executed for the 5 credited)" if kind == "attn_bwd" else "executed MFMA cycles "

@@ -11,5 +11,7 @@ scripts/gpu_steps.sh \
   "prof|240|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline" \
   "prof_serial|240|VSPIKE_SIDE=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_serial -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline"
 scripts/pmc_traffic.sh $tag
-ONLY=attn scripts/pmc_attn.sh gpurun_out/pmc_attn
-ONLY=gemm:dW scripts/pmc_attn.sh gpurun_out/pmc_dw
+ONLY=attn MB_ARGS="--batch 128 --attn-scale 0.5" scripts/pmc_attn.sh gpurun_out/pmc_attn
+ONLY=gemm:dW MB_ARGS="--batch 128" scripts/pmc_attn.sh gpurun_out/pmc_dw
+python3 scripts/pmc_json.py gpurun_out/pmc_attn gpurun_out/${tag}_pmc_attn.json
+python3 scripts/pmc_json.py gpurun_out/pmc_dw gpurun_out/${tag}_pmc_dw.json
