@@ -136,13 +136,17 @@ def test_gemm_panel_path_many_items(bkc, shape):
 @pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 192), (25088, 192, 576), (8200, 64, 128),
                                    (12345, 128, 64), (40000, 192, 128)])
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_res"])
-def test_gemm_row_slab_path(bkc, shape, epi):
+@pytest.mark.parametrize("wv", [0, 8])
+def test_gemm_row_slab_path(knobs, bkc, shape, epi, wv):
     """N <= 192 bf16 products at M >= 8192 run on the row-slab kernel (one balanced row range per
     workgroup, all N columns): the ViT block's proj / fc2 (+ bias + f32 residual) and the dX
     products (plain, f32 or bf16 out).  Ragged M (slabs of 16..17 rows), M > 32,768 (two 64-row
-    tiles per workgroup), both W layouts.  Reference: fp64 on the same bf16 inputs; tolerance 1e-5
-    of max|ref| for f32 outputs (f32 accumulation), 8e-3 for bf16 outputs (one rounding)."""
+    tiles per workgroup), both W layouts; wv = 8 forces the 8-wave / 128-row-tile variant (the
+    default from 256 rows per workgroup) on the same shapes (slabs shorter than a tile, 128-row tiles
+    with partial halves).  Reference: fp64 on the same bf16 inputs; tolerance 1e-5 of max|ref| for f32
+    outputs (f32 accumulation), 8e-3 for bf16 outputs (one rounding)."""
     from vspike import ops, _lib as L
+    knobs("slab_wv", wv)
     M, N, K = shape
     x = _rand(M, K, seed=21).to(torch.bfloat16).to(DEV)
     w = _rand(N, K, seed=22, scale=0.1).to(torch.bfloat16).to(DEV)
@@ -346,10 +350,13 @@ def test_patch_embed_gemm_pos_on_row_slab(M):
 
 @pytest.mark.parametrize("shape", [(25088, 192, 192), (9409, 192, 192), (25088, 192, 768)])
 @pytest.mark.parametrize("bias", [True, False])
-def test_gemm_ln_fwd_fused(shape, bias):
+@pytest.mark.parametrize("wv", [0, 8])
+def test_gemm_ln_fwd_fused(knobs, shape, bias, wv):
     """vs_gemm_ln_fwd: y = x W^T (+ b) + residual and h = LayerNorm(y) in one row-slab launch (the
     ViT block's proj product + layernorm_after) — bitwise the two-launch result (same epilogue order,
-    same 16-lane row layout and reduction order as ln_fwd_vec_kernel), and close to fp64."""
+    same 16-lane row layout and reduction order as ln_fwd_vec_kernel), and close to fp64; wv = 8: the
+    8-wave / 128-row-tile slab kernel."""
+    knobs("slab_wv", wv)
     from vspike import ops, _lib as L
     M, N, K = shape
     x = _rand(M, K, seed=51).to(torch.bfloat16).to(DEV)
@@ -380,14 +387,17 @@ def test_gemm_ln_fwd_fused(shape, bias):
 @pytest.mark.parametrize("shape", [(25088, 192, 768), (25088, 192, 576), (12345, 128, 64), (40000, 64, 128),
                                    (300, 192, 256)])
 @pytest.mark.parametrize("dres,lp", [(True, True), (False, False)])
-def test_gemm_ln_bwd_fused(shape, dres, lp):
+@pytest.mark.parametrize("wv", [0, 8])
+def test_gemm_ln_bwd_fused(knobs, shape, dres, lp, wv):
     """vs_gemm_ln_bwd: the block's dh = dY W product with the LayerNorm backward in its epilogue
     (fused for bf16, N <= 192, M >= 8192: ragged slabs, two tiles per workgroup at M > 32,768; the
     small case runs the unfused GEMM + vs_layernorm_bwd).  Reference: fp64 autograd of
     LayerNorm(eps 1e-12) on dh = dY W computed from the same bf16 inputs.  dx within 1e-4 of
     max|ref| (f32 arithmetic), dgamma/dbeta 1e-4 of their max (the 16-lane row sums reorder), the
-    bf16 copy within 8e-3; the fused call is bitwise reproducible."""
+    bf16 copy within 8e-3; the fused call is bitwise reproducible.  wv = 8: the 8-wave / 128-row-tile
+    slab kernel (its dgamma/dbeta partial rows sum 8 waves)."""
     from vspike import ops
+    knobs("slab_wv", wv)
     M, D, Nout = shape
     dy = _rand(M, Nout, seed=41).to(torch.bfloat16).to(DEV)
     w = _rand(Nout, D, seed=42, scale=0.05).to(torch.bfloat16).to(DEV)

@@ -864,24 +864,27 @@ struct LnBwdParams {
   float* rstd_out;
 };
 
-template <int NT, bool BKC, uint32_t EF, bool LNB = false, bool LNF = false>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __restrict__ A, int64_t lda,
+template <int NT, bool BKC, uint32_t EF, bool LNB = false, bool LNF = false, int WV = 4>
+__global__ __launch_bounds__(64 * WV, 2) __attribute__((amdgpu_waves_per_eu(WV / 2, WV / 2))) void gemm_bf16_slab_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                 const bf16_t* __restrict__ B, int64_t ldb, int64_t K,
                                                                 EpiParams e, LnBwdParams ln) {
-  using OA = OperandBf16<64, true>;
+  // WV = 4: 64-row tiles (2 x 2 waves); WV = 8: 128-row tiles (4 x 2 waves, 2 workgroups = 16 waves
+  // per CU): the W slice of a k-step (N x 64, L2) is streamed once per 128 rows instead of per 64
+  constexpr int RT = 16 * WV, NTH = 64 * WV, PR = NTH / 16;  // tile rows, threads, LN' rows per pass
+  using OA = OperandBf16<RT, true>;
   using OB = OperandBf16<64, BKC>;
   constexpr int N = 64 * NT, TM = 2, TN = NT * 2, WN = N / 2;
   constexpr int STAGE = OA::BYTES + NT * OB::BYTES;
-  constexpr int PER = OA::PPW + NT * OB::PPW;  // DMA wave-instructions per k-step
   constexpr int LDT = N + 4;
-  static_assert(64 * LDT * 4 <= 2 * STAGE, "epilogue staging fits the ring");
+  static_assert(64 * LDT * 4 <= 2 * STAGE, "epilogue staging (64 rows at a time) fits the ring");
+  static_assert(WV == 4 || WV == 8, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
   const int64_t G = gridDim.x;
   const int64_t r_begin = (int64_t)blockIdx.x * e.M / G, r_end = ((int64_t)blockIdx.x + 1) * e.M / G;
   const int nk = (int)(K / 64);
-  // LN': 16 lanes per row (lane gl owns columns 4 (gl + 16 j), j < NT), 16 rows per pass
+  // LN': 16 lanes per row (lane gl owns columns 4 (gl + 16 j), j < NT), PR rows per pass
   const int gl = tid & 15, rsub = tid >> 4;
   float4 pg[NT], pb[NT];
 #pragma unroll
@@ -890,8 +893,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
     pb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  for (int64_t m0 = r_begin; m0 < r_end; m0 += 64) {
-    const int64_t m_end = m0 + 64 < r_end ? m0 + 64 : r_end;
+  for (int64_t m0 = r_begin; m0 < r_end; m0 += RT) {
+    const int64_t m_end = m0 + RT < r_end ? m0 + RT : r_end;
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -899,9 +902,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto issue = [&](int t, char* st) {
       const int64_t k0 = (int64_t)t * 64;
-      OA::template dma<true>(st, A, lda, m0, m_end, k0, wid, lane);   // rows >= m_end re-read row m_end - 1
+      if constexpr (WV == 4) {
+        OA::template dma<true>(st, A, lda, m0, m_end, k0, wid, lane);   // rows >= m_end re-read row m_end - 1
 #pragma unroll
-      for (int j = 0; j < NT; ++j) OB::template dma<true>(st + OA::BYTES + j * OB::BYTES, B, ldb, j * 64, N, k0, wid, lane);
+        for (int j = 0; j < NT; ++j) OB::template dma<true>(st + OA::BYTES + j * OB::BYTES, B, ldb, j * 64, N, k0, wid, lane);
+      } else {
+        OA::template dma_nw<WV>(st, A, lda, m0, m_end, k0, wid, lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) OB::template dma_nw<WV>(st + OA::BYTES + j * OB::BYTES, B, ldb, j * 64, N, k0, wid, lane);
+      }
     };
     auto compute = [&](const char* sa) {
 #pragma unroll
@@ -937,27 +946,33 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
       step(t, IC<0>{});
       if (t + 1 < nk) step(t + 1, IC<1>{});
     }
-    (void)PER;
-    // epilogue: stage the f32 tile (alpha applied) over the ring, then 8-column groups per thread
-    __syncthreads();  // every wave's last MFMA operand reads are done
+    // epilogue, 64 rows at a time (the 128-row tile in two halves): the owning waves stage their f32
+    // rows (alpha applied) over the ring, then every thread takes 8-column groups / LN' rows
+    for (int hf = 0; hf < RT / 64; ++hf) {
+    const int64_t mb = m0 + hf * 64, mbe = mb + 64 < m_end ? mb + 64 : m_end;
+    if (mb >= m_end) break;  // workgroup-uniform
+    __syncthreads();  // every wave's last MFMA operand reads (or the previous half's reads) are done
     float* stg = (float*)smem;
+    if ((wr >> 1) == hf) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          stg[(wr * 32 + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
+          for (int r = 0; r < 4; ++r)
+            stg[((wr & 1) * 32 + i * 16 + (lane >> 4) * 4 + r) * LDT + wc * WN + j * 16 + (lane & 15)] = acc[i][j][r] * e.alpha;
+    }
     __syncthreads();
     if constexpr (LNB) {
       // dx = rstd (g dh - mean(g dh) - xh mean(g dh xh)) + dres, xh = (x - mu) rstd (ln_bwd_vec_kernel)
       constexpr float inv = 1.f / (float)N;
-      float4 xv[4][NT], rv[4][NT];
-      float mu[4], rs[4];
+      constexpr int NP = 64 / PR;
+      float4 xv[NP][NT], rv[NP][NT];
+      float mu[NP], rs[NP];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {  // every operand load of the 4 passes issued first
-        int64_t m = m0 + p * 16 + rsub;
-        m = m < m_end ? m : m_end - 1;
+      for (int p = 0; p < NP; ++p) {  // every operand load of the passes issued first
+        int64_t m = mb + p * PR + rsub;
+        m = m < mbe ? m : mbe - 1;
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           const int c = 4 * (gl + 16 * j);
@@ -971,10 +986,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
 #pragma unroll
       for (int j = 0; j < NT; ++j) gam[j] = *(const float4*)(ln.gamma + 4 * (gl + 16 * j));
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int rr = p * 16 + rsub;
-        const int64_t m = m0 + rr;
-        const bool valid = m < m_end;
+      for (int p = 0; p < NP; ++p) {
+        const int rr = p * PR + rsub;
+        const int64_t m = mb + rr;
+        const bool valid = m < mbe;
         float4 d[NT];
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -1027,11 +1042,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
       // y = (v + bias) + residual (epi_eight's order), stored f32; then ln_fwd_vec_kernel's LayerNorm
       // on the row held by 16 lanes (same lane layout and reduction order: bitwise the unfused result)
       constexpr float inv = 1.f / (float)N;
-      float4 rv[4][NT];
+      constexpr int NP = 64 / PR;
+      float4 rv[NP][NT];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {  // every residual load of the 4 passes issued first
-        int64_t m = m0 + p * 16 + rsub;
-        m = m < m_end ? m : m_end - 1;
+      for (int p = 0; p < NP; ++p) {  // every residual load of the passes issued first
+        int64_t m = mb + p * PR + rsub;
+        m = m < mbe ? m : mbe - 1;
 #pragma unroll
         for (int j = 0; j < NT; ++j) rv[p][j] = *(const float4*)(e.residual + m * e.ldr + 4 * (gl + 16 * j));
       }
@@ -1044,10 +1060,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
         bet[j] = *(const float4*)(ln.beta + c);
       }
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int rr = p * 16 + rsub;
-        const int64_t m = m0 + rr;
-        const bool valid = m < m_end;
+      for (int p = 0; p < NP; ++p) {
+        const int rr = p * PR + rsub;
+        const int64_t m = mb + rr;
+        const bool valid = m < mbe;
         float4 v[NT];
         float sm = 0.f;
 #pragma unroll
@@ -1094,13 +1110,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
       }
       continue;
     }
-    constexpr int CPR = N / 8, ITEMS = 64 * CPR / 256;
-    static_assert(64 * CPR % 256 == 0, "whole items per thread");
+    constexpr int CPR = N / 8, ITEMS = 64 * CPR / NTH;
+    static_assert(64 * CPR % NTH == 0, "whole items per thread");
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
-      const int idx = tid + 256 * it, rr = idx / CPR, cg = idx % CPR;
-      const int64_t m = m0 + rr;
-      if (m < m_end) {
+      const int idx = tid + NTH * it, rr = idx / CPR, cg = idx % CPR;
+      const int64_t m = mb + rr;
+      if (m < mbe) {
         const float* src = stg + rr * LDT + cg * 8;
         float v[8];
         const float4 a = *(const float4*)src;
@@ -1109,11 +1125,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
         epi_eight<EF>(e, m, (int64_t)cg * 8, v, false);
       }
     }
+    }  // halves
   }
   if constexpr (LNB) {
     // dgamma / dbeta partial row of this workgroup: the 4 row groups of a wave (lanes of equal gl),
     // then the 4 waves in wave order through LDS (fixed order: bitwise reproducible)
-    float* red = (float*)smem;  // [2][4][N]
+    float* red = (float*)smem;  // [2][WV][N]
     __syncthreads();            // the last tile's staging reads are done
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -1129,14 +1146,18 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_slab_kernel(const bf16_t* __
       VS_RED(pg[j]) VS_RED(pb[j])
 #undef VS_RED
       if (lane < 16) {
-        *(float4*)&red[(0 * 4 + wid) * N + 4 * (gl + 16 * j)] = pg[j];
-        *(float4*)&red[(1 * 4 + wid) * N + 4 * (gl + 16 * j)] = pb[j];
+        *(float4*)&red[(0 * WV + wid) * N + 4 * (gl + 16 * j)] = pg[j];
+        *(float4*)&red[(1 * WV + wid) * N + 4 * (gl + 16 * j)] = pb[j];
       }
     }
     __syncthreads();
-    for (int c = tid; c < N; c += 256) {
-      const float a = (red[0 * N + c] + red[1 * N + c]) + (red[2 * N + c] + red[3 * N + c]);
-      const float b = (red[4 * N + c] + red[5 * N + c]) + (red[6 * N + c] + red[7 * N + c]);
+    for (int c = tid; c < N; c += NTH) {
+      float a = (red[0 * N + c] + red[1 * N + c]) + (red[2 * N + c] + red[3 * N + c]);
+      float b = (red[WV * N + c] + red[(WV + 1) * N + c]) + (red[(WV + 2) * N + c] + red[(WV + 3) * N + c]);
+      if constexpr (WV == 8) {  // waves 4..7, added in the same fixed order
+        a += (red[4 * N + c] + red[5 * N + c]) + (red[6 * N + c] + red[7 * N + c]);
+        b += (red[12 * N + c] + red[13 * N + c]) + (red[14 * N + c] + red[15 * N + c]);
+      }
       ln.part[(int64_t)blockIdx.x * 2 * N + c] = a;
       ln.part[(int64_t)blockIdx.x * 2 * N + N + c] = b;
     }
@@ -1891,11 +1912,30 @@ static void launch_bf16_panel_ef(const vs_gemm_desc* d, unsigned grid, int64_t i
     hipLaunchKernelGGL((gemm_bf16_panel_kernel<KT, false, EF>), dim3(grid), dim3(256), 0, s, a, d->lda, b, d->ldb, items, e);
 }
 
+// 8 waves x 128-row tiles once a workgroup's slab holds at least two of them (M >= 131,072 rows at
+// the 512-workgroup grid: 128 clips of C2) and the W slice re-streamed per tile is the larger operand
+// stream (K >= 384); 4 waves x 64 rows otherwise (VS_KNOB_SLAB_WV forces 4 / 8).  Measured at 128
+// clips (per launch, 4 -> 8 waves): dh2 + LN2' 247 -> 218 us, dh1 + LN1' 222 -> 195, fc2 200 -> 198;
+// the K = 192 products lose (proj + LN2 102 -> 107, do 40 -> 45).
+static inline bool slab_wide(int64_t M, int64_t K, unsigned grid) {
+  const int f = knob(VS_KNOB_SLAB_WV);
+  if (f == 4 || f == 8) return f == 8;
+  return M / (int64_t)grid >= 256 && K >= 384;
+}
 template <int NT, uint32_t EF, bool LNB = false, bool LNF = false>
 static void launch_bf16_slab_ef(const vs_gemm_desc* d, unsigned grid, const EpiParams& e, hipStream_t s,
                                 const LnBwdParams& ln = LnBwdParams{}) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
+  if (slab_wide(d->M, d->K, grid)) {
+    if (d->b_kcontig)
+      hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, true, EF, LNB, LNF, 8>), dim3(grid), dim3(512), 0, s, a, d->lda, b,
+                         d->ldb, d->K, e, ln);
+    else
+      hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, false, EF, LNB, LNF, 8>), dim3(grid), dim3(512), 0, s, a, d->lda, b,
+                         d->ldb, d->K, e, ln);
+    return;
+  }
   if (d->b_kcontig)
     hipLaunchKernelGGL((gemm_bf16_slab_kernel<NT, true, EF, LNB, LNF>), dim3(grid), dim3(256), 0, s, a, d->lda, b,
                        d->ldb, d->K, e, ln);
