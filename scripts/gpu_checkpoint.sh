@@ -10,6 +10,7 @@ scripts/gpu_steps.sh \
   "bench|300|python bench.py" \
   "prof|240|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline" \
   "prof_serial|240|VSPIKE_SIDE=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_serial -o run -- python3 bench.py --steps 5 --warmup 2 --profile-steps 0 --no-cpu-baseline"
+timeout -k 10 90 python3 scripts/store_rate.py > gpurun_out/${tag}_store_rate.txt 2>&1
 scripts/pmc_traffic.sh $tag
 ONLY=attn MB_ARGS="--batch 128 --attn-scale 0.5" scripts/pmc_attn.sh gpurun_out/pmc_attn
 ONLY=gemm:dW MB_ARGS="--batch 128" scripts/pmc_attn.sh gpurun_out/pmc_dw

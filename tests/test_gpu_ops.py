@@ -220,13 +220,16 @@ def test_gemm_wide_row_slab_path(bkc, shape, epi):
 @pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape", [(8269, 384, 192), (25093, 576, 192), (25088, 768, 192)])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gelu_bwd", "none", "gelu_grad", "mul_aux"])
-def test_gemm_w_resident_path(knobs, bkc, shape, epi):
+@pytest.mark.parametrize("wv", [0, 8])
+def test_gemm_w_resident_path(knobs, bkc, shape, epi, wv):
     """K = 192, N a multiple of 192 (qkv, fc1 + GELU, the GELU' product) run on the W-resident kernel
     (W part in LDS once per workgroup, permuted rows so a lane stores 8 consecutive columns, ragged
     row ranges / token blocks): fp64 reference on the same bf16 inputs (tolerances as the wide
-    row-slab test), and the same values as the tile kernels (knob no_wres) to bf16 rounding."""
+    row-slab test), and the same values as the tile kernels (knob no_wres) to bf16 rounding; both
+    workgroup sizes (4 and 8 waves sharing one W part)."""
     from vspike import ops, _lib as L
     knobs("wres_gbwd", 1)   # the GELU' product too (off by default)
+    knobs("wres_wv", wv)    # 4 waves per workgroup at these row counts, or the 8-wave variant
     M, N, K = shape
     x = _rand(M, K, seed=41).to(torch.bfloat16).to(DEV)
     w = _rand(N, K, seed=42, scale=0.1).to(torch.bfloat16).to(DEV)
@@ -605,12 +608,13 @@ def _attn_ref(qkv, B, N, H, scale=0.125):
 ATTN_SHAPES = [(1, 100, 1), (2, 196, 2), (1, 1568, 3), (2, 130, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4])
+@pytest.mark.parametrize("variant", [0, 1, 4, 6])
 @pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1)])
 def test_attention_fwd_variants(knobs, variant, shape):
     """The bf16 forward kernels (VS_KNOB_ATTN_VARIANT low nibble: 0 = 3 waves/SIMD x 32 rows; 1 = one
     wave per SIMD x 96 rows, 3-stage K/V ring, S(i+1) issued before softmax(i); 4 = that body at 32
-    rows per wave and 2 waves per SIMD) against fp64 on the same bf16 inputs, at tails of
+    rows per wave and 2 waves per SIMD; 6 = the default body with PV(a) issued before QK(b)) against
+    fp64 on the same bf16 inputs, at tails of
     every kind: N = 1 / 33 / 100 / 130 / 196 (partial 32-key block), 1568 (= 4 x 384 + 32: a
     workgroup with one live q-block), 1600 (partial 64-key tile), 3136 (C5: 98 blocks)."""
     from vspike import ops

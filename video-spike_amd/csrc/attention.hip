@@ -356,6 +356,8 @@ __device__ __forceinline__ bf16x8 rowsum_selector(int lane) {
   return __builtin_convertvector(v, bf16x8);
 }
 
+// SW: QK(b) is issued before PV(a), so softmax(b) waits on a chain that ran under PV(a)'s MFMAs
+template <bool SW = false>
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                bf16_t* __restrict__ o, int64_t ldo,
                                                                float* __restrict__ lse, int N, int H,
@@ -563,13 +565,26 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
         __builtin_amdgcn_sched_barrier(0);
         bf16x8 a0, a1;
         softmax(safec, sa, kt * 64, kt == 0, a0, a1);
-        pv(va, a0, a1);
-        f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        const VFrag vb = vread(cur, 1);
-        __builtin_amdgcn_sched_barrier(0);
+        f32x16 sb;
+        VFrag vb;
+        if constexpr (SW) {
+          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
 #pragma unroll
-        for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+          for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          vb = vread(cur, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          pv(va, a0, a1);
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          pv(va, a0, a1);
+          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          vb = vread(cur, 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+        }
         softmax(safec, sb, kt * 64 + 32, false, b0, b1);
         __builtin_amdgcn_sched_barrier(0);
         if (kt + 1 < nkt) {
@@ -2195,7 +2210,9 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
     count_path(VS_PATH_ATTN_FWD);
     // VS_KNOB_ATTN_VARIANT low nibble: 0 the default kernel; 1..3 the software-pipelined kernel with
-    // (query blocks per wave, waves per SIMD) = (3, 1), (1, 3), (2, 2), (1, 2)
+    // (query blocks per wave, waves per SIMD) = (3, 1), (1, 3), (2, 2), (1, 2); 6: the default kernel
+    // with PV(a) issued before QK(b) (round-2 order; 5 = the default, QK(b) ahead of PV(a): 299 -> 252 us
+    // back to back at 128 clips, neutral inside the step)
     const int fv = knob(VS_KNOB_ATTN_VARIANT) & 15;
     auto w1 = [&](auto kern, int nqb) {
       dim3 grid((unsigned)(cdiv(N, 128 * nqb) * H * B));
@@ -2212,7 +2229,8 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
       w1(attn_fwd_bf16_w1_kernel<1, 2>, 1);
     } else {
       dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-      hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o,
+      auto kern = fv == 6 ? attn_fwd_bf16_kernel<false> : attn_fwd_bf16_kernel<true>;
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o,
                          lse, (int)N, (int)H, scale * kLog2e);
     }
   } else if (dtype == VS_F32) {

@@ -1363,8 +1363,8 @@ __device__ __forceinline__ int wres_lds_row(int n) {
   return ch * 64 + (2 * p + ((q >> 2) & 1)) * 16 + 4 * (q >> 3) + (q & 3);
 }
 
-template <bool BKC, uint32_t EF>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __restrict__ A, int64_t lda,
+template <bool BKC, uint32_t EF, int WV = 4>
+__global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                 const bf16_t* __restrict__ B, int64_t ldb,
                                                                 EpiParams e) {
   constexpr int K = 192, KS = K / 32, NCH = kWresNH / 64;
@@ -1383,29 +1383,30 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __
 
   // ---- W part -> LDS (permuted rows), once: every thread issues all 18 of its 16-B loads before
   // its first LDS write (a load -> write chain per chunk serialises 18 HBM latencies)
-  constexpr int FILL = kWresNH * K / 8 / 256;  // 16-B chunks per thread
-  static_assert(FILL * 256 * 8 == kWresNH * K, "fill split");
+  constexpr int NTH = 64 * WV;
+  constexpr int FILL = kWresNH * K / 8 / NTH;  // 16-B chunks per thread
+  static_assert(FILL * NTH * 8 == kWresNH * K, "fill split");
   uint4 fv[FILL];
   if constexpr (BKC) {  // W[n][k]: 24 16-B chunks per row
 #pragma unroll
     for (int i = 0; i < FILL; ++i) {
-      const int c = tid + 256 * i, n = c / (K / 8), kc = c % (K / 8);
+      const int c = tid + NTH * i, n = c / (K / 8), kc = c % (K / 8);
       fv[i] = *(const uint4*)(B + (n_part + n) * ldb + kc * 8);
     }
 #pragma unroll
     for (int i = 0; i < FILL; ++i) {
-      const int c = tid + 256 * i, n = c / (K / 8), kc = c % (K / 8);
+      const int c = tid + NTH * i, n = c / (K / 8), kc = c % (K / 8);
       *(uint4*)(wl + wres_lds_row(n) * kWresRow + kc * 16) = fv[i];
     }
   } else {  // W[k][n] (N-contiguous): 8 columns per 16-B load, scattered into 8 LDS rows
 #pragma unroll
     for (int i = 0; i < FILL; ++i) {
-      const int c = tid + 256 * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
+      const int c = tid + NTH * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
       fv[i] = *(const uint4*)(B + (int64_t)k * ldb + n_part + nc * 8);
     }
 #pragma unroll
     for (int i = 0; i < FILL; ++i) {
-      const int c = tid + 256 * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
+      const int c = tid + NTH * i, k = c / (kWresNH / 8), nc = c % (kWresNH / 8);
       const uint32_t w[4] = {fv[i].x, fv[i].y, fv[i].z, fv[i].w};
 #pragma unroll
       for (int t = 0; t < 8; ++t)
@@ -1424,7 +1425,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_wres_kernel(const bf16_t* __
   const int64_t rows = r_end - r_begin;
   const int tb_n = (int)((rows + 15) / 16);
   const int units = tb_n * NCH;
-  const int u0 = wid * units / 4, u1 = (wid + 1) * units / 4;
+  const int u0 = wid * units / WV, u1 = (wid + 1) * units / WV;
   const int g = lane >> 4, tok = lane & 15;
   const char* wbase = wl + tok * kWresRow + g * 16;  // + (tile row block) * kWresRow, + ks * 64
   auto load_x = [&](int tb, bf16x8 (&dst)[KS]) {
@@ -1979,10 +1980,14 @@ template <uint32_t EF>
 static void launch_bf16_wres_ef(const vs_gemm_desc* d, const EpiParams& e, hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
-  if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_wres_kernel<true, EF>), dim3(512), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
-  else
-    hipLaunchKernelGGL((gemm_bf16_wres_kernel<false, EF>), dim3(512), dim3(256), 0, s, a, d->lda, b, d->ldb, e);
+  // VSPIKE_WRES_WV=8: 8 waves per workgroup (16 per CU sharing 2 W parts; the GELU' / aux-product
+  // instantiations need > 128 VGPRs, so one workgroup per CU there).  Measured at 128 clips: qkv
+  // 94.3 -> 95.2 us, fc1 + GELU 216 -> 225 us (more waves do not raise the store-bound rate): 4 waves.
+  const bool wide = knob(VS_KNOB_WRES_WV) == 8;
+  void (*kern)(const bf16_t*, int64_t, const bf16_t*, int64_t, EpiParams);
+  if (d->b_kcontig) kern = wide ? gemm_bf16_wres_kernel<true, EF, 8> : gemm_bf16_wres_kernel<true, EF, 4>;
+  else kern = wide ? gemm_bf16_wres_kernel<false, EF, 8> : gemm_bf16_wres_kernel<false, EF, 4>;
+  hipLaunchKernelGGL(kern, dim3(512), dim3(wide ? 512 : 256), 0, s, a, d->lda, b, d->ldb, e);
 }
 
 template <uint32_t EF>
