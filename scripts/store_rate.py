@@ -15,7 +15,7 @@ def rate(fn, nbytes, reps=20):
     e.record()
     torch.cuda.synchronize()
     us = 1e3 * s.elapsed_time(e) / reps
-    return us, nbytes / us / 1e3
+    return us, nbytes / us / 1e6
 
 
 def main():
