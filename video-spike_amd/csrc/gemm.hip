@@ -1353,7 +1353,11 @@ __global__ __launch_bounds__(256, 2) void patch_embed_fwd_kernel(const float* __
 //     16-B vectors, no staging.  The GELU' operand of a chunk is loaded before its MFMAs.
 // ----------------------------------------------------------------------------------------------
 constexpr int kWresNH = 192;                  // columns per part
-constexpr int kWresRow = 192 * 2 + 16;        // LDS bytes per W row (K = 192, +16 B: bank spread)
+// LDS bytes per W row: K = 192 plus 32 B.  A ds_read_b128 of the MFMA A fragment (row = lane & 15,
+// 16-B chunk 4 ks + lane / 16) is serviced in four 16-lane groups; a row stride of 104 dwords puts the
+// 16 chunks of every group on distinct 4-bank quads (the 400-B stride collided in half of them:
+// SQ_LDS_BANK_CONFLICT 46 % of the LDS cycles at 128 clips).  2 x (192 x 416 + 768) B fits 160 KiB.
+constexpr int kWresRow = 192 * 2 + 32;
 
 // LDS row of part-local column n: chunk ch = n / 64; within it MFMA tile jj = 2 (r / 32) + (r % 8) / 4
 // and tile row i = 4 ((r % 32) / 8) + r % 4 (r = n % 64), so that accumulator rows 4g..4g+3 of
@@ -1366,13 +1370,14 @@ __device__ __forceinline__ int wres_lds_row(int n) {
 template <bool BKC, uint32_t EF, int WV = 4>
 __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                 const bf16_t* __restrict__ B, int64_t ldb,
-                                                                EpiParams e) {
+                                                                EpiParams e, int dbg) {
   constexpr int K = 192, KS = K / 32, NCH = kWresNH / 64;
   constexpr bool MULA = (EF & VS_EPI_MUL_AUX) != 0;             // v *= aux (the stored gelu')
   constexpr bool GBWD = (EF & VS_EPI_GELU_BWD) != 0 || MULA;    // an aux operand per output
   __shared__ __attribute__((aligned(16))) char wl[kWresNH * kWresRow];
   __shared__ __attribute__((aligned(16))) float bl[kWresNH];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wave-uniform work bounds (readfirstlane): the block and chunk loops run on scalar counters
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int parts = (int)(e.N / kWresNH);
   const int G = gridDim.x, ranges = G / parts;
   const int logical = xcd_remap(blockIdx.x, G);
@@ -1420,45 +1425,69 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
   }
   __syncthreads();
 
-  // ---- this wave's units: (16-token block, 64-column chunk), chunk-minor; the next block's
-  // operand rows are loaded while this block's chunks run
+  // ---- this wave's 16-token blocks (all NCH 64-column chunks of each); the next block's operand
+  // rows are loaded while this block's chunks run
   const int64_t rows = r_end - r_begin;
   const int tb_n = (int)((rows + 15) / 16);
-  const int units = tb_n * NCH;
-  const int u0 = wid * units / WV, u1 = (wid + 1) * units / WV;
+  const int tb0 = wid * tb_n / WV, tb1 = (wid + 1) * tb_n / WV - 1;
   const int g = lane >> 4, tok = lane & 15;
   const char* wbase = wl + tok * kWresRow + g * 16;  // + (tile row block) * kWresRow, + ks * 64
-  auto load_x = [&](int tb, bf16x8 (&dst)[KS]) {
-    int64_t m = r_begin + (int64_t)tb * 16 + tok;
-    m = m < r_end ? m : r_end - 1;  // rows past the range: its last row (never stored)
-    const bf16_t* p = A + m * lda + 8 * g;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) dst[ks] = *(const bf16x8*)(p + 32 * ks);
+  if (tb0 > tb1) return;
+  // Every global access goes through a buffer descriptor whose base is the token block's first row
+  // (wave-uniform: the per-block address arithmetic is scalar) and whose extent ends at r_end: loads
+  // of rows past the range return 0 and their stores are dropped by the range check, so no lane
+  // predicate or branch remains, and hipcc sees one fixed sequence of loads and stores per block
+  // (counted vmcnt waits).  Per lane only constant 32-bit offsets (+ immediates).  The host keeps
+  // M x ld x 2 bytes below 2^31 for every operand.
+  const uint32_t xoff = (uint32_t)(tok * lda + 8 * g) * 2u;
+  const uint32_t coff = (uint32_t)(tok * e.ldc + n_part + 8 * g) * 2u;
+  const uint32_t aooff = (uint32_t)(tok * e.ld_aux_out + n_part + 8 * g) * 2u;
+  const uint32_t aioff = (uint32_t)(tok * e.ld_aux_in + n_part + 8 * g) * 2u;
+  auto rsrc = [&](const void* base, int64_t row0, int64_t ld, bool live = true) {
+    const int64_t left = live ? r_end - row0 : 0;  // a dead block: every store dropped
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(left * ld * 2), 0x00020000);
   };
-  if (u0 >= u1) return;
-  const int tb0 = u0 / NCH, tb1 = (u1 - 1) / NCH;
-  bf16x8 xf[KS], xn[KS];
-  load_x(tb0, xn);
-  for (int tb = tb0; tb <= tb1; ++tb) {
+  // x fragments held as 32-bit vectors (bf16 vector copies were re-packed lane half by lane half)
+  auto load_x = [&](int tb, u32x4v (&dst)[KS]) {
+    const int64_t row0 = r_begin + (int64_t)(dbg & 2 ? 0 : tb) * 16;  // dbg & 2 (timing): L2-resident reads
+    const auto rx = rsrc(A + row0 * lda, row0, lda);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) xf[ks] = xn[ks];
-    if (tb < tb1) load_x(tb + 1, xn);
-    const int64_t m = r_begin + (int64_t)tb * 16 + tok;
-    const bool mok = m < r_end;
-    const int c0 = tb == tb0 ? u0 - tb * NCH : 0, c1 = tb == tb1 ? u1 - tb * NCH : NCH;
+    for (int ks = 0; ks < KS; ++ks) dst[ks] = __builtin_amdgcn_raw_buffer_load_b128(rx, xoff + 64 * ks, 0, 0);
+  };
+  auto pack8 = [](const float (&v)[8]) {
+    u32x4v u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      u[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2v));
+    return u;
+  };
+  // two fragment sets, the loop unrolled by two token blocks: no register copy per block
+  u32x4v xa[KS], xb[KS];
+  load_x(tb0, xa);
+  auto block = [&](int tb, const u32x4v (&xf)[KS], u32x4v (&xn)[KS], bool live) {
+    // compiler barrier: the W fragment reads are loop-invariant, and hoisted out of the block loop
+    // they need 288 VGPRs (spills); re-read per block from LDS instead
+    asm volatile("" ::: "memory");
+    // unconditional (the last block re-loads itself): with a conditional prefetch the path without
+    // it made hipcc wait vmcnt(0) for this block's fragments, i.e. for the prefetch just issued too
+    load_x(tb < tb1 ? tb + 1 : tb1, xn);
+    __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out first, ahead of this block's work
+    const int64_t row0 = r_begin + (int64_t)tb * 16;
+    // dbg & 1 (timing only): every block's stores rewrite the range's first two blocks (L2-resident)
+    const int64_t srow0 = dbg & 1 ? r_begin + (int64_t)(tb & 1) * 16 : row0;
+    const auto rc = rsrc((const bf16_t*)e.c + srow0 * e.ldc, srow0, e.ldc, live);
+    const auto rao = rsrc((const bf16_t*)e.aux_out + srow0 * e.ld_aux_out, srow0, e.ld_aux_out, live);
+    const auto rai = rsrc((const bf16_t*)e.aux_in + row0 * e.ld_aux_in, row0, e.ld_aux_in);
     // GELU' operand: chunk c + 1's is loaded before chunk c's stores (a counted wait then skips them)
-    uint4 aux[2][2];
-    auto load_aux = [&](int ch, uint4 (&dst)[2]) {
+    u32x4v aux[2][2];
+    auto load_aux = [&](int ch, u32x4v (&dst)[2]) {
       if constexpr (GBWD) {
-        const int64_t n0 = n_part + ch * 64 + 8 * g;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
-          dst[p] = mok ? *(const uint4*)((const bf16_t*)e.aux_in + m * e.ld_aux_in + n0 + 32 * p) : make_uint4(0, 0, 0, 0);
+        for (int p = 0; p < 2; ++p) dst[p] = __builtin_amdgcn_raw_buffer_load_b128(rai, aioff + 2 * (ch * 64 + 32 * p), 0, 0);
       }
     };
-    auto chunk = [&](int ch, uint4 (&ax)[2], uint4 (&axn)[2]) {
-      if (ch + 1 < c1) load_aux(ch + 1, axn);
-      const int64_t n0 = n_part + ch * 64 + 8 * g;  // this lane's columns: n0 .. n0 + 7 and n0 + 32 ..
+    auto chunk = [&](int ch, u32x4v (&ax)[2], u32x4v (&axn)[2]) {
+      if (ch + 1 < NCH) load_aux(ch + 1, axn);
       f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1468,20 +1497,21 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
 #pragma unroll
         for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(wbase + (ch * 64 + j * 16) * kWresRow + ks * 64);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[ks], acc[j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], __builtin_bit_cast(bf16x8, xf[ks]), acc[j], 0, 0, 0);
       }
-      if (!mok) return;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
+        // this lane's 8 columns: n_part + ch * 64 + 32 p + 8 g .. + 7 of token row row0 + tok
+        const uint32_t cb = 2 * (ch * 64 + 32 * p);
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = acc[2 * p][r] * e.alpha;
           v[4 + r] = acc[2 * p + 1][r] * e.alpha;
         }
-        bf16_t* crow = (bf16_t*)e.c + m * e.ldc + n0 + 32 * p;
         if constexpr (GBWD) {
-          const uint32_t w[4] = {ax[p].x, ax[p].y, ax[p].z, ax[p].w};
+          const u32x4v w = ax[p];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float lo = __uint_as_float(w[q] << 16), hi = __uint_as_float(w[q] & 0xffff0000u);
@@ -1499,21 +1529,31 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
             float gr[8];  // gelu' of the bf16-rounded pre-activation: what the backward multiplies by
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = gelu_fast_both(bf2f(f2bf(v[k])), gr[k]);
-            st8((bf16_t*)e.aux_out + m * e.ld_aux_out + n0 + 32 * p, 0, 1, gr);
+            __builtin_amdgcn_raw_buffer_store_b128(pack8(gr), rao, aooff + cb, 0, 0);
           } else if constexpr ((EF & VS_EPI_GELU) != 0) {
-            st8((bf16_t*)e.aux_out + m * e.ld_aux_out + n0 + 32 * p, 0, 1, v);
+            __builtin_amdgcn_raw_buffer_store_b128(pack8(v), rao, aooff + cb, 0, 0);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = gelu_fast(bf2f(f2bf(v[k])));  // GELU of the stored value
           }
         }
-        st8(crow, 0, 1, v);
+        __builtin_amdgcn_raw_buffer_store_b128(pack8(v), rc, coff + cb, 0, 0);
       }
     };
-    load_aux(c0, aux[0]);
-    for (int ch = c0; ch < c1; ch += 2) {
-      chunk(ch, aux[0], aux[1]);
-      if (ch + 1 < c1) chunk(ch + 1, aux[1], aux[0]);
-    }
+    // the chunks unrolled and unconditional (no inner loop: hipcc waits vmcnt(0) before a loop that
+    // reads a pending load, i.e. for the next block's prefetch too), so every block issues the same
+    // loads and stores and the waits before its MFMAs count past the previous block's stores
+    load_aux(0, aux[0]);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) chunk(ch, aux[ch & 1], aux[(ch + 1) & 1]);
+  };
+  // The first block peeled (every entry into the loop then follows a block's stores), then pairs of
+  // blocks, both unconditional: a conditional second block let hipcc sink the first block's prefetch
+  // into it (its only user), i.e. issue it right before its use.  An odd count ends with one dead
+  // block (its stores dropped by an empty descriptor).
+  block(tb0, xa, xb, true);
+  for (int tb = tb0 + 1; tb <= tb1; tb += 2) {
+    block(tb, xb, xa, true);
+    block(tb + 1, xa, xb, tb + 1 <= tb1);
   }
 }
 
@@ -1976,6 +2016,13 @@ static void launch_bf16_wslab(const vs_gemm_desc* d, unsigned grid, const EpiPar
   }
 }
 
+// the W-resident kernel addresses every operand through 32-bit buffer descriptors
+static inline bool wres_extent_ok(int64_t M, std::initializer_list<int64_t> lds) {
+  for (int64_t ld : lds)
+    if (M * ld * 2 >= ((int64_t)1 << 31)) return false;
+  return true;
+}
+
 template <uint32_t EF>
 static void launch_bf16_wres_ef(const vs_gemm_desc* d, const EpiParams& e, hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
@@ -1984,10 +2031,10 @@ static void launch_bf16_wres_ef(const vs_gemm_desc* d, const EpiParams& e, hipSt
   // instantiations need > 128 VGPRs, so one workgroup per CU there).  Measured at 128 clips: qkv
   // 94.3 -> 95.2 us, fc1 + GELU 216 -> 225 us (more waves do not raise the store-bound rate): 4 waves.
   const bool wide = knob(VS_KNOB_WRES_WV) == 8;
-  void (*kern)(const bf16_t*, int64_t, const bf16_t*, int64_t, EpiParams);
+  void (*kern)(const bf16_t*, int64_t, const bf16_t*, int64_t, EpiParams, int);
   if (d->b_kcontig) kern = wide ? gemm_bf16_wres_kernel<true, EF, 8> : gemm_bf16_wres_kernel<true, EF, 4>;
   else kern = wide ? gemm_bf16_wres_kernel<false, EF, 8> : gemm_bf16_wres_kernel<false, EF, 4>;
-  hipLaunchKernelGGL(kern, dim3(512), dim3(wide ? 512 : 256), 0, s, a, d->lda, b, d->ldb, e);
+  hipLaunchKernelGGL(kern, dim3(512), dim3(wide ? 512 : 256), 0, s, a, d->lda, b, d->ldb, e, knob(VS_KNOB_WRES_DBG));
 }
 
 template <uint32_t EF>
@@ -2346,7 +2393,8 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
                        e.op_bf16 && e.out_bf16;
     if (!no_wres && ef_ok && d->dtype == VS_BF16 && d->a_kcontig && d->K == 192 && d->N % kWresNH == 0 &&
         d->N >= 2 * kWresNH && d->N <= 64 * kWresNH && d->M >= 8192 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->lda % 8 == 0 &&
-        d->ldb % 8 == 0 && aligned16(d->a) && aligned16(d->b)) {
+        d->ldb % 8 == 0 && aligned16(d->a) && aligned16(d->b) &&
+        wres_extent_ok(d->M, {d->lda, d->ldc, e.aux_out ? e.ld_aux_out : 0, e.aux_in ? e.ld_aux_in : 0})) {
       count_path(VS_PATH_GEMM_WRES);
       if (f == VS_EPI_BIAS) launch_bf16_wres_ef<(uint32_t)VS_EPI_BIAS>(d, e, s);
       else if (f == (VS_EPI_BIAS | VS_EPI_GELU)) launch_bf16_wres_ef<(uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)>(d, e, s);
