@@ -1444,7 +1444,8 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
   const uint32_t aooff = (uint32_t)(tok * e.ld_aux_out + n_part + 8 * g) * 2u;
   const uint32_t aioff = (uint32_t)(tok * e.ld_aux_in + n_part + 8 * g) * 2u;
   auto rsrc = [&](const void* base, int64_t row0, int64_t ld, bool live = true) {
-    const int64_t left = live ? r_end - row0 : 0;  // a dead block: every store dropped
+    // a dead block (or one starting past the range): an empty descriptor, loads give 0, stores dropped
+    const int64_t left = live && r_end > row0 ? r_end - row0 : 0;
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(left * ld * 2), 0x00020000);
   };
   // x fragments held as 32-bit vectors (bf16 vector copies were re-packed lane half by lane half)
@@ -1461,16 +1462,18 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
       u[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2v));
     return u;
   };
-  // two fragment sets, the loop unrolled by two token blocks: no register copy per block
-  u32x4v xa[KS], xb[KS];
+  // three fragment sets, prefetch two token blocks ahead (one block of MFMA work, ~0.5 us, hid too
+  // little of the loaded HBM latency), the loop unrolled by three blocks: no register copies
+  u32x4v xa[KS], xb[KS], xc[KS];
   load_x(tb0, xa);
+  load_x(tb0 < tb1 ? tb0 + 1 : tb1, xb);
   auto block = [&](int tb, const u32x4v (&xf)[KS], u32x4v (&xn)[KS], bool live) {
     // compiler barrier: the W fragment reads are loop-invariant, and hoisted out of the block loop
     // they need 288 VGPRs (spills); re-read per block from LDS instead
     asm volatile("" ::: "memory");
     // unconditional (the last block re-loads itself): with a conditional prefetch the path without
     // it made hipcc wait vmcnt(0) for this block's fragments, i.e. for the prefetch just issued too
-    load_x(tb < tb1 ? tb + 1 : tb1, xn);
+    load_x(tb + 2 <= tb1 ? tb + 2 : tb1, xn);
     __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out first, ahead of this block's work
     const int64_t row0 = r_begin + (int64_t)tb * 16;
     // dbg & 1 (timing only): every block's stores rewrite the range's first two blocks (L2-resident)
@@ -1546,14 +1549,15 @@ __global__ __launch_bounds__(64 * WV, 2) void gemm_bf16_wres_kernel(const bf16_t
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) chunk(ch, aux[ch & 1], aux[(ch + 1) & 1]);
   };
-  // The first block peeled (every entry into the loop then follows a block's stores), then pairs of
-  // blocks, both unconditional: a conditional second block let hipcc sink the first block's prefetch
-  // into it (its only user), i.e. issue it right before its use.  An odd count ends with one dead
-  // block (its stores dropped by an empty descriptor).
-  block(tb0, xa, xb, true);
-  for (int tb = tb0 + 1; tb <= tb1; tb += 2) {
+  // The first block peeled (every entry into the loop then follows a block's stores), then triples
+  // of blocks, all unconditional: a conditional block let hipcc sink the previous blocks' prefetch
+  // into it (its only user), i.e. issue it right before its use.  A count that is not a multiple of
+  // three ends with dead blocks (their stores dropped by an empty descriptor).
+  block(tb0, xa, xc, true);
+  for (int tb = tb0 + 1; tb <= tb1; tb += 3) {
     block(tb, xb, xa, true);
-    block(tb + 1, xa, xb, tb + 1 <= tb1);
+    block(tb + 1, xc, xb, tb + 1 <= tb1);
+    block(tb + 2, xa, xc, tb + 2 <= tb1);
   }
 }
 
