@@ -94,48 +94,64 @@ def _cpu_model_name():
 
 
 def cpu_baseline(cfg, params, pixels, target, seconds):
-    """BASELINE.md CPU plan: the oracle (torch-CPU fp32 restatement of the step) per clip, fwd and
-    fwd+bwd at B=1 and B=4, median of up to 5 runs after one warm-up, on the host threads this
-    process may use (the box's OMP_NUM_THREADS share; `nproc` there counts the whole machine)."""
+    """BASELINE.md CPU plan (BASELINE.md:37): the oracle (torch-CPU fp32 restatement of the step) per
+    clip, fwd and fwd+bwd at B=1 and B=4, on `os.cpu_count()` threads, median of >= 5 runs after two
+    warm-ups per cell (the first call of a shape pays one-off costs: allocator growth, first-touch page
+    faults, oneDNN primitive creation; round 3's single warm-up left B=1 slower per clip than B=4).
+    The box's OMP_NUM_THREADS share (16) is timed the same way and reported beside it; `value` is
+    the B=4 fwd+bwd rate on the thread count that ran it faster.  Each cell reports its median, min
+    and max (the spread) and the cells are checked for monotonicity (fwd+bwd slower than fwd, B=4
+    no slower per clip than B=1 by more than the spread)."""
     from oracle import cpu_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    torch.set_num_threads(threads)
+    counts = []
+    for t in (os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)):
+        if t > 0 and t not in counts:
+            counts.append(t)
     P = cpu_ref.to_torch(params)
-    res, t_start, budget_left = {}, time.perf_counter(), seconds
-    loss4 = None
-    for B in (1, 4):
-        px, y = pixels[:B], target[:B]
-        for mode in ("fwd", "fwd_bwd"):
-            def run():
-                if mode == "fwd":
-                    with torch.no_grad():
-                        return cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
-                loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
-                loss.backward()
-                for p in P.values():
-                    p.grad = None
-                return loss.detach()
-            t0 = time.perf_counter()
-            loss = run()                                        # warm-up
-            w = time.perf_counter() - t0
-            if B == 4 and mode == "fwd":
-                loss4 = float(loss)
-            left = max(budget_left - (time.perf_counter() - t_start), 0.0)
-            reps = int(max(1, min(5, left / 4 / max(w, 1e-3))))
-            ts = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                run()
-                ts.append(time.perf_counter() - t0)
-            res[f"B{B}_{mode}_s_per_clip"] = round(statistics.median(ts) / B, 4)
-            res[f"B{B}_{mode}_runs"] = reps
+    t_start = time.perf_counter()
+    per_count, loss4 = {}, None
+    for threads in counts:
+        torch.set_num_threads(threads)
+        res = {}
+        for B in (1, 4):
+            px, y = pixels[:B], target[:B]
+            for mode in ("fwd", "fwd_bwd"):
+                def run():
+                    if mode == "fwd":
+                        with torch.no_grad():
+                            return cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                    loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                    loss.backward()
+                    for p in P.values():
+                        p.grad = None
+                    return loss.detach()
+                for _ in range(2):                                   # warm-ups
+                    loss = run()
+                if B == 4 and mode == "fwd":
+                    loss4 = float(loss)
+                ts = []
+                for _ in range(5):
+                    t0 = time.perf_counter()
+                    run()
+                    ts.append((time.perf_counter() - t0) / B)
+                res[f"B{B}_{mode}"] = {"s_per_clip": round(statistics.median(ts), 4), "min": round(min(ts), 4),
+                                       "max": round(max(ts), 4), "runs": len(ts)}
+        c = lambda k: res[k]["s_per_clip"]  # noqa: E731
+        res["monotone"] = bool(c("B1_fwd_bwd") > c("B1_fwd") and c("B4_fwd_bwd") > c("B4_fwd") and
+                               c("B4_fwd") <= res["B1_fwd"]["max"] and c("B4_fwd_bwd") <= res["B1_fwd_bwd"]["max"])
+        per_count[str(threads)] = res
+        if time.perf_counter() - t_start > seconds:
+            break                                   # bounded: the first count (os.cpu_count()) always runs
     elapsed = time.perf_counter() - t_start
-    value = 1.0 / res["B4_fwd_bwd_s_per_clip"]
-    out = {"value": round(value, 4), "unit": "clips/sec", "cores": threads, "kind": "port",
-           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of "
-                     f"{res['B4_fwd_bwd_runs']} after 1 warm-up ({elapsed:.1f} s of CPU work in all)",
-           "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(), "threads_used": threads},
-           "detail": res}
+    best = min(per_count, key=lambda k: per_count[k]["B4_fwd_bwd"]["s_per_clip"])
+    value = 1.0 / per_count[best]["B4_fwd_bwd"]["s_per_clip"]
+    out = {"value": round(value, 4), "unit": "clips/sec", "cores": int(best), "kind": "port",
+           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of 5 after 2 warm-ups, "
+                     f"{best} threads (also timed: {', '.join(k for k in per_count if k != best) or 'none'}); "
+                     f"{elapsed:.1f} s of CPU work in all",
+           "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(),
+                    "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
+           "detail": per_count}
     return out, loss4
 
 
@@ -152,10 +168,11 @@ def _reference_grads(model):
     return out
 
 
-# bf16 bars of the full-batch check: 2x the worst values measured at the bench geometry
-# (tests/test_gpu_parity_bench.py holds the same numbers for the B=16 fixture)
+# bf16 bars of the full-batch check: about 2x the worst values measured at the bench geometry
+# (r03 on MI355X at 128 clips: log-rates 3.4e-3, loss 1.8e-5, worst gradient 4.6e-3); a failed check
+# makes bench.py exit non-zero after printing its line
 PARITY_TOL = {"fp32": {"log_rates": 1e-4, "loss": 1e-5, "grad": 1e-3},
-              "bf16": {"log_rates": 1e-2, "loss": 1e-3, "grad": 4e-2}}
+              "bf16": {"log_rates": 7e-3, "loss": 1e-4, "grad": 1e-2}}
 
 
 def full_batch_parity(ccfg, params, pixels, target, gpu, args):
@@ -452,12 +469,17 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
             "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
             "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
+            "knobs_nondefault": L.knobs_nondefault(),
         }
         if args.graph:
             line["step_mode"] = "hipGraph replay (vspike.graph.GraphedStep)"
         print(json.dumps(line), flush=True)
+        if parity is not None and not parity["ok"]:
+            print(f"bench.py: PARITY FAILED for the benched dispatch: {json.dumps(parity)}", file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and not parity["ok"]:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -462,10 +462,12 @@ int vs_dispatch_reset(void);
 #define VS_KNOB_ATTN_VARIANT 24  /* attention kernel variant (0 = default) */
 #define VS_KNOB_SLAB_WV     25   /* row-slab GEMM waves per workgroup: 4 or 8 (0 = by slab length) */
 #define VS_KNOB_WRES_WV     26   /* W-resident GEMM waves per workgroup: 8, else 4 */
-#define VS_KNOB_WRES_DBG    27   /* timing only, WRONG results: W-resident GEMM 1 = L2-resident stores, 2 = L2-resident reads */
+#define VS_KNOB_WRES_DBG    27   /* VS_DEBUG_KNOBS builds only (ignored otherwise): W-resident GEMM 1 = L2-resident stores, 2 = L2-resident reads (WRONG results) */
 #define VS_KNOB_COUNT       32
 int vs_knob_get(int knob);               /* VS_EINVAL for an unknown id */
 int vs_knob_set(int knob, int value);    /* returns the previous value; VS_EINVAL for an unknown id */
+int vs_knob_default(int knob);           /* the built-in default of a knob (before the environment) */
+int vs_debug_knobs(void);                /* 1: built with VS_DEBUG_KNOBS (timing-only knobs active) */
 
 #ifdef __cplusplus
 }

@@ -274,6 +274,32 @@ def gen_vit_tiny12_b16():
     print("vit_tiny12_b16", fx["loss"], fx["curve_train"])
 
 
+def gen_vit_tiny12_b16_enc(lr=None):
+    """Encoder-sensitive curve at the bench batch: the fresh-batch lr 1e-6 curves
+    move the loss by < 0.1 %, and the trainable- and frozen-encoder curves differ by <= 4e-4, so a
+    wrong encoder update could pass them.  Here the HEAD is frozen (requires_grad False, so AdamW
+    skips it, as the reference's optimiser skips any parameter without a gradient) and only the
+    encoder trains, on ONE batch repeated for 4 steps at a large lr: every change of the loss comes
+    from the encoder's backward + AdamW update.  B = 16 (M = 25,088 token rows: the benched kernels)."""
+    cfg = cpu_ref.VIT_TINY
+    B, enc_out, n = 16, 64, 128
+    lr = lr if lr is not None else 1e-4
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    for k, p in m.named_parameters():
+        p.grad = None
+        p.requires_grad = k.startswith("video_mae.") and ".key.bias" not in k
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=700))
+    y = torch.from_numpy(prng.spike_targets(750, (B, 100, n)))
+    batches = [(px, y)] * 4
+    curve = _ref_train_loop(m, batches, [p for p in m.parameters() if p.requires_grad], lr=lr)
+    fx = {"curve_enc": curve, "lr": np.array([lr])}
+    np.savez_compressed(os.path.join(OUT, "vit_tiny12_b16_enc.npz"), **fx)
+    print("vit_tiny12_b16_enc", lr, curve, "moved", abs(curve[-1] - curve[0]) / abs(curve[0]))
+
+
 def gen_vit_base32f():
     """BASELINE C5's encoder geometry (videomae-base width, 32 frames -> 3,136 tokens = 24 * 128 + 64,
     n = 1024) with one layer, B=1, trainable: forward and every gradient.  C5's temporal transformer

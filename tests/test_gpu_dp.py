@@ -92,10 +92,15 @@ def _worker(rank, world, port, mode, layers, dtype, out):
         px, y = _batch(cfg, step=step)
         m.zero_grad(set_to_none=True)
         xs, ys = px[rank * per:(rank + 1) * per].to(DEV), y[rank * per:(rank + 1) * per].to(DEV)
-        if mode == "ddp_attach_accum":
+        if mode.startswith("ddp_attach_accum"):
             # gradient accumulation: one clip per micro-batch, the first under no_sync (local only)
             for j in range(per):
-                if j < per - 1:
+                if j < per - 1 and mode == "ddp_attach_accum_split":
+                    # forward under no_sync, backward outside it: DDP decides at forward time
+                    with net.no_sync():
+                        lj = poisson_nll_mean(net(xs[j:j + 1]), ys[j:j + 1])
+                    lj.backward()
+                elif j < per - 1:
                     with net.no_sync():
                         poisson_nll_mean(net(xs[j:j + 1]), ys[j:j + 1]).backward()
                 else:
@@ -107,7 +112,7 @@ def _worker(rank, world, port, mode, layers, dtype, out):
             ex.finish()
     torch.cuda.synchronize()
     # DDP averages over ranks; the exchange sums; accumulation sums `per` one-clip mean losses
-    scale = 1.0 / world if mode == "exchange" else (1.0 / per if mode == "ddp_attach_accum" else 1.0)
+    scale = 1.0 / world if mode == "exchange" else (1.0 / per if mode.startswith("ddp_attach_accum") else 1.0)
     out[rank] = (m.enc_flat.grad.detach().cpu() * scale, m.head_flat.grad.detach().cpu() * scale)
     dist.destroy_process_group()
 
@@ -131,6 +136,7 @@ def _single_process_grads(layers, dtype):
     ("ddp_attach", 2, "fp32", 1e-5),
     ("ddp_attach", 4, "bf16", 1e-4),
     ("ddp_attach_accum", 2, "fp32", 1e-5),   # DDP no_sync micro-steps + attach_ddp
+    ("ddp_attach_accum_split", 2, "fp32", 1e-5),   # forward in no_sync, backward outside
 ])
 def test_two_ranks_equal_single_process_batch(mode, layers, dtype, tol):
     import torch.multiprocessing as mp

@@ -13,6 +13,7 @@ Tolerances (documented; measured values are printed with -s):
   * attention alone at the bench grids (B=16: H=3 -> 624 workgroups, H=12 -> 2496) against an fp64
     reference: the tolerances of tests/test_gpu_ops.py::test_attention_fwd_bwd.
 """
+import contextlib
 import math
 
 import numpy as np
@@ -125,7 +126,7 @@ def test_vit_tiny12_bench_geometry_loss_curve(golden, dtype):
         losses.append(loss.item())
     rel = np.abs(np.array(losses) - fx["curve_train"]) / np.abs(fx["curve_train"])
     print(f"\n[{dtype}] curve {losses} ref {fx['curve_train'].tolist()} max rel {rel.max():.3e}")
-    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+    assert rel.max() < (1e-5 if dtype == "fp32" else BF16_LOSS)
 
 
 # kernel paths the benched bf16 step takes at M = B * 1568 = 25,088 token rows (vspike.h VS_PATH_*):
@@ -135,18 +136,39 @@ BENCH_PATHS_BF16 = ("gemm_wres", "gemm_ln_fwd", "gemm_slab", "gemm_wslab", "gemm
                     "attn_bwd")
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_vit_tiny12_b16_benched_dispatch_forward_backward(golden, dtype):
-    """The bench's exact workload (C2, 12 layers, B=16 -> M = 25,088) against the reference's own
+@contextlib.contextmanager
+def bench128_dispatch():
+    """The kernel choices the bench makes at its 128 clips (M = 200,704 token rows), forced at B = 16
+    so the oracle-pinned fixture reaches them: the dX products fused with the
+    LayerNorm backwards (gemm_ln_bwd, on from 65,536 rows), the 8-wave 128-row slab tiles (used at
+    >= 256 rows per workgroup) and the 3-wave attention backward (used once the grid exceeds 3 x CUs)."""
+    import vspike.vit as V
+    from vspike import _lib as L
+    old = V._LN_FUSE
+    V._LN_FUSE = True
+    try:
+        with L.knob("slab_wv", 8), L.knob("attn_variant", 0x90):
+            yield
+    finally:
+        V._LN_FUSE = old
+
+
+@pytest.mark.parametrize("dtype,dispatch", [("fp32", "b16"), ("bf16", "b16"), ("bf16", "b128")])
+def test_vit_tiny12_b16_benched_dispatch_forward_backward(golden, dtype, dispatch):
+    """The bench's workload (C2, 12 layers, B=16 -> M = 25,088) against the reference's own
     forward/backward at that batch (fixture vit_tiny12_b16 from HF VideoMAEModel): log-rates, loss and
-    all 183 gradients; in bf16 the dispatch counters prove the benched kernel paths ran."""
+    all 183 gradients; in bf16 the dispatch counters prove the benched kernel paths ran.  dispatch
+    "b128": the choices of the 128-clip bench forced (bench128_dispatch), gemm_ln_bwd asserted."""
     from vspike import _lib as L
     fx = golden("vit_tiny12_b16.npz")
     cfg, B, n = cpu_ref.VIT_TINY, 16, 128
     L.dispatch_reset()
-    m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=16, y_seed=16)
+    with (bench128_dispatch() if dispatch == "b128" else contextlib.nullcontext()):
+        m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=16, y_seed=16)
     counts = {k: v for k, v in L.dispatch_counts().items() if v}
-    print(f"[{dtype}] dispatch {counts}")
+    print(f"[{dtype} {dispatch}] dispatch {counts}")
+    if dispatch == "b128":
+        assert counts.get("gemm_ln_bwd") == 2 * cfg.num_hidden_layers, counts
     if dtype == "fp32":
         assert out_err < 1e-4 and loss_err < 1e-5
         shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
@@ -161,9 +183,10 @@ def test_vit_tiny12_b16_benched_dispatch_forward_backward(golden, dtype):
         assert not bad, bad
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_vit_tiny12_b16_benched_dispatch_loss_curve(golden, dtype):
-    """3 optimiser steps of the reference loop (base.py:144-159) at the bench batch (B=16)."""
+@pytest.mark.parametrize("dtype,dispatch", [("fp32", "b16"), ("bf16", "b16"), ("bf16", "b128")])
+def test_vit_tiny12_b16_benched_dispatch_loss_curve(golden, dtype, dispatch):
+    """3 optimiser steps of the reference loop (base.py:144-159) at the bench batch (B=16); fp32 bar
+    1e-5 (measured ~1e-7: VERDICT r3 item 8)."""
     from vspike import FusedAdamW, poisson_nll_mean
     fx = golden("vit_tiny12_b16.npz")
     cfg, B, n = cpu_ref.VIT_TINY, 16, 128
@@ -171,18 +194,58 @@ def test_vit_tiny12_b16_benched_dispatch_loss_curve(golden, dtype):
     opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-6, weight_decay=0.01, eps=1e-8)
     sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=3, max_lr=1e-6, pct_start=0.15, div_factor=10)
     losses = []
-    for s in range(3):
-        px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=600 + s)).to(DEV)
-        y = torch.from_numpy(prng.spike_targets(650 + s, (B, 100, n))).to(DEV)
-        loss = poisson_nll_mean(m(px), y)
-        loss.backward()
-        opt.step()
-        sched.step()
-        opt.zero_grad()
-        losses.append(loss.item())
+    with (bench128_dispatch() if dispatch == "b128" else contextlib.nullcontext()):
+        for s in range(3):
+            px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=600 + s)).to(DEV)
+            y = torch.from_numpy(prng.spike_targets(650 + s, (B, 100, n))).to(DEV)
+            loss = poisson_nll_mean(m(px), y)
+            loss.backward()
+            opt.step()
+            sched.step()
+            opt.zero_grad()
+            losses.append(loss.item())
     rel = np.abs(np.array(losses) - fx["curve_train"]) / np.abs(fx["curve_train"])
-    print(f"\n[{dtype}] B=16 curve {losses} ref {fx['curve_train'].tolist()} max rel {rel.max():.3e}")
-    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+    print(f"\n[{dtype} {dispatch}] B=16 curve {losses} ref {fx['curve_train'].tolist()} max rel {rel.max():.3e}")
+    assert rel.max() < (1e-5 if dtype == "fp32" else BF16_LOSS)
+
+
+# bf16 bar of the encoder-only curve: the loss moves ~4 % over the 4 steps (fixture), the bar must be
+# far below that so a wrong encoder update fails
+BF16_ENC_CURVE = 2e-3
+
+
+@pytest.mark.parametrize("dtype,dispatch", [("fp32", "b16"), ("bf16", "b16"), ("bf16", "b128")])
+def test_vit_tiny12_b16_encoder_only_curve(golden, dtype, dispatch):
+    """Encoder-sensitive curve (fixture vit_tiny12_b16_enc from the reference's
+    HF encoder + head, oracle/gen_fixtures.py): the head frozen, the encoder trained by AdamW +
+    OneCycleLR on ONE batch repeated 4 times at lr 1e-4, so every change of the loss comes from the
+    encoder's backward and update; B = 16 (M = 25,088 rows: the benched kernels)."""
+    from vspike import FusedAdamW, poisson_nll_mean
+    fx = golden("vit_tiny12_b16_enc.npz")
+    cfg, B, n = cpu_ref.VIT_TINY, 16, 128
+    lr = float(fx["lr"][0])
+    m = _vit_model(cfg, 64, n, dtype)
+    m.head_flat.requires_grad_(False)
+    opt = FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=lr, weight_decay=0.01, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, total_steps=4, max_lr=lr, pct_start=0.15, div_factor=10)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=700)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(750, (B, 100, n))).to(DEV)
+    losses = []
+    with (bench128_dispatch() if dispatch == "b128" else contextlib.nullcontext()):
+        for s in range(4):
+            loss = poisson_nll_mean(m(px), y)
+            loss.backward()
+            opt.step()
+            sched.step()
+            opt.zero_grad()
+            losses.append(loss.item())
+    ref = fx["curve_enc"]
+    rel = np.abs(np.array(losses) - ref) / np.abs(ref)
+    moved = abs(ref[-1] - ref[0]) / abs(ref[0])
+    print(f"\n[{dtype} {dispatch}] encoder-only curve {losses} ref {ref.tolist()} max rel {rel.max():.3e} "
+          f"(reference moves {moved:.2%})")
+    assert moved > 0.01
+    assert rel.max() < (1e-5 if dtype == "fp32" else BF16_ENC_CURVE)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -245,7 +308,7 @@ def test_vit_base_frozen_encoder_loss_curve(golden, dtype):
         losses.append(loss.item())
     rel = np.abs(np.array(losses) - fx["curve_frozen"]) / np.abs(fx["curve_frozen"])
     print(f"\n[{dtype}] frozen curve {losses} max rel {rel.max():.3e}")
-    assert rel.max() < (1e-3 if dtype == "fp32" else BF16_LOSS)
+    assert rel.max() < (1e-5 if dtype == "fp32" else BF16_LOSS)
 
 
 def test_loaded_library_is_built_from_these_sources():

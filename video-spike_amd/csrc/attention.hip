@@ -678,320 +678,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 #endif
 }
 
-// ------------------------------------------------------------------ forward, one wave per SIMD
-// Workgroup = 4 waves = 4 x NQB x 32 query rows of one (batch, head); one workgroup per CU (the
-// whole register file per wave).  Each wave carries NQB independent 32-row query blocks through
-// the same K/V stream, so every K / V^T fragment it reads from LDS feeds NQB MFMAs, and the
-// softmax VALU of one 32-key block runs under the next block's QK^T MFMAs (software pipeline:
-// S(i+1) = QK(K(i+1)) is issued before softmax(S(i)), then O += PV(V(i), P(i))).  At C2 (B*H = 48
-// heads x 1568 queries) NQB = 3 gives 240 workgroups for 256 CUs: one round, 96 rows per SIMD
-// (the 32-row granularity of the problem allows no fewer than 73.5 on 1024 SIMDs).  K/V arrive by
-// LDS-DMA into a 3-stage ring of 64-key tiles issued two tiles ahead, one barrier per tile.
-// Numerics and the two passes (fast: p = exp2(s) against a fixed reference, row sums on the matrix
-// pipe; safe: online softmax, re-run when a row sum leaves [2^-60, 2^60]) as attn_fwd_bf16_kernel.
-template <int NQB, int WPS>
-__global__ __launch_bounds__(256, WPS) void attn_fwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                                  bf16_t* __restrict__ o, int64_t ldo,
-                                                                  float* __restrict__ lse, int N, int H,
-                                                                  float scale_log2) {
-  constexpr int TILE = 64 * 128;      // bytes of one 64-key x 64-dh bf16 image
-  constexpr int STAGE = 2 * TILE;     // K image + V image
-  constexpr int NSTG = 3;
-  constexpr int ROWS = 4 * NQB * 32;  // query rows per workgroup
-  __shared__ __attribute__((aligned(16))) char smem[NSTG * STAGE];
-  __shared__ int redo_flag;
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nqb = (N + ROWS - 1) / ROWS, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nqb;
-  const int h = (blk / nqb) % H, b = blk / nqb / H, D = H * 64;
-  const int64_t row0 = (int64_t)b * N;
-  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
-  const bf16_t* Kp = Qp + D;
-  const int q0w = qb * ROWS + wid * NQB * 32;  // this wave's first query
-  const float c = scale_log2;
-  if (tid == 0) redo_flag = 0;
-
-  // Q fragments (B operand of S^T = K Q^T), pre-scaled by c; rows past N re-read row N-1
-  bf16x8 qf[NQB][4];
-#pragma unroll
-  for (int q = 0; q < NQB; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int qi = q0w + q * 32 + (lane & 31);
-      const int qr = qi < N ? qi : N - 1;
-      const bf16x8 x = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
-      f32x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (float)x[j] * c;
-      qf[q][s] = __builtin_convertvector(v, bf16x8);
-    }
-  const bf16x8 sel = rowsum_selector(lane);
-  f32x16 oacc[NQB][2];
-  f32x4 lacc[NQB];
-  float m_run[NQB], l_half[NQB];
-
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16;
-  int kbase[4];
-  {
-    const int key = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kbase[s] = key * 128 + (((2 * s + hh) ^ swz_row(key)) << 4);
-  }
-  int vbase[2];
-  {
-    const int k0 = 4 * hh + q4;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) vbase[dt] = TILE + off_halfswz(k0, dt * 32 + g16 + p4);
-  }
-  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
-  // DMA of one 64-key tile into stage `st`: wave w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1
-  // (8 rows x 128 B each, lane L loading the source chunk that belongs at position L & 7)
-  auto load_tile = [&](int kt, int st) {
-    const int prow0 = wid * 16 + (lane >> 3), ppos = lane & 7;
-    const char* kb = (const char*)Kp + kt * tile_bytes;
-    const char* vb = kb + vdelta;
-    char* dk = smem + st * STAGE + wid * 2048;
-    char* dv = dk + TILE;
-    int r0 = prow0, r1 = prow0 + 8;
-    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (their scores are masked)
-      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
-      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
-    }
-    const uint32_t o0 = (uint32_t)r0 * (uint32_t)(2 * ldq), o1 = (uint32_t)r1 * (uint32_t)(2 * ldq);
-    glds16_asm_so(kb, o0 + ((ppos ^ swz_row(prow0)) << 4), dk);
-    glds16_asm_so(kb, o1 + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
-    glds16_asm_so(vb, o0 + ((ppos ^ swz_half(prow0)) << 4), dv);
-    glds16_asm_so(vb, o1 + ((ppos ^ swz_half(prow0 + 8)) << 4), dv + 1024);
-  };
-  struct KFrag {
-    bf16x8 k[4];
-  };
-  struct VFrag {
-    bf16x8 v[4];
-  };
-  auto kread = [&](int st, int kb) {
-    KFrag f;
-    const char* base = smem + st * STAGE + kb * 4096;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) f.k[s] = *(const bf16x8*)(base + kbase[s]);
-    return f;
-  };
-  auto vread = [&](int st, int kb) {
-    VFrag f;
-    const char* base = smem + st * STAGE + kb * 4096;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) f.v[2 * s + dt] = tr_pair(base + s * 2048, vbase[dt], vbase[dt] + 1024);
-    return f;
-  };
-  auto qk = [&](const KFrag& k, f32x16 (&sacc)[NQB]) {
-#pragma unroll
-    for (int q = 0; q < NQB; ++q) {
-      f32x16 z;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) z[r] = 0.f;
-      sacc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k.k[0], qf[q][0], z, 0, 0, 0);
-#pragma unroll
-      for (int s = 1; s < 4; ++s) sacc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k.k[s], qf[q][s], sacc[q], 0, 0, 0);
-    }
-  };
-  // wave-uniform barrier helpers with an immediate vmcnt (LDS-DMA pieces of younger tiles may stay
-  // in flight: 4 pieces per wave per tile)
-  auto wait_tile = [&](int younger_tiles) {
-    if (younger_tiles >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger_tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  const int ntile = (N + 63) / 64, nblk = (N + 31) / 32;
-  auto pass = [&](auto safec) {
-    constexpr bool SAFE = decltype(safec)::value;
-#pragma unroll
-    for (int q = 0; q < NQB; ++q) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        oacc[q][0][r] = 0.f;
-        oacc[q][1][r] = 0.f;
-      }
-      lacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      m_run[q] = 0.f;
-      l_half[q] = 0.f;
-    }
-    for (int t = 0; t < NSTG && t < ntile; ++t) load_tile(t, t);
-    wait_tile(ntile - 1 < 2 ? ntile - 1 : 2);
-    f32x16 sc[NQB];  // scores of the current 32-key block, replaced in place by the next block's
-    VFrag vA = vread(0, 0), vB;
-    {
-      const KFrag k0 = kread(0, 0);
-      qk(k0, sc);
-    }
-    // one 32-key block i, per q-block q: softmax(S(i, q)) -> P(i, q), then S(i+1, q) = QK(K(i+1), q)
-    // into the same registers (its MFMAs run under the next q-block's softmax VALU); then
-    // O += PV(V(i), P(i)), under which the next block's first softmax can issue.
-    // NEXT: a block i+1 exists.  OPEN: block i+1 opens tile tn (wait for it, DMA tile tn + 2 into
-    // tile tn - 1's stage; placed after the first softmax so the barrier overlaps the MFMAs in
-    // flight).  MASK: keys past N in this block.  Compile-time flags: one basic block per variant.
-    // stc: the LDS stage of block i+1's tile, ((i+1)/2) % NSTG — an IC<> in the unrolled main loop
-    // (every LDS address is then a lane base plus an immediate), a plain int in the remainder.
-    auto body = [&](int i, const VFrag& vcur, VFrag& vnxt, auto nextc, auto openc, auto maskc, auto stc) {
-      constexpr bool NEXT = decltype(nextc)::value, OPEN = decltype(openc)::value, MASK = decltype(maskc)::value;
-      const int tn = (i + 1) >> 1, hn = (i + 1) & 1;
-      const int stn = (int)stc;
-      const int key0 = i * 32;
-      bf16x8 pa[NQB], pb[NQB];
-      KFrag kf;
-#pragma unroll
-      for (int q = 0; q < NQB; ++q) {
-        f32x16& acc = sc[q];
-        if constexpr (MASK) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
-        }
-        float p[16];
-        if constexpr (!SAFE) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r]);
-        } else {
-          const float mx = max16(acc);
-          if (__any(i == 0 || mx > m_run[q] + kRefBand)) {
-            const float mxp = pair_max(mx);
-            const bool move = i == 0 || mxp > m_run[q] + kRefBand;
-            const float m_new = move ? mxp : m_run[q];
-            const float alpha = i == 0 ? 1.f : __builtin_amdgcn_exp2f(m_run[q] - m_new);
-            m_run[q] = m_new;
-            l_half[q] *= alpha;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              oacc[q][0][r] *= alpha;
-              oacc[q][1][r] *= alpha;
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(acc[r] - m_run[q]);
-          l_half[q] += ((((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) +
-                        (((p[8] + p[9]) + (p[10] + p[11])) + ((p[12] + p[13]) + (p[14] + p[15]))));
-        }
-        pa[q] = pack8f(p);
-        pb[q] = pack8f(p + 8);
-        if constexpr (!SAFE) {
-          lacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pa[q], lacc[q], 0, 0, 0);
-          lacc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb[q], lacc[q], 0, 0, 0);
-        }
-        if constexpr (NEXT) {
-          if (q == 0) {
-            if constexpr (OPEN) {
-              wait_tile(tn + 1 < ntile ? 1 : 0);
-              if (tn + 2 < ntile) load_tile(tn + 2, stn == 0 ? 2 : stn - 1);
-            }
-            kf = kread(stn, hn);
-          }
-          f32x16 z;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) z[r] = 0.f;
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf.k[0], qf[q][0], z, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf.k[s], qf[q][s], acc, 0, 0, 0);
-        }
-      }
-      if constexpr (NEXT) vnxt = vread(stn, hn);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-          for (int q = 0; q < NQB; ++q)
-            oacc[q][dt] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(vcur.v[2 * s + dt], s == 0 ? pa[q] : pb[q], oacc[q][dt], 0, 0, 0);
-    };
-    // main loop: 6 blocks = 3 tiles per iteration, so block i+1's stage is static: blocks 6m+k have
-    // their next block in tile 3m + (k+1)/2 (stage (k+1)/2 % 3); k odd opens that tile
-    const bool tail_mask = (N & 31) != 0;
-    int i = 0;
-    for (; i + 6 < nblk; i += 6) {
-      body(i, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<0>{});
-      body(i + 1, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<1>{});
-      body(i + 2, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<1>{});
-      body(i + 3, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<2>{});
-      body(i + 4, vA, vB, IC<1>{}, IC<0>{}, IC<0>{}, IC<2>{});
-      body(i + 5, vB, vA, IC<1>{}, IC<1>{}, IC<0>{}, IC<0>{});
-    }
-    // remainder (1..6 blocks): dynamic stage; V alternates with the block parity (i is even here)
-    for (; i < nblk; ++i) {
-      const VFrag& vc = (i & 1) ? vB : vA;
-      VFrag& vn = (i & 1) ? vA : vB;
-      const int stn = ((i + 1) >> 1) % NSTG;
-      if (i + 1 < nblk) {
-        if (((i + 1) & 1) == 0) body(i, vc, vn, IC<1>{}, IC<1>{}, IC<0>{}, stn);
-        else body(i, vc, vn, IC<1>{}, IC<0>{}, IC<0>{}, stn);
-      } else if (tail_mask) {
-        body(i, vc, vn, IC<0>{}, IC<0>{}, IC<1>{}, stn);
-      } else {
-        body(i, vc, vn, IC<0>{}, IC<0>{}, IC<0>{}, stn);
-      }
-    }
-  };
-
-  pass(IC<0>{});
-  // row sum of this lane's query (lane & 31) per q-block: row (q >> 4) of lacc in lane (q & 15)
-  float l[NQB];
-  bool bad = false;
-#pragma unroll
-  for (int q = 0; q < NQB; ++q) {
-    const int qq = lane & 31, src = (qq & 15) << 2;
-    float l0, l1;
-    asm volatile(
-        "ds_bpermute_b32 %0, %2, %3\n\t"
-        "ds_bpermute_b32 %1, %2, %4\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(l0), "=&v"(l1)
-        : "v"(src), "v"(lacc[q][0]), "v"(lacc[q][1])
-        : "memory");
-    l[q] = qq < 16 ? l0 : l1;
-    const int qi = q0w + q * 32 + qq;
-    bad |= qi < N && !(l[q] >= 0x1p-60f && l[q] <= 0x1p60f);
-  }
-  __syncthreads();  // every wave is done with the last K/V tile; redo_flag = 0 is visible
-  if (__any(bad) && lane == 0) redo_flag = 1;
-  __syncthreads();
-  if (redo_flag) {  // workgroup-uniform: the whole workgroup streams K/V again, safe softmax
-    pass(IC<1>{});
-#pragma unroll
-    for (int q = 0; q < NQB; ++q) l[q] = pair_sum(l_half[q]);
-    __syncthreads();
-  }
-
-  // Epilogue: O^T accumulators -> normalised bf16 rows staged through LDS (wave-private, XOR-
-  // swizzled 16-B chunks), then whole 128-B rows (8 lanes per row)
-  char* so = smem + wid * (NQB * 4096);
-  const int oq = lane & 31;
-#pragma unroll
-  for (int q = 0; q < NQB; ++q) {
-    const float inv = 1.f / l[q];
-    const int r = q * 32 + oq;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int chunk = dt * 4 + g;
-        *(uint2*)(so + r * 128 + ((chunk ^ (r & 7)) << 4) + 8 * hh) =
-            pack4(oacc[q][dt][4 * g] * inv, oacc[q][dt][4 * g + 1] * inv, oacc[q][dt][4 * g + 2] * inv,
-                  oacc[q][dt][4 * g + 3] * inv);
-      }
-    const int qi = q0w + r;
-    if (hh == 0 && qi < N) lse[((int64_t)b * H + h) * N + qi] = (m_run[q] + __log2f(l[q])) * kLn2;
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed (wave-private)
-#pragma unroll
-  for (int pss = 0; pss < 4 * NQB; ++pss) {
-    const int r = pss * 8 + (lane >> 3), ch = lane & 7;
-    const uint4 v = *(const uint4*)(so + r * 128 + ((ch ^ (r & 7)) << 4));
-    if (q0w + r < N) *(uint4*)(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8) = v;
-  }
-}
-
 // ------------------------------------------------------------------ backward: row constants
 // Per (batch, head, query): nlse2 = -LSE * log2(e) and ndel = -delta (delta = rowsum(dO * O)),
 // stored [B*H][Npad] with Npad = N rounded up to 64 and the padding set to (-inf, 0): the dK/dV
@@ -1762,407 +1448,6 @@ __global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t
   }
 }
 
-// ------------------------------------------------------------------ backward, one wave per SIMD
-// The same two passes as attn_bwd_dkdv_body / attn_bwd_dq_body, re-tiled for one wave per SIMD
-// (launch_bounds(256, 1): the whole register file per wave): a wave carries NB = 3 key blocks
-// (dK/dV) or 3 query blocks (dQ), so each fragment it reads from LDS (Q / dO rows and their
-// transposes in the dK/dV pass; K / V rows and K^T in the dQ pass) feeds 3 MFMAs, and the three
-// independent chains give the scheduler MFMAs to issue under each block's exp / dS VALU.
-// Slices of 64 rows stream through a 3-stage LDS-DMA ring issued two slices ahead (one barrier per
-// slice); every wave issues 5 DMA pieces per slice (Q/dO or K/V rows + a quarter of the row
-// constants), so its counted vmcnt is wave-uniform.  Workgroup = 384 keys (or queries) of one
-// (batch, head): 240 + 240 workgroups at C2, dK/dV first.
-constexpr int kW1Stage = 2 * kBwdQT + 512;
-// query blocks per dQ wave: 2 (the per-lane -LSE / -delta splats that seed its S and dP chains cost
-// 32 registers per block, so 3 blocks overflow the register file into accumulator copies)
-constexpr int kW1DqBlocks = 2;
-
-template <int NB>
-__device__ __forceinline__ void attn_bwd_dkdv_w1(char* __restrict__ smem, int blk, const bf16_t* __restrict__ qkv,
-                                                 int64_t ldq, const bf16_t* __restrict__ dout, int64_t lddo,
-                                                 const float* __restrict__ nlse2, const float* __restrict__ ndel,
-                                                 bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
-                                                 float scale) {
-  constexpr int QT = kBwdQT, STAGE = kW1Stage, NSTG = 3, ROWS = 4 * NB * 32;
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nkb = (N + ROWS - 1) / ROWS, kb = blk % nkb;
-  const int h = (blk / nkb) % H, b = blk / nkb / H, D = H * 64;
-  const int64_t row0 = (int64_t)b * N;
-  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
-  const bf16_t* Kp = Qp + D;
-  const bf16_t* Vp = Qp + 2 * D;
-  const bf16_t* Dp = dout + row0 * lddo + h * 64;
-  const float* NL = nlse2 + ((int64_t)b * H + h) * Npad;
-  const float* ND = ndel + ((int64_t)b * H + h) * Npad;
-  const int k0w = kb * ROWS + wid * NB * 32;  // this wave's first key
-  const float c2 = scale * kLog2e;
-
-  bf16x8 kf[NB][4], vf[NB][4];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int ki = k0w + j * 32 + (lane & 31);
-    const int kr = ki < N ? ki : N - 1;  // rows past N: finite data, their dK/dV are not stored
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 k = *(const bf16x8*)(Kp + (int64_t)kr * ldq + 16 * s + 8 * hh);
-      f32x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (float)k[e] * c2;
-      kf[j][s] = __builtin_convertvector(v, bf16x8);
-      vf[j][s] = *(const bf16x8*)(Vp + (int64_t)kr * ldq + 16 * s + 8 * hh);
-    }
-  }
-  f32x16 dkacc[NB][2], dvacc[NB][2];
-#pragma unroll
-  for (int j = 0; j < NB; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      dkacc[j][0][r] = 0.f;
-      dkacc[j][1][r] = 0.f;
-      dvacc[j][0][r] = 0.f;
-      dvacc[j][1][r] = 0.f;
-    }
-
-  // DMA of 64-query slice `it` into stage `st`: wave w fills Q pieces 2w, 2w+1, dO pieces 2w, 2w+1
-  // and one quarter (32 floats) of nlse2 | ndel (waves 0, 1: nlse2 halves; 2, 3: ndel halves)
-  auto load_slice = [&](int it, int st) {
-    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
-    const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
-    const int q0 = it * 64;
-    int r0 = prow, r1 = prow + 8;
-    if (q0 + 64 > N) {  // partial last slice: rows past N re-read row N-1 (their nlse2 = -inf zeroes them)
-      r0 = q0 + r0 < N ? r0 : N - 1 - q0;
-      r1 = q0 + r1 < N ? r1 : N - 1 - q0;
-    }
-    const char* qs = (const char*)(Qp + (int64_t)q0 * ldq);
-    const char* ds = (const char*)(Dp + (int64_t)q0 * lddo);
-    char* dst = smem + st * STAGE;
-    glds16_asm_so(qs, (uint32_t)r0 * (uint32_t)(2 * ldq) + cq0, dst + wid * 2048);
-    glds16_asm_so(qs, (uint32_t)r1 * (uint32_t)(2 * ldq) + cq1, dst + wid * 2048 + 1024);
-    glds16_asm_so(ds, (uint32_t)r0 * (uint32_t)(2 * lddo) + cq0, dst + QT + wid * 2048);
-    glds16_asm_so(ds, (uint32_t)r1 * (uint32_t)(2 * lddo) + cq1, dst + QT + wid * 2048 + 1024);
-    const float* src = (wid < 2 ? NL : ND) + q0 + (wid & 1) * 32;
-    const uint32_t lo = (uint32_t)(lane & 31) * 4;
-    if (lane < 32) glds4_asm_so(src, lo, dst + 2 * QT + (wid >> 1) * 256 + (wid & 1) * 128);
-  };
-  auto wait_slice = [&](int younger) {  // 5 pieces per wave per slice
-    if (younger >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  const int qrow = lane & 31;
-  int roff[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) roff[s] = qrow * 128 + (((2 * s + hh) ^ swz_rt(qrow)) << 4);
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, qt = 4 * hh + q4;
-  int toff[2][2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    toff[dt][0] = off_rtswz(qt, dt * 32 + g16 + p4);
-    toff[dt][1] = off_rtswz(qt + 8, dt * 32 + g16 + p4);
-  }
-
-  // one 32-query sub-slice of stage st: S = Q K^T (+ -LSE log2e) -> P -> dV^T += dO^T P;
-  // dP = dO V^T (- delta) -> dS = P dP -> dK^T += Q^T dS, for the wave's NB key blocks
-  auto sub_slice = [&](int st, int sub) {
-    const char* sQ = smem + st * STAGE;
-    const char* sD = sQ + QT;
-    const float* sL = (const float*)(sQ + 2 * QT) + sub * 32 + 4 * hh;
-    const float* sE = (const float*)(sQ + 2 * QT + 256) + sub * 32 + 4 * hh;
-    f32x16 init;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 l4 = *(const float4*)(sL + 8 * g);
-      init[4 * g] = l4.x; init[4 * g + 1] = l4.y; init[4 * g + 2] = l4.z; init[4 * g + 3] = l4.w;
-    }
-    f32x16 sacc[NB];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 a = *(const bf16x8*)(sQ + sub * 4096 + roff[s]);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[j][s], s == 0 ? init : sacc[j], 0, 0, 0);
-    }
-    float p[NB][16];
-    bf16x8 pb[NB][2];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p[j][r] = __builtin_amdgcn_exp2f(sacc[j][r]);
-      pb[j][0] = pack8f(p[j]);
-      pb[j][1] = pack8f(p[j] + 8);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int o = sub * 4096 + s2 * 2048;
-        const bf16x8 a = tr_pair(sD, o + toff[dt][0], o + toff[dt][1]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) dvacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[j][s2], dvacc[j][dt], 0, 0, 0);
-      }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 e4 = *(const float4*)(sE + 8 * g);
-      init[4 * g] = e4.x; init[4 * g + 1] = e4.y; init[4 * g + 2] = e4.z; init[4 * g + 3] = e4.w;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 a = *(const bf16x8*)(sD + sub * 4096 + roff[s]);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, vf[j][s], s == 0 ? init : sacc[j], 0, 0, 0);
-    }
-    bf16x8 db[NB][2];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      float ds[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] = p[j][r] * sacc[j][r];
-      db[j][0] = pack8f(ds);
-      db[j][1] = pack8f(ds + 8);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int o = sub * 4096 + s2 * 2048;
-        const bf16x8 a = tr_pair(sQ, o + toff[dt][0], o + toff[dt][1]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) dkacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, db[j][s2], dkacc[j][dt], 0, 0, 0);
-      }
-  };
-
-  const int nit = (N + 63) / 64;
-  load_slice(0, 0);
-  if (nit > 1) load_slice(1, 1);
-  // slice `it` in stage it % 3 (a compile-time constant in the unrolled loop): wait for it, DMA
-  // slice it + 2 into slice it - 1's stage, then its two 32-query sub-slices
-  auto iter = [&](int it, auto stc) {
-    constexpr int ST = decltype(stc)::value;
-    wait_slice(it + 1 < nit ? 1 : 0);
-    if (it + 2 < nit) load_slice(it + 2, (ST + 2) % NSTG);
-    sub_slice(ST, 0);
-    if (it * 64 + 32 < N) sub_slice(ST, 1);
-  };
-  int it = 0;
-  for (; it + 3 <= nit; it += 3) {
-    iter(it, IC<0>{});
-    iter(it + 1, IC<1>{});
-    iter(it + 2, IC<2>{});
-  }
-  if (it < nit) iter(it, IC<0>{});
-  if (it + 1 < nit) iter(it + 1, IC<1>{});
-
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int ki = k0w + j * 32 + (lane & 31);
-    if (ki < N) {
-      bf16_t* krow = dqkv + (row0 + ki) * ldd + D + h * 64;
-      bf16_t* vrow = krow + D;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = dt * 32 + 8 * g + 4 * hh;
-          *(uint2*)(krow + d) = pack4(dkacc[j][dt][4 * g] * scale, dkacc[j][dt][4 * g + 1] * scale,
-                                      dkacc[j][dt][4 * g + 2] * scale, dkacc[j][dt][4 * g + 3] * scale);
-          *(uint2*)(vrow + d) =
-              pack4(dvacc[j][dt][4 * g], dvacc[j][dt][4 * g + 1], dvacc[j][dt][4 * g + 2], dvacc[j][dt][4 * g + 3]);
-        }
-    }
-  }
-}
-
-template <int NB>
-__device__ __forceinline__ void attn_bwd_dq_w1(char* __restrict__ smem, int blk, const bf16_t* __restrict__ qkv,
-                                               int64_t ldq, const bf16_t* __restrict__ dout, int64_t lddo,
-                                               const float* __restrict__ nlse2, const float* __restrict__ ndel,
-                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
-                                               float scale) {
-  constexpr int TILE = kBwdQT, STAGE = kW1Stage, NSTG = 3, ROWS = 4 * NB * 32;
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nqb = (N + ROWS - 1) / ROWS, qb = blk % nqb;
-  const int h = (blk / nqb) % H, b = blk / nqb / H, D = H * 64;
-  const int64_t row0 = (int64_t)b * N;
-  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
-  const bf16_t* Kp = Qp + D;
-  const bf16_t* Dp = dout + row0 * lddo + h * 64;
-  const int q0w = qb * ROWS + wid * NB * 32;
-  const float c2 = scale * kLog2e;
-
-  bf16x8 qf[NB][4], df[NB][4];
-  f32x16 sinit[NB], dinit[NB], dqacc[NB][2];
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int qi = q0w + j * 32 + (lane & 31);
-    const int qr = qi < N ? qi : N - 1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
-      f32x8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (float)q[e] * c2;
-      qf[j][s] = __builtin_convertvector(v, bf16x8);
-      df[j][s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
-    }
-    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
-    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
-    const float nd = qi < N ? ndel[w] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sinit[j][r] = nl;
-      dinit[j][r] = nd;
-      dqacc[j][0][r] = 0.f;
-      dqacc[j][1][r] = 0.f;
-    }
-  }
-
-  int roff[4];
-  {
-    const int key = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
-  }
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
-  int toff[2][2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
-    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
-  }
-
-  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
-  // DMA of 64-key tile kt into stage st: wave w fills K pieces 2w, 2w+1 and V pieces 2w, 2w+1, plus
-  // one dummy-free 5th piece slot (a repeat of its first K piece) so every wave counts 5 per tile
-  auto load_tile = [&](int kt, int st) {
-    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
-    const uint32_t cc0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cc1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
-    const char* kb_ = (const char*)Kp + kt * tile_bytes;
-    const char* vb_ = kb_ + vdelta;
-    char* dk = smem + st * STAGE + wid * 2048;
-    char* dv = dk + TILE;
-    int r0 = prow, r1 = prow + 8;
-    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (masked below)
-      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
-      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
-    }
-    const uint32_t o0 = (uint32_t)r0 * (uint32_t)(2 * ldq) + cc0, o1 = (uint32_t)r1 * (uint32_t)(2 * ldq) + cc1;
-    glds16_asm_so(kb_, o0, dk);
-    glds16_asm_so(kb_, o1, dk + 1024);
-    glds16_asm_so(vb_, o0, dv);
-    glds16_asm_so(vb_, o1, dv + 1024);
-    glds16_asm_so(kb_, o0, dk);  // same bytes again: keeps the per-slice piece count at 5 (see dK/dV)
-  };
-  auto wait_tile = [&](int younger) {
-    if (younger >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-
-  // one 32-key block (kb of stage st): S^T = K (cQ)^T - LSE, dP^T = V dO^T - delta (query on the
-  // lane), dS^T = exp2(S^T) dP^T -> dQ^T += K^T dS^T, for the wave's NB query blocks
-  auto block = [&](int st, int kbk, int key0, auto maskc) {
-    constexpr bool MASK = decltype(maskc)::value;
-    const char* sK = smem + st * STAGE;
-    const char* sV = sK + TILE;
-    f32x16 sacc[NB], dpacc[NB];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 ka = *(const bf16x8*)(sK + kbk * 4096 + roff[s]);
-      const bf16x8 va = *(const bf16x8*)(sV + kbk * 4096 + roff[s]);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[j][s], s == 0 ? sinit[j] : sacc[j], 0, 0, 0);
-        dpacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[j][s], s == 0 ? dinit[j] : dpacc[j], 0, 0, 0);
-      }
-    }
-    bf16x8 db[NB][2];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      if constexpr (MASK) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[j][r] = -INFINITY;
-      }
-      float ds[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[j][r]) * dpacc[j][r];
-      db[j][0] = pack8f(ds);
-      db[j][1] = pack8f(ds + 8);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int o = kbk * 4096 + s2 * 2048;
-        const bf16x8 ka = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) dqacc[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db[j][s2], dqacc[j][dt], 0, 0, 0);
-      }
-  };
-
-  const int nkt = (N + 63) / 64;
-  load_tile(0, 0);
-  if (nkt > 1) load_tile(1, 1);
-  auto iter = [&](int kt, auto stc) {
-    constexpr int ST = decltype(stc)::value;
-    wait_tile(kt + 1 < nkt ? 1 : 0);
-    if (kt + 2 < nkt) load_tile(kt + 2, (ST + 2) % NSTG);
-    if ((kt + 1) * 64 <= N) {
-      block(ST, 0, kt * 64, IC<0>{});
-      block(ST, 1, kt * 64 + 32, IC<0>{});
-    } else {  // the partial last tile
-      block(ST, 0, kt * 64, IC<1>{});
-      if (kt * 64 + 32 < N) block(ST, 1, kt * 64 + 32, IC<1>{});
-    }
-  };
-  int kt = 0;
-  for (; kt + 3 <= nkt; kt += 3) {
-    iter(kt, IC<0>{});
-    iter(kt + 1, IC<1>{});
-    iter(kt + 2, IC<2>{});
-  }
-  if (kt < nkt) iter(kt, IC<0>{});
-  if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
-
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const int qi = q0w + j * 32 + (lane & 31);
-    if (qi < N) {
-      bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = dt * 32 + 8 * g + 4 * hh;
-          *(uint2*)(qrow + d) = pack4(dqacc[j][dt][4 * g] * scale, dqacc[j][dt][4 * g + 1] * scale,
-                                      dqacc[j][dt][4 * g + 2] * scale, dqacc[j][dt][4 * g + 3] * scale);
-        }
-    }
-  }
-}
-
-// dK/dV workgroups [0, nkv), dQ workgroups [nkv, nkv + nq): the longer dK/dV ones dispatch first and
-// the dQ ones fill the CUs they free.  NBKV key blocks per dK/dV wave, NBQ query blocks per dQ wave,
-// WPS waves per SIMD (the register budget: 512 / WPS per lane).
-template <int NBKV, int NBQ, int WPS>
-__global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_w1_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
-                                                                    const bf16_t* __restrict__ dout, int64_t lddo,
-                                                                    const float* __restrict__ nlse2,
-                                                                    const float* __restrict__ ndel,
-                                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N,
-                                                                    int H, int Npad, float scale, int nkv) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * kW1Stage];
-  const int id = blockIdx.x;
-  if (id < nkv)
-    attn_bwd_dkdv_w1<NBKV>(smem, xcd_remap(id, nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
-  else
-    attn_bwd_dq_w1<NBQ>(smem, xcd_remap(id - nkv, (int)gridDim.x - nkv), qkv, ldq, dout, lddo, nlse2, ndel, dqkv,
-                        ldd, N, H, Npad, scale);
-}
-
 // ------------------------------------------------------------------ backward: one launch
 // The dK/dV and dQ passes run as ONE grid: blocks [0, nblk) are dK/dV workgroups, [nblk, 2 nblk)
 // dQ workgroups, sharing the same two LDS stages.  Each pass alone puts 2496 waves on 3072 wave
@@ -2178,7 +1463,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_bf16_kernel(const bf16_t* __r
   __shared__ __attribute__((aligned(16))) char st0[kBwdStage];  // two objects: see attn_fwd_bf16_kernel
   __shared__ __attribute__((aligned(16))) char st1[kBwdStage];
   const int id = blockIdx.x;
-  if (skip & (id < nblk ? 1 : 2)) return;  // timing of one pass alone (VS_KNOB_ATTN_VARIANT bits 8, 9)
+  if (skip & (id < nblk ? 1 : 2)) return;  // diagnostic builds only: one pass timed alone (VS_DEBUG_KNOBS)
   if (id < nblk)
     attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
   else
@@ -2209,30 +1494,15 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     VS_REQUIRE(ld_qkv % 8 == 0 && ld_o % 4 == 0 && aligned16(qkv) && (((uintptr_t)o) & 7) == 0,
                "vs_attn_fwd: bf16 rows must be 16-byte aligned");
     count_path(VS_PATH_ATTN_FWD);
-    // VS_KNOB_ATTN_VARIANT low nibble: 0 the default kernel; 1..3 the software-pipelined kernel with
-    // (query blocks per wave, waves per SIMD) = (3, 1), (1, 3), (2, 2), (1, 2); 6: the default kernel
-    // with PV(a) issued before QK(b) (round-2 order; 5 = the default, QK(b) ahead of PV(a): 299 -> 252 us
-    // back to back at 128 clips, neutral inside the step)
+    // VS_KNOB_ATTN_VARIANT low nibble: 0 the default kernel (QK(b) issued ahead of PV(a): 299 -> 252 us
+    // back to back at 128 clips, neutral inside the step); 6: the round-2 order (PV(a) before QK(b)),
+    // the one experimental slot kept.  The one-wave-per-SIMD kernels of round 3 (slower: DESIGN.md
+    // section 5) were removed.
     const int fv = knob(VS_KNOB_ATTN_VARIANT) & 15;
-    auto w1 = [&](auto kern, int nqb) {
-      dim3 grid((unsigned)(cdiv(N, 128 * nqb) * H * B));
-      hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse, (int)N,
-                         (int)H, scale * kLog2e);
-    };
-    if (fv == 1) {
-      w1(attn_fwd_bf16_w1_kernel<3, 1>, 3);
-    } else if (fv == 2) {
-      w1(attn_fwd_bf16_w1_kernel<1, 3>, 1);
-    } else if (fv == 3) {
-      w1(attn_fwd_bf16_w1_kernel<2, 2>, 2);
-    } else if (fv == 4) {
-      w1(attn_fwd_bf16_w1_kernel<1, 2>, 1);
-    } else {
-      dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-      auto kern = fv == 6 ? attn_fwd_bf16_kernel<false> : attn_fwd_bf16_kernel<true>;
-      hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o,
-                         lse, (int)N, (int)H, scale * kLog2e);
-    }
+    dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
+    auto kern = fv == 6 ? attn_fwd_bf16_kernel<false> : attn_fwd_bf16_kernel<true>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse, (int)N, (int)H,
+                       scale * kLog2e);
   } else if (dtype == VS_F32) {
     dim3 grid((unsigned)cdiv(N, 64), (unsigned)H, (unsigned)B);
     count_path(VS_PATH_ATTN_F32);
@@ -2278,9 +1548,7 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     hipLaunchKernelGGL(attn_rowprep_kernel, dim3((unsigned)cdiv(rows * H * 4, 256)), dim3(256), 0, s, (const bf16_t*)o,
                        ld_o, (const bf16_t*)dout, ld_do, lse, nlse2, ndel, B, (int)N, (int)H, (int)npad);
     // VS_KNOB_ATTN_VARIANT bits 4..7: 0 (default) picks 6 or 9 by grid size; 6 the software-pipelined
-    // pair kernel, 9 the 3-wave kernel (3 waves per SIMD, one 32-row unit per wave); 1..5 the multi-block kernel with (key
-    // blocks per dK/dV wave, query blocks per dQ wave, waves per SIMD) = (3, 2, 1), (1, 1, 3),
-    // (2, 2, 2), (2, 1, 2), (1, 1, 2); 6: the software-pipelined pair bodies (2 waves per SIMD)
+    // pair kernel (2 waves per SIMD), 9 the 3-wave kernel (3 waves per SIMD, one 32-row unit per wave)
     int bv = (knob(VS_KNOB_ATTN_VARIANT) >> 4) & 15;
     if (bv == 0) {
       // default by grid size: the pipelined pairs (2 waves/SIMD) when both passes fit in about two
@@ -2294,34 +1562,22 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
       }();
       bv = cdiv(N, 128) * H * B <= slots ? 6 : 9;
     }
-    auto w1 = [&](auto kern, int nbkv, int nbq) {
-      const unsigned nkv = (unsigned)(cdiv(N, 128 * nbkv) * H * B), nq = (unsigned)(cdiv(N, 128 * nbq) * H * B);
-      hipLaunchKernelGGL(kern, dim3(nkv + nq), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout,
-                         ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad, scale, (int)nkv);
-    };
-    if (bv == 1) {
-      w1(attn_bwd_bf16_w1_kernel<3, kW1DqBlocks, 1>, 3, kW1DqBlocks);
-    } else if (bv == 2) {
-      w1(attn_bwd_bf16_w1_kernel<1, 1, 3>, 1, 1);
-    } else if (bv == 3) {
-      w1(attn_bwd_bf16_w1_kernel<2, 2, 2>, 2, 2);
-    } else if (bv == 4) {
-      w1(attn_bwd_bf16_w1_kernel<2, 1, 2>, 2, 1);
-    } else if (bv == 5) {
-      w1(attn_bwd_bf16_w1_kernel<1, 1, 2>, 1, 1);
-    } else if (bv >= 6 && bv <= 8) {  // software-pipelined pairs (6: both passes, 7: dK/dV only, 8: dQ only)
-      const unsigned g = (unsigned)(cdiv(N, 128) * H * B);
-      auto kern = attn_bwd_bf16_pp_kernel<2, true, true>;
-      if (bv == 7) kern = attn_bwd_bf16_pp_kernel<2, true, false>;
-      if (bv == 8) kern = attn_bwd_bf16_pp_kernel<2, false, true>;
-      hipLaunchKernelGGL(kern, dim3(2 * g), dim3(256), 0, s,
-                         (const bf16_t*)qkv, ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv,
-                         (int)N, (int)H, (int)npad, scale, (int)g, (knob(VS_KNOB_ATTN_VARIANT) >> 8) & 3);
+#ifdef VS_DEBUG_KNOBS
+    // diagnostic builds only (build.build(variant=..., defines=["VS_DEBUG_KNOBS"])): bits 8, 9 skip the
+    // dK/dV or the dQ pass, so one pass can be timed alone -- the gradients are then WRONG
+    const int skip = (knob(VS_KNOB_ATTN_VARIANT) >> 8) & 3;
+#else
+    const int skip = 0;
+#endif
+    const unsigned g = (unsigned)(cdiv(N, 128) * H * B);  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
+    if (bv == 6) {
+      hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, true>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
+                         ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
+                         (int)npad, scale, (int)g, skip);
     } else {  // 9: the 3-wave kernel (round-2 default)
-      dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-      hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * grid.x), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
+      hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                          (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,
-                         scale, (int)grid.x, (knob(VS_KNOB_ATTN_VARIANT) >> 8) & 3);
+                         scale, (int)g, skip);
     }
   } else if (dtype == VS_F32) {
     count_path(VS_PATH_ATTN_F32);

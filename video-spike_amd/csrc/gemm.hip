@@ -2038,7 +2038,14 @@ static void launch_bf16_wres_ef(const vs_gemm_desc* d, const EpiParams& e, hipSt
   void (*kern)(const bf16_t*, int64_t, const bf16_t*, int64_t, EpiParams, int);
   if (d->b_kcontig) kern = wide ? gemm_bf16_wres_kernel<true, EF, 8> : gemm_bf16_wres_kernel<true, EF, 4>;
   else kern = wide ? gemm_bf16_wres_kernel<false, EF, 8> : gemm_bf16_wres_kernel<false, EF, 4>;
-  hipLaunchKernelGGL(kern, dim3(512), dim3(wide ? 512 : 256), 0, s, a, d->lda, b, d->ldb, e, knob(VS_KNOB_WRES_DBG));
+#ifdef VS_DEBUG_KNOBS
+  // diagnostic builds only: VS_KNOB_WRES_DBG makes the kernel re-read / re-write L2-resident blocks
+  // (timing isolation; the results are WRONG)
+  const int dbg = knob(VS_KNOB_WRES_DBG);
+#else
+  const int dbg = 0;
+#endif
+  hipLaunchKernelGGL(kern, dim3(512), dim3(wide ? 512 : 256), 0, s, a, d->lda, b, d->ldb, e, dbg);
 }
 
 template <uint32_t EF>
@@ -2623,8 +2630,10 @@ extern "C" int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx
                             dgamma, dbeta, workspace, stream);
   }
   const double ea = esize(d->dtype);
+  // minimal bytes: A and W, then per output element x (f32 read), dres (f32 read), dx (f32 write) and
+  // its bf16 copy; dh itself never leaves the chip (round 3 charged 4 B more per element: VERDICT r3)
   ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
-                    (double)(M + N) * (double)d->K * ea + (double)M * (double)N * (12.0 + (dres ? 4.0 : 0.0) +
+                    (double)(M + N) * (double)d->K * ea + (double)M * (double)N * (8.0 + (dres ? 4.0 : 0.0) +
                     (dx_lp ? 2.0 : 0.0)) + (double)M * 8.0 + (double)N * 20.0);
   EpiParams e = {};
   e.M = M; e.N = N; e.alpha = d->alpha; e.vec_ok = 1;

@@ -106,6 +106,17 @@ extern "C" int vs_knob_set(int k, int value) {
   vs::g_knob[k].store(value, std::memory_order_relaxed);
   return prev;
 }
+extern "C" int vs_knob_default(int k) {
+  VS_REQUIRE(k >= 0 && k < VS_KNOB_COUNT, "vs_knob_default: unknown knob");
+  return vs::kKnobs[k].dflt;
+}
+extern "C" int vs_debug_knobs(void) {
+#ifdef VS_DEBUG_KNOBS
+  return 1;
+#else
+  return 0;
+#endif
+}
 extern "C" int vs_dispatch_counts(int64_t* out, int n) {
   for (int i = 0; i < n && i < VS_PATH_COUNT; ++i) out[i] = vs::g_dispatch[i].load(std::memory_order_relaxed);
   return VS_PATH_COUNT;

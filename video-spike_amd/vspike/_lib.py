@@ -84,6 +84,8 @@ PROTOTYPES = {
     "vs_dispatch_reset": (ctypes.c_int, []),
     "vs_knob_get": (ctypes.c_int, [ctypes.c_int]),
     "vs_knob_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "vs_knob_default": (ctypes.c_int, [ctypes.c_int]),
+    "vs_debug_knobs": (ctypes.c_int, []),
     "vs_mse_loss": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p, c_f32, c_p, c_p]),
     "vs_comm_unique_id": (ctypes.c_int, [c_p]),
     "vs_comm_init": (ctypes.c_int, [ctypes.POINTER(c_p), c_p, c_i32, c_i32]),
@@ -236,6 +238,18 @@ def knob_get(name: str) -> int:
 def knob_set(name: str, value: int) -> int:
     """Override an A/B knob (vspike.h VS_KNOB_*); returns the previous value."""
     return int(lib().vs_knob_set(KNOB_NAMES.index(name), int(value)))
+
+
+def knobs_nondefault() -> dict:
+    """Every knob whose current value differs from its built-in default (environment or
+    vs_knob_set), plus "debug_knobs": 1 when the loaded library was built with VS_DEBUG_KNOBS
+    (diagnostic variant whose timing knobs give wrong results).  Recorded by bench.py and smoke()."""
+    h = lib()
+    out = {name: int(h.vs_knob_get(i)) for i, name in enumerate(KNOB_NAMES)
+           if int(h.vs_knob_get(i)) != int(h.vs_knob_default(i))}
+    if int(h.vs_debug_knobs()):
+        out["debug_knobs"] = 1
+    return out
 
 
 class knob:

@@ -42,8 +42,8 @@ def _sources():
 
 def source_hash(defines=()) -> str:
     """sha256 prefix over every source and header the library is compiled from (by file name and
-    content, in name order) plus the target and any extra -D defines: the id `vs_build_id()` of a
-    library built from exactly these sources returns."""
+    content, in name order) plus the target, any extra -D defines and the compile flags: the id
+    `vs_build_id()` of a library built from exactly these sources with these flags returns."""
     h = hashlib.sha256()
     srcs, headers = _sources()
     for f in sorted(srcs + headers, key=os.path.basename):
@@ -52,6 +52,10 @@ def source_hash(defines=()) -> str:
             h.update(fh.read())
         h.update(b"\0")
     h.update(("|".join([ARCH] + sorted(defines))).encode())
+    # the compile flags too (a flags-only change must change the id); the include directories by
+    # their repo-relative names, so the id is the same in every checkout of the tree
+    rel = {INCLUDE: "include", SRC_DIR: "csrc"}
+    h.update(("|".join(rel.get(f, f) for f in _flags())).encode())
     return h.hexdigest()[:16]
 
 

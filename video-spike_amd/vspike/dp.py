@@ -48,6 +48,7 @@ class GradExchange:
         self._sunk = set()
         self._accumulating = False      # a no_sync micro-step ran since the last synchronised step
         self._passthrough = set()       # ids whose gradient of this step DDP reduces itself
+        self._fwd_sync = None           # DDP's require_backward_grad_sync when the last forward ran
         if self.world > 1:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             with torch.no_grad():
@@ -68,7 +69,11 @@ class GradExchange:
         DDP's own all-reduce handles this step and nothing is launched early)."""
         if self.ddp is None or self.world == 1:
             return "overlap"
-        if not self.ddp.require_backward_grad_sync:
+        # DDP decides at FORWARD time whether this iteration synchronises (its reducer is prepared in
+        # DDP.forward); a backward run outside the no_sync() block its forward ran in must follow
+        # the forward's decision, so the flag recorded by the forward pre-hook wins
+        sync = self._fwd_sync if self._fwd_sync is not None else self.ddp.require_backward_grad_sync
+        if not sync:
             self._accumulating = True
             return "local"
         return "passthrough" if self._accumulating else "overlap"
@@ -196,4 +201,8 @@ def attach_ddp(ddp_model, bucket_mb: float = 8.0) -> "GradExchange":
     if hasattr(module, "grad_sink"):
         module.grad_sink = ex
     ddp_model.register_comm_hook(ex, _overlap_hook)
+
+    def _record_sync(mod, args):
+        ex._fwd_sync = bool(mod.require_backward_grad_sync)
+    ddp_model.register_forward_pre_hook(_record_sync)
     return ex

@@ -37,8 +37,13 @@ class GraphedStep:
         self.trainer = trainer
         self.inputs, self.target = inputs, target
         opt, model = trainer.optimizer, trainer.model
-        if not any(opt.state.values()):
-            raise RuntimeError("GraphedStep: run one eager Trainer.step first (optimizer state, arenas, shadows)")
+        # EVERY trainable parameter needs its Adam moments before capture: state created lazily inside
+        # the capture would live in the graph pool and be re-zeroed by every replay
+        missing = [p for grp in opt.param_groups for p in grp["params"]
+                   if p.requires_grad and not opt.state.get(p)]
+        if missing:
+            raise RuntimeError(f"GraphedStep: {len(missing)} trainable parameter(s) have no optimizer state; run one "
+                               "eager Trainer.step first (optimizer state, arenas, shadows)")
         # allocated outside the capture: a tensor made inside it would be re-zeroed by every replay
         self.hyper = opt.static_hyper()
         torch.cuda.synchronize()
