@@ -83,6 +83,12 @@ def parse():
     return ap.parse_args()
 
 
+def _progress(msg):
+    """Heartbeat on stderr (the JSON line stays the only stdout line): long CPU phases (baseline,
+    full-batch parity) print every few seconds so a supervisor can tell them from a hang."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _cpu_model_name():
     try:
         for line in open("/proc/cpuinfo"):
@@ -136,6 +142,7 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
                     ts.append((time.perf_counter() - t0) / B)
                 res[f"B{B}_{mode}"] = {"s_per_clip": round(statistics.median(ts), 4), "min": round(min(ts), 4),
                                        "max": round(max(ts), 4), "runs": len(ts)}
+                _progress(f"cpu baseline, {threads} threads, B={B} {mode}: {res[f'B{B}_{mode}']}")
         c = lambda k: res[k]["s_per_clip"]  # noqa: E731
         res["monotone"] = bool(c("B1_fwd_bwd") > c("B1_fwd") and c("B4_fwd_bwd") > c("B4_fwd") and
                                c("B4_fwd") <= res["B1_fwd"]["max"] and c("B4_fwd_bwd") <= res["B1_fwd_bwd"]["max"])
@@ -193,6 +200,7 @@ def full_batch_parity(ccfg, params, pixels, target, gpu, args):
         part.backward()
         loss += float(part)
         outs.append(ref.detach())
+        _progress(f"parity: CPU oracle clips {i}..{min(i + 8, B) - 1} of {B}")
     secs = time.perf_counter() - t0
     ref_out = torch.cat(outs).numpy()
     e_out = float(np.abs(gpu["log_rates"].numpy() - ref_out).max() / max(np.abs(ref_out).max(), 1e-30))
@@ -351,6 +359,8 @@ def main():
     for _ in range(args.warmup):
         trainer.step(pixels, target)
     barrier_sync()
+    if rank == 0:
+        _progress(f"warm-up done ({args.warmup} steps); timing {args.steps} steps")
     L.dispatch_reset()
     step_fn = trainer.step
     if args.graph:
@@ -421,6 +431,13 @@ def main():
             ach = nbytes / (ms / 1e3) / 1e9                                 # bytes-weighted over launches
             ent = {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                    "frac": round(ach / PEAK_HBM_GBS, 4), "work_per_launch": round(nbytes / n, 0)}
+            if name in ("fwd_mlp", "dx_mlp"):
+                # the fused MLP kernels sit near the ridge (~300 flop/B): their MFMA side as well
+                # (fwd: h2 W1^T and a W2^T; dx: h2 W1^T recomputed and dy W2 = 4 M D F flop per launch)
+                fl = 4.0 * B * N * bb.hidden_size * bb.intermediate_size
+                tf = fl / avg_s / 1e12
+                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2),
+                            "mfma_frac": round(tf / peak_mfma, 4)})
         ent.update({"ms_per_step": round(ms / args.profile_steps, 4), "launches_per_step": round(per_step, 2),
                     "avg_launch_us": round(1e3 * ms / n, 2)})
         roof_all[name] = ent

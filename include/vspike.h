@@ -145,6 +145,22 @@ int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const flo
                    const float* gamma, const float* dres, int64_t lddres, float* dx, int64_t lddx, void* dx_lp,
                    float* dgamma, float* dbeta, void* workspace, void* stream);
 
+/* The ViT block's whole MLP in one launch (mv:370-399: VideoMAEIntermediate dense + GELU(erf),
+ * VideoMAEOutput dense + residual), bf16 operands, f32 accumulation and residual stream:
+ *   x_out = y + gelu(h2 W1^T + b1) W2^T + b2,   h2 [M, D] bf16, W1 [F, D] bf16, W2 [D, F] bf16,
+ *   y / x_out [M, D] f32.  The [M, F] intermediate never reaches HBM.
+ * vs_mlp_bwd_da: its backward's GELU' product with the pre-activation RECOMPUTED from h2 (the same
+ *   MFMA chain as the forward):  da = (dy W2) * gelu'(h2 W1^T + b1)  and  a = gelu(h2 W1^T + b1),
+ *   dy [M, D] bf16 (dx' of the block), da / a [M, F] bf16 (the operands of dh2 = da W1, dW1 = da^T h2,
+ *   dW2 = dy^T a).  GELU: Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7, below bf16's 2^-9).
+ * Both need vs_mlp_fused_ok(M, D, F): D = 192 (ViT-Tiny), F % 64 == 0, F <= 3072. */
+int vs_mlp_fused_ok(int64_t M, int64_t D, int64_t F);
+int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
+               const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx, void* stream);
+int vs_mlp_bwd_da(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
+                  const void* w2, const void* dy, int64_t lddy, void* da, int64_t ldda, void* a, int64_t lda,
+                  void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Non-causal multi-head attention, head dim 64 (mv:243-258; SDPA variant mv:286-294):
  *   O = softmax(Q K^T * scale) V per (batch, head), scale = 1/sqrt(64) = 0.125.
@@ -280,7 +296,12 @@ typedef struct vs_vit_layer {
   void* h2;  float* mean2; float* rstd2;
   void* a_pre; void* a_act;                  /* [M, F] dtype.  bf16 mode (ABI v4): a_pre holds gelu'(pre),
                                                 the factor the backward's GELU' product multiplies by
-                                                (VS_EPI_GELU_GRAD / VS_EPI_MUL_AUX), not pre itself */
+                                                (VS_EPI_GELU_GRAD / VS_EPI_MUL_AUX), not pre itself.
+                                                ABI v5: a_pre == NULL selects the FUSED MLP (vs_mlp_fwd /
+                                                vs_mlp_bwd_da; bf16 and vs_mlp_fused_ok only): the forward
+                                                stores nothing of the intermediate, and a_act is [M, F]
+                                                bf16 scratch that the backward writes (gelu(pre) for dW2) —
+                                                one buffer may serve every layer of a model */
   float* x_out;                              /* [M, D] f32 */
 } vs_vit_layer;
 
@@ -397,7 +418,9 @@ const char* vs_shard_last_error(void);
 #define VS_TIMER_DW_FC1   17   /* dW1 += da^T h2 (+ db1) */
 #define VS_TIMER_DW_PROJ  18   /* dWp += dy^T o (+ dbp) */
 #define VS_TIMER_DW_QKV   19   /* dWqkv += dqkv^T h1 (+ dbqkv) */
-#define VS_TIMER_COUNT    20
+#define VS_TIMER_FWD_MLP  20   /* the fused MLP forward (vs_mlp_fwd, a_pre == NULL)   (mv:370-399) */
+#define VS_TIMER_DX_MLP   21   /* the fused MLP backward's GELU' product (vs_mlp_bwd_da) */
+#define VS_TIMER_COUNT    22
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
 int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */
@@ -425,6 +448,8 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 #define VS_PATH_ATTN_F32     15   /* exact-f32 attention, forward or backward */
 #define VS_PATH_PATCH_FUSED  16   /* patch embedding GEMM with the tubelet gather in its A-load */
 #define VS_PATH_DW_GROUPED   17   /* grouped dW launch (several weight gradients in one launch) */
+#define VS_PATH_MLP_FWD      18   /* vs_mlp_fwd: fused fc1 + GELU + fc2 + residual */
+#define VS_PATH_MLP_BWD      19   /* vs_mlp_bwd_da: fused recompute + GELU' product */
 #define VS_PATH_COUNT        24
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);

@@ -1,0 +1,392 @@
+// mlp.hip — the ViT block's MLP (VideoMAEIntermediate + VideoMAEOutput, modeling_videomae.py:370-399)
+// as fused bf16 kernels for the narrow widths (D = 192: ViT-Tiny, the bench's C2), gfx950.
+//
+// Forward, one launch:  x' = y + gelu(h2 W1^T + b1) W2^T + b2.
+//   The 4x-wide intermediate never reaches HBM: per launch the kernel reads h2 (bf16) and the f32
+//   residual y and writes x' (f32) — 1,920 B per token at D = 192 instead of the 5,000 B the two
+//   GEMMs moved with the stored gelu / gelu' pair.
+// Backward, one launch (vs_mlp_bwd_da):  pre = h2 W1^T + b1 is RECOMPUTED from h2 (same MFMA
+//   chain as the forward: bitwise the same pre and gelu), da = (dx' W2) * gelu'(pre) and a = gelu(pre)
+//   are written (bf16) for the dh2 / dW1 / dW2 products that follow.
+//
+// Structure (both kernels): 8 waves (2 per SIMD), one workgroup per CU, persistent over rounds of
+// 256 tokens (32 per wave).  Each wave computes TRANSPOSED products with its 32 tokens on the MFMA
+// N axis (lanes): pre^T = W1_c h2^T (32x32x16, W1 rows from LDS as the A operand, h2 rows straight
+// from HBM as B fragments, kept in registers for the round), then the accumulator IS the next
+// product's B operand (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+// The weights stream through LDS in chunks of 64 intermediate features (W1_c: 64 x D, W2_c: D x 64,
+// 48 KB per stage, two stages) by LDS-DMA, shared by the 8 waves, one barrier per chunk.
+// Row permutation: the W1 (and forward W2) rows of every 32-row MFMA tile are stored with bits 2 and
+// 3 of the row index swapped (DMA source selection), so that a lane's 16 accumulator registers are
+// two runs of 8 CONSECUTIVE features (registers 0-7: 8h .. 8h+7, 8-15: 16+8h ..): the accumulator
+// feeds the next MFMA in natural k order, and the epilogues write 16-byte / 32-byte runs.
+// LDS images: W1_c rows of 2D bytes, W2_c rows of 128 B; 16-B chunk c of row r is stored at chunk
+// position (c & ~7) | ((c & 7) ^ ((r >> 1) & 7)): every ds_read_b128 of a 32x32x16 operand is
+// conflict-free (16 lanes of a group = 16 rows of distinct (r & 1, chunk position)).
+#include "common.h"
+
+namespace vs {
+
+constexpr int kMlpWaves = 8;
+constexpr int kMlpFC = 64;          // intermediate features per chunk
+constexpr int kMlpMaxF = 3072;
+constexpr int kMlpRound = 32 * kMlpWaves;  // tokens per workgroup round
+
+__device__ __forceinline__ int mlp_swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+__device__ __forceinline__ int mlp_cpos(int c, int r) { return (c & ~7) | ((c & 7) ^ ((r >> 1) & 7)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base, int64_t rows_left, int64_t ld, int es) {
+  const int64_t n = rows_left > 0 ? rows_left : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(n * ld * es), 0x00020000);
+}
+
+__device__ __forceinline__ u32x4v mlp_pack8(const float* v) {
+  u32x4v u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    u[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){v[2 * q], v[2 * q + 1]}, bf16x2v));
+  return u;
+}
+
+template <int D>
+struct MlpGeom {
+  static constexpr int KS1 = D / 16;            // k-steps of the W1 product (32x32x16)
+  static constexpr int NT = D / 32;             // 32-row output tiles of the W2 product
+  static constexpr int W1B = kMlpFC * D * 2;    // bytes of one W1 chunk image
+  static constexpr int W2B = D * kMlpFC * 2;
+  static constexpr int STG = W1B + W2B;
+  static constexpr int DMA1 = W1B / 1024 / kMlpWaves;  // 1-KB LDS-DMA pieces per wave per chunk
+  static constexpr int DMA2 = W2B / 1024 / kMlpWaves;
+  static_assert(DMA1 * 1024 * kMlpWaves == W1B && DMA2 * 1024 * kMlpWaves == W2B, "DMA split");
+};
+
+// Per-lane DMA source offsets (bytes, chunk-invariant) of the W1 / W2 chunk images; the chunk adds a
+// wave-uniform base.  fwd_w2_perm: the forward's W2 image has its rows (d) swap23-permuted too.
+template <int D>
+__device__ __forceinline__ void mlp_dma_offsets(int wave, int lane, int64_t F, bool fwd_w2_perm,
+                                                uint32_t (&o1)[MlpGeom<D>::DMA1], uint32_t (&o2)[MlpGeom<D>::DMA2]) {
+  using G = MlpGeom<D>;
+#pragma unroll
+  for (int k = 0; k < G::DMA1; ++k) {
+    const int P = 64 * (wave * G::DMA1 + k) + lane;  // 16-B chunk index of the image
+    const int r = P / (D / 8), cp = P % (D / 8);
+    const int grow = 32 * (r >> 5) + mlp_swap23(r & 31);
+    const int cl = mlp_cpos(cp, r);  // the map is an involution on the low 3 bits
+    o1[k] = (uint32_t)((grow * D + 8 * cl) * 2);
+  }
+#pragma unroll
+  for (int k = 0; k < G::DMA2; ++k) {
+    const int P = 64 * (wave * G::DMA2 + k) + lane;
+    const int p = P / 8, cp = P % 8;
+    const int d = fwd_w2_perm ? 32 * (p >> 5) + mlp_swap23(p & 31) : p;
+    const int cl = cp ^ ((p >> 1) & 7);
+    o2[k] = (uint32_t)(((int64_t)d * F + 8 * cl) * 2);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void mlp_dma_chunk(const bf16_t* w1, const bf16_t* w2, int c, char* stage, int wave,
+                                              const uint32_t (&o1)[MlpGeom<D>::DMA1],
+                                              const uint32_t (&o2)[MlpGeom<D>::DMA2]) {
+  using G = MlpGeom<D>;
+  const bf16_t* s1 = w1 + (int64_t)c * kMlpFC * D;
+  const bf16_t* s2 = w2 + (int64_t)c * kMlpFC;
+#pragma unroll
+  for (int k = 0; k < G::DMA1; ++k) glds16_asm_so(s1, o1[k], stage + 1024 * (wave * G::DMA1 + k));
+#pragma unroll
+  for (int k = 0; k < G::DMA2; ++k) glds16_asm_so(s2, o2[k], stage + G::W1B + 1024 * (wave * G::DMA2 + k));
+}
+
+// pre^T (two 32-row tiles of the chunk's 64 features x 32 tokens) = W1_c h2^T
+template <int D>
+__device__ __forceinline__ void mlp_stage1(const char* st, int lane, const u32x4v (&xf)[MlpGeom<D>::KS1],
+                                           f32x16 (&pre)[2]) {
+  using G = MlpGeom<D>;
+  const int rr = lane & 31, h = lane >> 5;
+  pre[0] = f32x16{};
+  pre[1] = f32x16{};
+#pragma unroll
+  for (int s = 0; s < G::KS1; ++s) {
+    const int cp = mlp_cpos(2 * s + h, rr);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const bf16x8 wa = *(const bf16x8*)(st + (32 * t + rr) * (2 * D) + 16 * cp);
+      pre[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, __builtin_bit_cast(bf16x8, xf[s]), pre[t], 0, 0, 0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t* __restrict__ h2, int64_t ldh,
+                                                                    const bf16_t* __restrict__ w1,
+                                                                    const float* __restrict__ b1,
+                                                                    const bf16_t* __restrict__ w2,
+                                                                    const float* __restrict__ b2,
+                                                                    const float* __restrict__ y, int64_t ldy,
+                                                                    float* __restrict__ xo, int64_t ldx, int64_t M,
+                                                                    int F) {
+  using G = MlpGeom<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STG];
+  __shared__ __attribute__((aligned(16))) float b1s[kMlpMaxF];
+  __shared__ __attribute__((aligned(16))) float b2s[D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rr = lane & 31, h = lane >> 5;
+  const int nch = F / kMlpFC;
+  const int64_t nround = (M + kMlpRound - 1) / kMlpRound;
+  if ((int64_t)blockIdx.x >= nround) return;  // workgroup-uniform
+  uint32_t o1[G::DMA1], o2[G::DMA2];
+  mlp_dma_offsets<D>(wave, lane, F, true, o1, o2);
+  mlp_dma_chunk<D>(w1, w2, 0, smem, wave, o1, o2);  // chunk 0 of the first round -> stage 0
+  for (int i = tid; i < F; i += 64 * kMlpWaves) b1s[i] = b1[i];
+  if (tid < D) b2s[tid] = b2[tid];
+
+  // h2 fragments of a round: lane (token rr, half h) holds d = 16 s + 8 h .. + 7 of its token
+  u32x4v xf[G::KS1];
+  auto load_x = [&](int64_t rd) {
+    const int64_t row0 = rd * kMlpRound + 32 * wave;
+    const auto rx = mlp_rsrc(h2 + row0 * ldh, M - row0, ldh, 2);
+#pragma unroll
+    for (int s = 0; s < G::KS1; ++s)
+      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)((rr * ldh + 16 * s + 8 * h) * 2), 0, 0);
+  };
+  load_x(blockIdx.x);
+  int q = 0;  // chunk stream position: stage q & 1
+  for (int64_t rd = blockIdx.x; rd < nround; rd += gridDim.x) {
+    const bool more = rd + gridDim.x < nround;
+    f32x16 acc[G::NT];
+#pragma unroll
+    for (int T = 0; T < G::NT; ++T) acc[T] = f32x16{};
+    for (int c = 0; c < nch; ++c, ++q) {
+      // this chunk's DMA pieces (every wave's) landed; every wave is done with the other stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const bool last = c + 1 == nch;
+      if (!last || more) mlp_dma_chunk<D>(w1, w2, last ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      const char* st = smem + (q & 1) * G::STG;
+      f32x16 pre[2];
+      mlp_stage1<D>(st, lane, xf, pre);
+      if (last && more) load_x(rd + gridDim.x);  // the fragments are dead after the last chunk's W1 product
+      // bias + GELU, as the next product's B fragments (k-step s = 2 t + j2: features 16 s + 8 h + j)
+      u32x4v af[4];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j2 = 0; j2 < 2; ++j2) {
+          const float* bb = b1s + c * kMlpFC + 32 * t + 16 * j2 + 8 * h;
+          const f32x4 bl = *(const f32x4*)bb, bh = *(const f32x4*)(bb + 4);
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gelu_fast(pre[t][8 * j2 + j] + (j < 4 ? bl[j] : bh[j - 4]));
+          af[2 * t + j2] = mlp_pack8(v);
+        }
+      // x'^T += W2_c a^T
+      const char* st2 = st + G::W1B;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int T = 0; T < G::NT; ++T) {
+          const int p = 32 * T + rr;
+          const bf16x8 wb = *(const bf16x8*)(st2 + p * 128 + 16 * ((2 * s + h) ^ ((p >> 1) & 7)));
+          acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, __builtin_bit_cast(bf16x8, af[s]), acc[T], 0, 0, 0);
+        }
+      }
+    }
+    // epilogue: x' = y + acc + b2; lane (token rr, half h) holds d = 32 T + 16 j2 + 8 h .. + 7
+    const int64_t row0 = rd * kMlpRound + 32 * wave;
+    const auto ry = mlp_rsrc(y + row0 * ldy, M - row0, ldy, 4);
+    const auto rxo = mlp_rsrc(xo + row0 * ldx, M - row0, ldx, 4);
+#pragma unroll
+    for (int T = 0; T < G::NT; ++T)
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2) {
+        const int d0 = 32 * T + 16 * j2 + 8 * h;
+        const uint32_t oy = (uint32_t)((rr * ldy + d0) * 4), ox = (uint32_t)((rr * ldx + d0) * 4);
+        const f32x4 y0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy, 0, 0));
+        const f32x4 y1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy + 16, 0, 0));
+        const f32x4 c0 = *(const f32x4*)(b2s + d0), c1 = *(const f32x4*)(b2s + d0 + 4);
+        f32x4 r0, r1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          r0[j] = y0[j] + (acc[T][8 * j2 + j] + c0[j]);
+          r1[j] = y1[j] + (acc[T][8 * j2 + 4 + j] + c1[j]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r0), rxo, ox, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r1), rxo, ox + 16, 0, 0);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward: da = (dx' W2) * gelu'(pre), a = gelu(pre), pre recomputed from h2
+// ---------------------------------------------------------------------------------------------
+// The W2 product here is da^T = W2_c^T dx'^T: its A operand (rows = features, k = d) is a COLUMN read
+// of the W2 image, done with ds_read_b64_tr_b16 (each lane of a 16-lane group supplies the address
+// of one 4-column quad of one row, so the swap23 feature order of the W1 product is chosen per lane).
+template <int D>
+__global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf16_t* __restrict__ h2, int64_t ldh,
+                                                                       const bf16_t* __restrict__ w1,
+                                                                       const float* __restrict__ b1,
+                                                                       const bf16_t* __restrict__ w2,
+                                                                       const bf16_t* __restrict__ dy, int64_t lddy,
+                                                                       bf16_t* __restrict__ da, int64_t ldda,
+                                                                       bf16_t* __restrict__ aout, int64_t lda,
+                                                                       int64_t M, int F) {
+  using G = MlpGeom<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::STG];
+  __shared__ __attribute__((aligned(16))) float b1s[kMlpMaxF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rr = lane & 31, h = lane >> 5;
+  const int nch = F / kMlpFC;
+  const int64_t nround = (M + kMlpRound - 1) / kMlpRound;
+  if ((int64_t)blockIdx.x >= nround) return;
+  uint32_t o1[G::DMA1], o2[G::DMA2];
+  mlp_dma_offsets<D>(wave, lane, F, false, o1, o2);  // W2 image rows in natural d order
+  mlp_dma_chunk<D>(w1, w2, 0, smem, wave, o1, o2);
+  for (int i = tid; i < F; i += 64 * kMlpWaves) b1s[i] = b1[i];
+
+  // transposed-read addresses (bytes within the W2 image) of the A operand of da^T, per tile t
+  // (features 32 t ..), k-step s and half e (k = 16 s + 8 hh + 4 e + qrow): lane i of 16-lane group
+  // g supplies row qrow = i >> 2 and column quad pq = i & 3 -> feature quad 16 (g & 1) + 4 swap(pq)
+  const int g16 = lane >> 4, i16 = lane & 15, hh = g16 >> 1;
+  const int pq = i16 & 3, qrow = i16 >> 2;
+  const int fq = 16 * (g16 & 1) + 4 * (((pq & 1) << 1) | (pq >> 1));  // swap23 on the feature index
+  auto tr_addr = [&](int t, int s, int e) {
+    const int d = 16 * s + 8 * hh + 4 * e + qrow;  // image row (natural order)
+    const int f = 32 * t + fq;                     // first column of the quad
+    const int cl = f >> 3;
+    return d * 128 + 16 * (cl ^ ((d >> 1) & 7)) + 2 * (f & 7);
+  };
+
+  u32x4v xf[G::KS1], yf[G::KS1];
+  auto load_xy = [&](int64_t rd) {
+    const int64_t row0 = rd * kMlpRound + 32 * wave;
+    const auto rx = mlp_rsrc(h2 + row0 * ldh, M - row0, ldh, 2);
+    const auto ry = mlp_rsrc(dy + row0 * lddy, M - row0, lddy, 2);
+#pragma unroll
+    for (int s = 0; s < G::KS1; ++s) {
+      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)((rr * ldh + 16 * s + 8 * h) * 2), 0, 0);
+      yf[s] = __builtin_amdgcn_raw_buffer_load_b128(ry, (uint32_t)((rr * lddy + 16 * s + 8 * h) * 2), 0, 0);
+    }
+  };
+  load_xy(blockIdx.x);
+  int q = 0;
+  for (int64_t rd = blockIdx.x; rd < nround; rd += gridDim.x) {
+    const bool more = rd + gridDim.x < nround;
+    const int64_t row0 = rd * kMlpRound + 32 * wave;
+    const auto rda = mlp_rsrc(da + row0 * ldda, M - row0, ldda, 2);
+    const auto raa = mlp_rsrc(aout + row0 * lda, M - row0, lda, 2);
+    for (int c = 0; c < nch; ++c, ++q) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const bool last = c + 1 == nch;
+      if (!last || more) mlp_dma_chunk<D>(w1, w2, last ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      const char* st = smem + (q & 1) * G::STG;
+      f32x16 pre[2];
+      mlp_stage1<D>(st, lane, xf, pre);
+      // da^T (same register layout as pre^T) = W2_c^T dx'^T
+      f32x16 dac[2] = {f32x16{}, f32x16{}};
+      const char* st2 = st + G::W1B;
+#pragma unroll
+      for (int s = 0; s < G::KS1; ++s) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + tr_addr(t, s, 0)));
+          const short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + tr_addr(t, s, 1)));
+          typedef __attribute__((ext_vector_type(8))) short short8v;
+          const short8v wv = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+          dac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wv),
+                                                            __builtin_bit_cast(bf16x8, yf[s]), dac[t], 0, 0, 0);
+        }
+      }
+      if (last && more) load_xy(rd + gridDim.x);
+      // lane (token rr, half h): features c*64 + 32 t + 16 j2 + 8 h .. + 7
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j2 = 0; j2 < 2; ++j2) {
+          const int f0 = c * kMlpFC + 32 * t + 16 * j2 + 8 * h;
+          const f32x4 bl = *(const f32x4*)(b1s + f0), bh = *(const f32x4*)(b1s + f0 + 4);
+          float av[8], dv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float gr;
+            av[j] = gelu_fast_both(pre[t][8 * j2 + j] + (j < 4 ? bl[j] : bh[j - 4]), gr);
+            dv[j] = dac[t][8 * j2 + j] * gr;
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(dv), rda, (uint32_t)((rr * ldda + f0) * 2), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(av), raa, (uint32_t)((rr * lda + f0) * 2), 0, 0);
+        }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+static int mlp_grid(int64_t M) {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n;
+  }();
+  const int64_t rounds = (M + kMlpRound - 1) / kMlpRound;
+  return (int)(rounds < cus ? rounds : cus);
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" int vs_mlp_fused_ok(int64_t M, int64_t D, int64_t F) {
+  return D == 192 && F % kMlpFC == 0 && F >= kMlpFC && F <= kMlpMaxF && M > 0 && M * F * 2 < (int64_t(1) << 31) &&
+                 M * D * 4 < (int64_t(1) << 31)
+             ? 1
+             : 0;
+}
+
+extern "C" int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
+                          const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx,
+                          void* stream) {
+  VS_REQUIRE(vs_mlp_fused_ok(M, D, F), "vs_mlp_fwd: needs D = 192, F % 64 == 0, F <= 3072");
+  VS_REQUIRE(h2 && w1 && b1 && w2 && b2 && y && x_out, "vs_mlp_fwd: null pointer");
+  VS_REQUIRE(ldh >= D && ldh % 8 == 0 && ldy >= D && ldy % 4 == 0 && ldx >= D && ldx % 4 == 0 &&
+                 aligned16(h2) && aligned16(w1) && aligned16(w2) && aligned16(y) && aligned16(x_out) &&
+                 aligned16(b1) && aligned16(b2),
+             "vs_mlp_fwd: rows must be 16-byte aligned");
+  VS_REQUIRE(M * ldy * 4 < (int64_t(1) << 31) && M * ldx * 4 < (int64_t(1) << 31) && M * ldh * 2 < (int64_t(1) << 31),
+             "vs_mlp_fwd: operand too large for 32-bit buffer offsets");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
+                    (double)M * (double)D * (2.0 + 4.0 + 4.0) + (double)F * (double)D * 4.0 + (double)(F + D) * 4.0);
+  count_path(VS_PATH_MLP_FWD);
+  hipLaunchKernelGGL(mlp_fwd_kernel<192>, dim3((unsigned)mlp_grid(M)), dim3(64 * kMlpWaves), 0, s, (const bf16_t*)h2,
+                     ldh, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, y, ldy, x_out, ldx, M, (int)F);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_mlp_bwd_da(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1,
+                             const float* b1, const void* w2, const void* dy, int64_t lddy, void* da, int64_t ldda,
+                             void* a, int64_t lda, void* stream) {
+  VS_REQUIRE(vs_mlp_fused_ok(M, D, F), "vs_mlp_bwd_da: needs D = 192, F % 64 == 0, F <= 3072");
+  VS_REQUIRE(h2 && w1 && b1 && w2 && dy && da && a, "vs_mlp_bwd_da: null pointer");
+  VS_REQUIRE(ldh >= D && ldh % 8 == 0 && lddy >= D && lddy % 8 == 0 && ldda >= F && ldda % 8 == 0 && lda >= F &&
+                 lda % 8 == 0 && aligned16(h2) && aligned16(w1) && aligned16(w2) && aligned16(dy) && aligned16(da) &&
+                 aligned16(a) && aligned16(b1),
+             "vs_mlp_bwd_da: rows must be 16-byte aligned");
+  VS_REQUIRE(M * ldda * 2 < (int64_t(1) << 31) && M * lda * 2 < (int64_t(1) << 31) && M * ldh * 2 < (int64_t(1) << 31) &&
+                 M * lddy * 2 < (int64_t(1) << 31),
+             "vs_mlp_bwd_da: operand too large for 32-bit buffer offsets");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
+                    (double)M * (double)D * 4.0 + (double)M * (double)F * 4.0 + (double)F * (double)D * 4.0 +
+                        (double)F * 4.0);
+  count_path(VS_PATH_MLP_BWD);
+  hipLaunchKernelGGL(mlp_bwd_da_kernel<192>, dim3((unsigned)mlp_grid(M)), dim3(64 * kMlpWaves), 0, s,
+                     (const bf16_t*)h2, ldh, (const bf16_t*)w1, b1, (const bf16_t*)w2, (const bf16_t*)dy, lddy,
+                     (bf16_t*)da, ldda, (bf16_t*)a, lda, M, (int)F);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

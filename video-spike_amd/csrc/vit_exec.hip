@@ -64,11 +64,18 @@ static int stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
   return (int)e;
 }
 
+// a_pre == NULL selects the fused MLP (vs_mlp_fwd / vs_mlp_bwd_da): bf16, a shape vs_mlp_fused_ok
+// accepts; a_act then points at [M, F] bf16 scratch that the BACKWARD writes (gelu(pre) for dW2)
+static bool mlp_fused(const vs_vit_layer* L) { return L->a_pre == nullptr; }
+
 static int check_layer(const vs_vit_layer* L) {
   VS_REQUIRE(L, "vs_vit_layer: null");
   VS_REQUIRE(L->dtype == VS_F32 || L->dtype == VS_BF16, "vs_vit_layer: bad dtype");
   VS_REQUIRE(L->hidden == L->heads * 64, "vs_vit_layer: hidden must be heads*64");
   VS_REQUIRE(L->batch > 0 && L->tokens > 0 && L->mlp > 0, "vs_vit_layer: empty");
+  VS_REQUIRE(!mlp_fused(L) || (L->dtype == VS_BF16 && vs_mlp_fused_ok(L->batch * L->tokens, L->hidden, L->mlp) &&
+                               L->a_act),
+             "vs_vit_layer: a_pre == NULL (fused MLP) needs bf16, D = 192, F % 64 == 0 and an a_act scratch");
   return VS_OK;
 }
 
@@ -103,6 +110,10 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   }
   if (T != VS_BF16)
     VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
+  if (mlp_fused(L)) {  // the whole MLP in one launch; nothing of the [M, F] intermediate is stored
+    TimerTag tag(VS_TIMER_FWD_MLP);
+    return vs_mlp_fwd(M, D, F, L->h2, D, L->w_fc1, L->b_fc1, L->w_fc2, L->b_fc2, L->y, D, L->x_out, D, stream);
+  }
   {
     // bf16: a_pre holds gelu'(pre) (VS_EPI_GELU_GRAD), so the backward's GELU' product is a plain
     // multiply (VS_EPI_MUL_AUX) instead of an erf/exp evaluation per element; f32 keeps pre.
@@ -158,7 +169,18 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   auto fork = [&](int k) -> int { return ch ? stream_wait(ms, ss, ev[k]) : 0; };
 
   // ---- MLP: x' = y + a W2^T + b2
-  VS_CALL(fork(0));  // dx' (and the block's saved activations) ready
+  if (mlp_fused(L)) {
+    // a (L->a_act) and d_a are rewritten here: the previous block's dW2 / dW1 read them
+    VS_CALL(wait_prev(0));
+    VS_CALL(wait_prev(1));
+    {  // da = (dx' W2) * gelu'(pre), a = gelu(pre), pre recomputed from h2
+      TimerTag tag(VS_TIMER_DX_MLP);
+      VS_CALL(vs_mlp_bwd_da(M, D, F, L->h2, D, L->w_fc1, L->b_fc1, L->w_fc2, gx, D, G->d_a, F, L->a_act, F, stream));
+    }
+    VS_CALL(fork(0));  // da, a ready
+  } else {
+    VS_CALL(fork(0));  // dx' (and the block's saved activations) ready
+  }
   {  // [side] dW2[D,F] += dx'^T a;  db2 += colsum(dx') fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, D, F, M, gx, D, L->a_act, F, G->w_fc2, F, VS_EPI_ATOMIC);
     TimerTag tag(VS_TIMER_DW_FC2);
@@ -168,16 +190,18 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
     VS_CALL(vs_gemm(&g, side));
     VS_CALL(mark(0));
   }
-  VS_CALL(wait_prev(1));  // d_a is read by the previous block's dW1
-  {  // d(pre-act) = (dx' W2) * gelu'(pre)
-    vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F,
-                           lp ? VS_EPI_MUL_AUX : VS_EPI_GELU_BWD);  // bf16: a_pre = gelu'(pre)
-    TimerTag tag(VS_TIMER_DX_FC2);
-    g.aux_in = L->a_pre;
-    g.ld_aux_in = F;
-    VS_CALL(vs_gemm(&g, stream));
+  if (!mlp_fused(L)) {
+    VS_CALL(wait_prev(1));  // d_a is read by the previous block's dW1
+    {  // d(pre-act) = (dx' W2) * gelu'(pre)
+      vs_gemm_desc g = gdesc(T, T, true, false, M, F, D, gx, D, L->w_fc2, F, G->d_a, F,
+                             lp ? VS_EPI_MUL_AUX : VS_EPI_GELU_BWD);  // bf16: a_pre = gelu'(pre)
+      TimerTag tag(VS_TIMER_DX_FC2);
+      g.aux_in = L->a_pre;
+      g.ld_aux_in = F;
+      VS_CALL(vs_gemm(&g, stream));
+    }
+    VS_CALL(fork(1));  // da ready
   }
-  VS_CALL(fork(1));  // da ready
   {  // [side] dW1[F,D] += da^T h2;  db1 += colsum(da) fused
     vs_gemm_desc g = gdesc(T, VS_F32, false, false, F, D, M, G->d_a, F, L->h2, D, G->w_fc1, D, VS_EPI_ATOMIC);
     TimerTag tag(VS_TIMER_DW_FC1);

@@ -24,12 +24,14 @@ TIMER_ATTN_FWD, TIMER_ATTN_BWD, TIMER_GEMM, TIMER_GEMM_DW, TIMER_LN_FWD, TIMER_L
 TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "adamw", "misc",
                # the block executor's products (vspike.h VS_TIMER_FWD_QKV ..): fwd, dX, dW of each Linear
                "fwd_qkv", "fwd_proj", "fwd_fc1", "fwd_fc2", "dx_fc2", "dx_fc1", "dx_proj", "dx_qkv",
-               "dw_fc2", "dw_fc1", "dw_proj", "dw_qkv")
+               "dw_fc2", "dw_fc1", "dw_proj", "dw_qkv",
+               # the fused MLP (a_pre == NULL in vs_vit_layer): forward, backward GELU' product
+               "fwd_mlp", "dx_mlp")
 
 # vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
               "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
-              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped")
+              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd")
 PATH_COUNT = 24
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
@@ -109,6 +111,10 @@ PROTOTYPES = {
     "vs_gemm_ln_fwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_p, ctypes.c_float, c_p, c_i64, c_p, c_p, c_p]),
     "vs_gemm_ln_bwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
                                       c_p, c_p, c_p, c_p, c_p]),
+    "vs_mlp_fused_ok": (ctypes.c_int, [c_i64, c_i64, c_i64]),
+    "vs_mlp_fwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p]),
+    "vs_mlp_bwd_da": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p,
+                                     c_i64, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),
     "vs_attn_bwd_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "vs_attn_bwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,

@@ -52,6 +52,35 @@ def linear(x, w, out, *, bias=None, epilogue=0, **kw):
                 ldc=out.stride(0), epilogue=epilogue, bias=bias, **kw)
 
 
+def mlp_fused_ok(M: int, D: int, F: int) -> bool:
+    """vs_mlp_fused_ok: the fused MLP kernels take this shape (bf16, D = 192, F % 64 == 0)."""
+    return bool(lib().vs_mlp_fused_ok(int(M), int(D), int(F)))
+
+
+def mlp_fwd(h2, w1, b1, w2, b2, y, out):
+    """out = y + gelu(h2 @ w1^T + b1) @ w2^T + b2 in one launch (vs_mlp_fwd): h2 [M, D] bf16, w1 [F, D],
+    w2 [D, F] bf16, y / out [M, D] f32 (modeling_videomae.py:370-399)."""
+    require_device(h2, w1, w2, y, out)
+    M, D = h2.shape
+    F = w1.shape[0]
+    check(lib().vs_mlp_fwd(M, D, F, h2.data_ptr(), h2.stride(0), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                           b2.data_ptr(), y.data_ptr(), y.stride(0), out.data_ptr(), out.stride(0), stream()),
+          "vs_mlp_fwd")
+    return out
+
+
+def mlp_bwd_da(h2, w1, b1, w2, dy, da, a):
+    """da = (dy @ w2) * gelu'(h2 @ w1^T + b1) and a = gelu(h2 @ w1^T + b1), the pre-activation
+    recomputed (vs_mlp_bwd_da): dy [M, D] bf16, da / a [M, F] bf16."""
+    require_device(h2, w1, w2, dy, da, a)
+    M, D = h2.shape
+    F = w1.shape[0]
+    check(lib().vs_mlp_bwd_da(M, D, F, h2.data_ptr(), h2.stride(0), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                              dy.data_ptr(), dy.stride(0), da.data_ptr(), da.stride(0), a.data_ptr(), a.stride(0),
+                              stream()), "vs_mlp_bwd_da")
+    return da, a
+
+
 def linear_dx(dy, w, out, *, epilogue=0, accumulate=False, **kw):
     """out[M,K] = dy[M,N] @ w[N,K]; accumulate=True adds into an f32 `out` with split-K atomics
     (for skinny products whose reduction N is long, e.g. the head's dZ over 100*neurons)."""

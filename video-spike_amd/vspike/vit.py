@@ -45,6 +45,10 @@ _SIDE = os.environ.get("VSPIKE_SIDE", "1") != "0"
 # VSPIKE_LN_FUSE=1 / 0 forces it either way
 _LN_FUSE = {"1": True, "0": False}.get(os.environ.get("VSPIKE_LN_FUSE", ""), None)
 _LN_FUSE_ROWS = 65536
+# The fused MLP (vs_mlp_fwd / vs_mlp_bwd_da: the 4x-wide intermediate never stored, the backward
+# recomputes the pre-activation) wherever the shape allows it (bf16, D = 192); VSPIKE_MLP_FUSE=0 keeps
+# the two-GEMM MLP with the stored gelu / gelu' pair (A/B)
+_MLP_FUSE = os.environ.get("VSPIKE_MLP_FUSE", "1") != "0"
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -212,15 +216,21 @@ class VideoMAE(nn.Module):
         st["grad_sink"] = None
         return st
 
+    def _mlp_fused(self, B: int) -> bool:
+        cfg = self.backbone
+        return (_MLP_FUSE and self.compute_dtype == torch.bfloat16 and
+                ops.mlp_fused_ok(B * cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size))
+
     # activation buffers of one block (names match VitLayer fields)
     def _plan_layer(self, ar: Arena, pfx: str, B: int):
         cfg, dt = self.backbone, self.compute_dtype
         N, D, F, H = cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size, cfg.num_attention_heads
         M = B * N
+        mlp = () if self._mlp_fused(B) else (("a_pre", (M, F), dt), ("a_act", (M, F), dt))
         for name, shape, d in (("h1", (M, D), dt), ("mean1", (M,), torch.float32), ("rstd1", (M,), torch.float32),
                                ("qkv", (M, 3 * D), dt), ("attn_o", (M, D), dt), ("lse", (B, H, N), torch.float32),
                                ("y", (M, D), torch.float32), ("h2", (M, D), dt), ("mean2", (M,), torch.float32),
-                               ("rstd2", (M,), torch.float32), ("a_pre", (M, F), dt), ("a_act", (M, F), dt)):
+                               ("rstd2", (M,), torch.float32)) + mlp:
             ar.add(pfx + name, shape, d)
 
     def _layer_struct(self, i, B, x_in, x_out, act, pfx, w_lp, w32):
@@ -237,8 +247,12 @@ class VideoMAE(nn.Module):
         for k in ("w_qkv", "w_proj", "w_fc1", "w_fc2"):
             setattr(s, k, lay.view(w_lp, f"{i}.{k}").data_ptr())
         s.x_in, s.x_out = x_in.data_ptr(), x_out.data_ptr()
-        for k in ("h1", "mean1", "rstd1", "qkv", "attn_o", "lse", "y", "h2", "mean2", "rstd2", "a_pre", "a_act"):
+        for k in ("h1", "mean1", "rstd1", "qkv", "attn_o", "lse", "y", "h2", "mean2", "rstd2"):
             setattr(s, k, act[pfx + k].data_ptr())
+        if self._mlp_fused(B):   # fused MLP: a_pre NULL, a_act = the backward's shared gelu(pre) scratch
+            s.a_pre, s.a_act = None, act["mlp_a"].data_ptr()
+        else:
+            s.a_pre, s.a_act = act[pfx + "a_pre"].data_ptr(), act[pfx + "a_act"].data_ptr()
         return s
 
     def set_side_stream(self, enabled: bool) -> None:
@@ -320,6 +334,8 @@ class VideoMAE(nn.Module):
         ar.add("x0", (M, D), torch.float32)
         for j in range(Lyr if save_encoder else 1):
             self._plan_layer(ar, f"L{j}.", B)
+        if self._mlp_fused(B):   # gelu(pre) of the layer being back-propagated (written by its backward)
+            ar.add("mlp_a", (M, cfg.intermediate_size), dt)
         for j in range(Lyr if save_encoder else 2):
             ar.add(f"X{j}", (M, D), torch.float32)
         if lp:
