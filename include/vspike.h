@@ -32,6 +32,8 @@ extern "C" {
 #define VS_F32 0
 #define VS_BF16 1
 #define VS_U8 2   /* raw video frames only (vs_video_preprocess) */
+#define VS_FP8 3  /* OCP e4m3 with MX (E8M0 per 32 k) scales: vs_gemm_mxfp8 operands; as vs_vit_layer.dtype:
+                     bf16 everywhere + MX-FP8 forward block products (BASELINE C5) */
 
 int vs_version(void);                 /* ABI version (monotonic) */
 /* sha256 prefix (16 hex digits) of the sources this library was compiled from: every csrc/ file
@@ -154,6 +156,20 @@ int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const flo
  *   dy [M, D] bf16 (dx' of the block), da / a [M, F] bf16 (the operands of dh2 = da W1, dW1 = da^T h2,
  *   dW2 = dy^T a).  GELU: Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7, below bf16's 2^-9).
  * Both need vs_mlp_fused_ok(M, D, F): D = 192 (ViT-Tiny), F % 64 == 0, F <= 3072. */
+/* ------------------------------------------------------------------------------------------
+ * MX-FP8 (BASELINE C5 "fp8 MFMA"): OCP e4m3 elements with one E8M0 power-of-two scale per 32
+ * consecutive k (scale = 2^(e - 127), e = 127 + ceil(log2(amax / 448)) over the block: nothing
+ * saturates).  vs_quant_mxfp8: x [M, K] (f32 or bf16) -> q [M, K] e4m3 bytes + scales [M, K / 32]
+ * bytes.  vs_gemm_mxfp8: the Linear forward of the ViT block on v_mfma_scale_f32_32x32x64_f8f6f4,
+ * C = A B^T with A [M, K] and B [N, K] (nn.Linear layout) both VS_FP8, scales as vs_quant_mxfp8
+ * writes them, then vs_gemm's epilogue (0, BIAS, BIAS|RESIDUAL or BIAS|GELU|GELU_GRAD); K % 128 == 0,
+ * N % 128 == 0.  Replaces the fp32 nn.Linear forwards mv:233-236, 312-319, 373-383, 390-397 at C5.
+ * ------------------------------------------------------------------------------------------ */
+int vs_quant_mxfp8(int32_t in_dtype, int64_t M, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq,
+                   void* scales, int64_t ld_scales, void* stream);
+int vs_gemm_mxfp8(const vs_gemm_desc* d, const void* scale_a, int64_t ld_scale_a, const void* scale_b,
+                  int64_t ld_scale_b, void* stream);
+
 int vs_mlp_fused_ok(int64_t M, int64_t D, int64_t F);
 int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
                const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx, void* stream);
@@ -303,7 +319,11 @@ typedef struct vs_vit_layer {
                                                 bf16 scratch that the backward writes (gelu(pre) for dW2) —
                                                 one buffer may serve every layer of a model */
   float* x_out;                              /* [M, D] f32 */
+  /* ABI v6: dtype VS_FP8 (bf16 block with MX-FP8 forward products, BASELINE C5) needs this scratch,
+     vs_vit_fp8_workspace_bytes(M, D, F) bytes, 256-B aligned; unused otherwise */
+  void* fp8_ws; int64_t fp8_ws_bytes;
 } vs_vit_layer;
+size_t vs_vit_fp8_workspace_bytes(int64_t M, int64_t D, int64_t F);
 
 typedef struct vs_vit_layer_grad {
   /* weight gradients (f32, ACCUMULATED) */
@@ -450,6 +470,7 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 #define VS_PATH_DW_GROUPED   17   /* grouped dW launch (several weight gradients in one launch) */
 #define VS_PATH_MLP_FWD      18   /* vs_mlp_fwd: fused fc1 + GELU + fc2 + residual */
 #define VS_PATH_MLP_BWD      19   /* vs_mlp_bwd_da: fused recompute + GELU' product */
+#define VS_PATH_GEMM_FP8     20   /* vs_gemm_mxfp8: block-scaled fp8 MFMA GEMM */
 #define VS_PATH_COUNT        24
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);

@@ -68,9 +68,42 @@ static int stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
 // accepts; a_act then points at [M, F] bf16 scratch that the BACKWARD writes (gelu(pre) for dW2)
 static bool mlp_fused(const vs_vit_layer* L) { return L->a_pre == nullptr; }
 
+// MX-FP8 scratch of one block forward (the A operand of the product being run, its scales, the
+// weight and its scales; reused product by product in stream order)
+struct Fp8Ws {
+  uint8_t *aq, *as, *wq, *ws;
+};
+static size_t a256(size_t x) { return (x + 255) / 256 * 256; }
+static Fp8Ws fp8_ws(const vs_vit_layer* L) {
+  const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp, KM = D > F ? D : F;
+  const int64_t WM = 3 * D * D > F * D ? 3 * D * D : F * D;
+  Fp8Ws w;
+  w.aq = (uint8_t*)L->fp8_ws;
+  w.as = w.aq + a256((size_t)(M * KM));
+  w.wq = w.as + a256((size_t)(M * KM / 32));
+  w.ws = w.wq + a256((size_t)WM);
+  return w;
+}
+
+// one MX-FP8 forward product: A (bf16 [M, K]) and W (bf16 [N, K]) quantised into the scratch, then
+// the block-scaled GEMM with the given epilogue (the epilogue fields of g; g.a / g.b are replaced)
+static int fp8_product(const vs_vit_layer* L, vs_gemm_desc g, void* stream) {
+  const Fp8Ws w = fp8_ws(L);
+  VS_CALL(vs_quant_mxfp8(VS_BF16, g.M, g.K, g.a, g.lda, w.aq, g.K, w.as, g.K / 32, stream));
+  VS_CALL(vs_quant_mxfp8(VS_BF16, g.N, g.K, g.b, g.ldb, w.wq, g.K, w.ws, g.K / 32, stream));
+  g.dtype = VS_FP8;
+  g.a = w.aq; g.lda = g.K;
+  g.b = w.wq; g.ldb = g.K;
+  return vs_gemm_mxfp8(&g, w.as, g.K / 32, w.ws, g.K / 32, stream);
+}
+
 static int check_layer(const vs_vit_layer* L) {
   VS_REQUIRE(L, "vs_vit_layer: null");
-  VS_REQUIRE(L->dtype == VS_F32 || L->dtype == VS_BF16, "vs_vit_layer: bad dtype");
+  VS_REQUIRE(L->dtype == VS_F32 || L->dtype == VS_BF16 || L->dtype == VS_FP8, "vs_vit_layer: bad dtype");
+  VS_REQUIRE(L->dtype != VS_FP8 || (L->hidden % 128 == 0 && L->mlp % 128 == 0 && L->fp8_ws &&
+                                    (size_t)L->fp8_ws_bytes >= vs_vit_fp8_workspace_bytes(L->batch * L->tokens,
+                                                                                           L->hidden, L->mlp)),
+             "vs_vit_layer: VS_FP8 needs hidden % 128 == 0, mlp % 128 == 0 and the fp8 workspace");
   VS_REQUIRE(L->hidden == L->heads * 64, "vs_vit_layer: hidden must be heads*64");
   VS_REQUIRE(L->batch > 0 && L->tokens > 0 && L->mlp > 0, "vs_vit_layer: empty");
   VS_REQUIRE(!mlp_fused(L) || (L->dtype == VS_BF16 && vs_mlp_fused_ok(L->batch * L->tokens, L->hidden, L->mlp) &&
@@ -83,16 +116,23 @@ static int check_layer(const vs_vit_layer* L) {
 
 using namespace vs;
 
+extern "C" size_t vs_vit_fp8_workspace_bytes(int64_t M, int64_t D, int64_t F) {
+  const int64_t KM = D > F ? D : F, WM = 3 * D * D > F * D ? 3 * D * D : F * D;
+  return a256((size_t)(M * KM)) + a256((size_t)(M * KM / 32)) + a256((size_t)WM) + a256((size_t)(WM / 32));
+}
+
 extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   VS_CALL(check_layer(L));
-  const int T = L->dtype;
+  const bool f8 = L->dtype == VS_FP8;  // bf16 block, MX-FP8 forward products
+  const int T = f8 ? VS_BF16 : L->dtype;
+  auto product = [&](const vs_gemm_desc& g) { return f8 ? fp8_product(L, g, stream) : vs_gemm(&g, stream); };
   const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
   VS_CALL(vs_layernorm_fwd(T, M, D, L->x_in, D, L->ln1_g, L->ln1_b, L->ln_eps, L->h1, D, L->mean1, L->rstd1, stream));
   {
     vs_gemm_desc g = gdesc(T, T, true, true, M, 3 * D, D, L->h1, D, L->w_qkv, D, L->qkv, 3 * D, VS_EPI_BIAS);
     TimerTag tag(VS_TIMER_FWD_QKV);
     g.bias = L->b_qkv;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(product(g));
   }
   VS_CALL(vs_attn_fwd(T, L->batch, L->tokens, L->heads, 64, L->qkv, 3 * D, L->attn_o, D, L->lse, L->attn_scale, stream));
   {
@@ -102,13 +142,15 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     TimerTag tag(VS_TIMER_FWD_PROJ);
     g.residual = L->x_in;
     g.ld_residual = D;
-    if (T == VS_BF16) {  // y and LN2(y) in one launch (the row-slab kernel owns whole rows of y)
+    if (f8) {
+      VS_CALL(product(g));
+    } else if (T == VS_BF16) {  // y and LN2(y) in one launch (the row-slab kernel owns whole rows of y)
       VS_CALL(vs_gemm_ln_fwd(&g, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
     } else {
       VS_CALL(vs_gemm(&g, stream));
     }
   }
-  if (T != VS_BF16)
+  if (T != VS_BF16 || f8)
     VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
   if (mlp_fused(L)) {  // the whole MLP in one launch; nothing of the [M, F] intermediate is stored
     TimerTag tag(VS_TIMER_FWD_MLP);
@@ -123,7 +165,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     g.bias = L->b_fc1;
     g.aux_out = L->a_pre;
     g.ld_aux_out = F;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(product(g));
   }
   {
     vs_gemm_desc g = gdesc(T, VS_F32, true, true, M, D, F, L->a_act, F, L->w_fc2, F, L->x_out, D,
@@ -132,7 +174,7 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     TimerTag tag(VS_TIMER_FWD_FC2);
     g.residual = L->y;
     g.ld_residual = D;
-    VS_CALL(vs_gemm(&g, stream));
+    VS_CALL(product(g));
   }
   return VS_OK;
 }
@@ -141,7 +183,7 @@ extern "C" int vs_vit_layer_bwd(const vs_vit_layer* L, const vs_vit_layer_grad* 
   VS_CALL(check_layer(L));
   VS_REQUIRE(G && G->dx_out && G->dx_in && G->d_a && G->d_h && G->dy && G->d_o && G->d_qkv && G->attn_ws,
              "vs_vit_layer_bwd: null gradient buffer");
-  const int T = L->dtype;
+  const int T = L->dtype == VS_FP8 ? VS_BF16 : L->dtype;  // the fp8 block's backward runs in bf16
   const bool lp = T == VS_BF16;
   VS_REQUIRE(!lp || (G->dx_out_lp && G->dy_lp), "vs_vit_layer_bwd: bf16 mode needs dx_out_lp and dy_lp");
   const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;

@@ -13,7 +13,7 @@ import torch
 
 from .build import LIB_PATH
 
-VS_F32, VS_BF16, VS_U8 = 0, 1, 2
+VS_F32, VS_BF16, VS_U8, VS_FP8 = 0, 1, 2, 3
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESIDUAL, EPI_POS = 0x1, 0x2, 0x4, 0x8, 0x10
 EPI_GELU_BWD, EPI_RELU_BWD, EPI_ATOMIC, EPI_ACCUM = 0x20, 0x40, 0x80, 0x100
 EPI_GELU_GRAD, EPI_MUL_AUX = 0x200, 0x400
@@ -31,7 +31,7 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
 # vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
               "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
-              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd")
+              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8")
 PATH_COUNT = 24
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
@@ -65,7 +65,7 @@ class VitLayer(ctypes.Structure):
                 ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
                 ("x_in", c_p), ("h1", c_p), ("mean1", c_p), ("rstd1", c_p), ("qkv", c_p), ("attn_o", c_p),
                 ("lse", c_p), ("y", c_p), ("h2", c_p), ("mean2", c_p), ("rstd2", c_p), ("a_pre", c_p),
-                ("a_act", c_p), ("x_out", c_p)]
+                ("a_act", c_p), ("x_out", c_p), ("fp8_ws", c_p), ("fp8_ws_bytes", c_i64)]
 
 
 class VitLayerGrad(ctypes.Structure):
@@ -112,6 +112,8 @@ PROTOTYPES = {
     "vs_gemm_ln_bwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
                                       c_p, c_p, c_p, c_p, c_p]),
     "vs_mlp_fused_ok": (ctypes.c_int, [c_i64, c_i64, c_i64]),
+    "vs_quant_mxfp8": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]),
+    "vs_gemm_mxfp8": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_i64, c_p]),
     "vs_mlp_fwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p]),
     "vs_mlp_bwd_da": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p,
                                      c_i64, c_p]),
@@ -140,6 +142,7 @@ PROTOTYPES = {
     "vs_shard_close": (None, [ctypes.c_void_p]),
     "vs_shard_last_error": (ctypes.c_char_p, []),
     "vs_vit_layer_fwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), c_p]),
+    "vs_vit_fp8_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
     "vs_bwd_chain_create": (ctypes.c_int, [ctypes.POINTER(c_p)]),
     "vs_bwd_chain_destroy": (ctypes.c_int, [c_p]),

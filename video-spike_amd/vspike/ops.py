@@ -52,6 +52,36 @@ def linear(x, w, out, *, bias=None, epilogue=0, **kw):
                 ldc=out.stride(0), epilogue=epilogue, bias=bias, **kw)
 
 
+def quant_mxfp8(x, q, scales):
+    """MX-FP8 quantisation (vs_quant_mxfp8): x [M, K] f32/bf16 -> q [M, K] uint8 (OCP e4m3 codes) and
+    scales [M, K // 32] uint8 (E8M0 exponents, 2^(e - 127) per 32 consecutive elements of a row)."""
+    require_device(x, q, scales)
+    M, K = x.shape
+    check(lib().vs_quant_mxfp8(L.dtype_code(x.dtype), M, K, x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0),
+                               scales.data_ptr(), scales.stride(0), stream()), "vs_quant_mxfp8")
+    return q, scales
+
+
+def gemm_mxfp8(a_q, a_s, b_q, b_s, c, *, epilogue=0, bias=None, residual=None, aux_out=None, alpha=1.0):
+    """c = epilogue(A B^T) on the block-scaled fp8 MFMA (vs_gemm_mxfp8): a_q [M, K], b_q [N, K] uint8
+    e4m3 codes with their E8M0 scales (quant_mxfp8 layout); c [M, N] f32 or bf16."""
+    require_device(a_q, b_q, c)
+    M, K = a_q.shape
+    N = b_q.shape[0]
+    d = L.GemmDesc()
+    d.dtype, d.out_dtype = L.VS_FP8, L.dtype_code(c.dtype)
+    d.a_kcontig = d.b_kcontig = 1
+    d.M, d.N, d.K = M, N, K
+    d.a, d.lda, d.b, d.ldb, d.c, d.ldc = a_q.data_ptr(), a_q.stride(0), b_q.data_ptr(), b_q.stride(0), c.data_ptr(), c.stride(0)
+    d.epilogue, d.alpha = epilogue, alpha
+    d.bias = ptr(bias)
+    d.residual, d.ld_residual = ptr(residual), (residual.stride(0) if residual is not None else 0)
+    d.aux_out, d.ld_aux_out = ptr(aux_out), (aux_out.stride(0) if aux_out is not None else 0)
+    check(lib().vs_gemm_mxfp8(ctypes.byref(d), a_s.data_ptr(), a_s.stride(0), b_s.data_ptr(), b_s.stride(0), stream()),
+          "vs_gemm_mxfp8")
+    return c
+
+
 def mlp_fused_ok(M: int, D: int, F: int) -> bool:
     """vs_mlp_fused_ok: the fused MLP kernels take this shape (bf16, D = 192, F % 64 == 0)."""
     return bool(lib().vs_mlp_fused_ok(int(M), int(D), int(F)))

@@ -51,7 +51,9 @@ _LN_FUSE_ROWS = 65536
 _MLP_FUSE = os.environ.get("VSPIKE_MLP_FUSE", "1") != "0"
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
-           "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+           "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+           # BASELINE C5: the bf16 block with its four Linear forwards on MX-FP8 (vs_gemm_mxfp8)
+           "fp8": torch.bfloat16, "mxfp8": torch.bfloat16}
 
 
 class _FwdState(dict):
@@ -79,7 +81,9 @@ class VideoMAE(nn.Module):
         super().__init__()
         self.backbone = BackboneCfg.from_config(_cfg_get(config, "backbone"))
         self.freeze_encoder = bool(_cfg_get(config, "freeze_encoder", True))
-        self.compute_dtype = _DTYPES[str(_cfg_get(config, "compute_dtype", "fp32")).lower()]
+        cdt = str(_cfg_get(config, "compute_dtype", "fp32")).lower()
+        self.compute_dtype = _DTYPES[cdt]
+        self.fp8 = cdt in ("fp8", "mxfp8")
         enc_out = int(config["encoder"]["output_dim"])
         out_dim = int(config["decoder"]["output_dim"])
         if out_dim % 100:
@@ -87,6 +91,9 @@ class VideoMAE(nn.Module):
         cfg = self.backbone
         if cfg.hidden_size != 64 * cfg.num_attention_heads:
             raise ValueError("this build supports head dim 64 (hidden_size = 64 * num_attention_heads)")
+        if self.fp8 and (cfg.hidden_size % 128 or cfg.intermediate_size % 128):
+            raise ValueError("compute_dtype fp8 (MX-FP8 block products) needs hidden_size and intermediate_size "
+                             "multiples of 128 (e.g. videomae-base)")
         self.layout = VitLayout(cfg, enc_out, out_dim)
         self.enc_flat = nn.Parameter(torch.zeros(self.layout.enc.numel), requires_grad=not self.freeze_encoder)
         self.head_flat = nn.Parameter(torch.zeros(self.layout.head.numel))
@@ -218,7 +225,7 @@ class VideoMAE(nn.Module):
 
     def _mlp_fused(self, B: int) -> bool:
         cfg = self.backbone
-        return (_MLP_FUSE and self.compute_dtype == torch.bfloat16 and
+        return (_MLP_FUSE and self.compute_dtype == torch.bfloat16 and not self.fp8 and
                 ops.mlp_fused_ok(B * cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size))
 
     # activation buffers of one block (names match VitLayer fields)
@@ -237,7 +244,7 @@ class VideoMAE(nn.Module):
         cfg = self.backbone
         lay = self.layout.enc
         s = L.VitLayer()
-        s.dtype = L.dtype_code(self.compute_dtype)
+        s.dtype = L.VS_FP8 if self.fp8 else L.dtype_code(self.compute_dtype)
         s.heads = cfg.num_attention_heads
         s.batch, s.tokens, s.hidden, s.mlp = B, cfg.num_tokens, cfg.hidden_size, cfg.intermediate_size
         s.ln_eps = cfg.layer_norm_eps
@@ -253,6 +260,8 @@ class VideoMAE(nn.Module):
             s.a_pre, s.a_act = None, act["mlp_a"].data_ptr()
         else:
             s.a_pre, s.a_act = act[pfx + "a_pre"].data_ptr(), act[pfx + "a_act"].data_ptr()
+        if self.fp8:
+            s.fp8_ws, s.fp8_ws_bytes = act["fp8_ws"].data_ptr(), act["fp8_ws"].numel()
         return s
 
     def set_side_stream(self, enabled: bool) -> None:
@@ -336,6 +345,8 @@ class VideoMAE(nn.Module):
             self._plan_layer(ar, f"L{j}.", B)
         if self._mlp_fused(B):   # gelu(pre) of the layer being back-propagated (written by its backward)
             ar.add("mlp_a", (M, cfg.intermediate_size), dt)
+        if self.fp8:             # MX-FP8 operands + scales of the product being run (shared by the layers)
+            ar.add("fp8_ws", (int(L.lib().vs_vit_fp8_workspace_bytes(M, D, cfg.intermediate_size)),), torch.uint8)
         for j in range(Lyr if save_encoder else 2):
             ar.add(f"X{j}", (M, D), torch.float32)
         if lp:
