@@ -47,6 +47,7 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_FP8_TFLOPS = 5000.0    # MI355X dense fp8 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0       # HBM3E spec (MI355X_MICROARCH.md); 6.3 TB/s is the measured copy rate
 # timer classes whose launches map one-to-one onto kernels that the committed PMC traffic summary
 # (scripts/traffic_summary.py) groups; the per-product GEMM timers share kernel templates
@@ -69,7 +70,10 @@ def parse():
                     help="clips per GPU (default: the train config's train_batch_size, 128 = the reference's)")
     ap.add_argument("--neurons", type=int, default=128)
     ap.add_argument("--model", default="vmae_tiny", help="config/model/<name>.yaml")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: BASELINE C5's precision — the ViT block's four Linear forwards on MX-FP8 "
+                         "(vs_gemm_mxfp8), the rest bf16")
+    ap.add_argument("--frames", type=int, default=None, help="clip length (16 = C2/C3; 32 = C5's encoder)")
     ap.add_argument("--freeze", action="store_true", help="reference default: encoder frozen (head-only training)")
     ap.add_argument("--lr", type=float, default=None,
                     help="override the config's max lr (throughput-neutral).  The synthetic C3 setup (random-init "
@@ -179,7 +183,9 @@ def _reference_grads(model):
 # (r03 on MI355X at 128 clips: log-rates 3.4e-3, loss 1.8e-5, worst gradient 4.6e-3); a failed check
 # makes bench.py exit non-zero after printing its line
 PARITY_TOL = {"fp32": {"log_rates": 1e-4, "loss": 1e-5, "grad": 1e-3},
-              "bf16": {"log_rates": 7e-3, "loss": 1e-4, "grad": 1e-2}}
+              "bf16": {"log_rates": 7e-3, "loss": 1e-4, "grad": 1e-2},
+              # MX-FP8 forward products (3 mantissa bits): the bars of tests/test_gpu_c5.py
+              "fp8": {"log_rates": 6e-2, "loss": 1e-2, "grad": 1.5e-1}}
 
 
 def full_batch_parity(ccfg, params, pixels, target, gpu, args):
@@ -318,6 +324,10 @@ def main():
                              os.path.join(cfg_dir, "train", "vmae_video.yaml"))
     config["model"]["decoder"]["output_dim"] = 100 * args.neurons       # src/train.py:41
     config["model"]["compute_dtype"] = args.dtype
+    if args.frames:
+        bbk = dict(config["model"].get("backbone") or {})
+        bbk["num_frames"] = args.frames
+        config["model"]["backbone"] = bbk
     config["model"]["freeze_encoder"] = bool(args.freeze)
     if args.lr is not None:
         config["optimizer"]["lr"] = args.lr
@@ -414,8 +424,9 @@ def main():
     clips = world * B * args.steps
     value = clips / elapsed
     N, H, Lyr = bb.num_tokens, bb.num_attention_heads, bb.num_hidden_layers
+    D0, F0 = bb.hidden_size, bb.intermediate_size
     fwd_flop = 4.0 * B * H * N * N * 64                 # QK^T + PV per launch (one layer)
-    peak_mfma = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+    peak_mfma = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS   # fp8: attention + backward are bf16
     roof_all = {}
     for name, (n, ms, nbytes) in kern.items():
         if not n:
@@ -431,6 +442,17 @@ def main():
             ach = nbytes / (ms / 1e3) / 1e9                                 # bytes-weighted over launches
             ent = {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                    "frac": round(ach / PEAK_HBM_GBS, 4), "work_per_launch": round(nbytes / n, 0)}
+            prod = {"fwd_qkv": 3 * D0 * D0, "fwd_proj": D0 * D0, "fwd_fc1": F0 * D0, "fwd_fc2": D0 * F0,
+                    "dx_qkv": 3 * D0 * D0, "dx_proj": D0 * D0, "dx_fc1": F0 * D0, "dx_fc2": D0 * F0,
+                    "dw_qkv": 3 * D0 * D0, "dw_proj": D0 * D0, "dw_fc1": F0 * D0, "dw_fc2": D0 * F0}.get(name)
+            if prod is not None:
+                # the product's MFMA side (2 M N K flop per launch) against the peak of its dtype (the fp8
+                # forward products: the 5 PF MX-FP8 peak)
+                fl = 2.0 * B * N * prod
+                pk = PEAK_FP8_TFLOPS if (args.dtype == "fp8" and name.startswith("fwd_")) else peak_mfma
+                tf = fl / avg_s / 1e12
+                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2), "mfma_peak": pk,
+                            "mfma_frac": round(tf / pk, 4)})
             if name in ("fwd_mlp", "dx_mlp"):
                 # the fused MLP kernels sit near the ridge (~300 flop/B): their MFMA side as well
                 # (fwd: h2 W1^T and a W2^T; dx: h2 W1^T recomputed and dy W2 = 4 M D F flop per launch)
@@ -469,10 +491,12 @@ def main():
         parity = full_batch_parity(ccfg, init_params, pixels.cpu(), target.cpu(), gpu_par, args)
 
     if rank == 0:
-        workload = ("C3 ViT-Base/16" if bb.hidden_size == 768 else "C2 ViT-Tiny/16" if bb.hidden_size == 192
+        workload = ("C5 ViT-Base/16 encoder (no temporal transformer: no reference code)"
+                    if bb.hidden_size == 768 and bb.num_frames == 32 else
+                    "C3 ViT-Base/16" if bb.hidden_size == 768 else "C2 ViT-Tiny/16" if bb.hidden_size == 192
                     else f"ViT d{bb.hidden_size}")
         line = {
-            "metric": "clips/sec (16-frame 224x224) train step", "value": round(value, 3), "unit": "clips/sec",
+            "metric": f"clips/sec ({bb.num_frames}-frame {bb.image_size}x{bb.image_size}) train step", "value": round(value, 3), "unit": "clips/sec",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (randn pixels, Poisson targets), random-init",

@@ -1,0 +1,97 @@
+"""BASELINE C5 at its stated precision: ViT-Base width at 32 frames (3,136 tokens), n = 1,024, with the
+block's four Linear forwards on MX-FP8 (compute_dtype "fp8": vs_gemm_mxfp8 via the block executor;
+everything else bf16, the backward bf16), against the reference's own encoder + head (fixture
+vit_base32f from the HF VideoMAEModel the reference plugin executes: oracle/gen_fixtures.py).
+
+The bars are the fp8 format's, documented here: e4m3 keeps 3 mantissa bits (2^-4 relative per
+element, 16x bf16's), so the block outputs carry ~1-2 % relative noise; log-rates FP8_OUT of
+max |ref|, loss FP8_LOSS relative, gradients FP8_GRAD norm-relative (the bf16 backward runs on the
+fp8 forward's activations).  Measured values are printed with -s.
+
+C5's temporal transformer has no reference code: nothing to pin it against,
+so it is not built.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, prng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+FP8_OUT = 6e-2
+FP8_LOSS = 1e-2
+FP8_GRAD = 1.5e-1
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _model(cfg, n, dtype):
+    from vspike import VideoMAE
+    conf = {"model_class": "VideoMAE", "freeze_encoder": False, "compute_dtype": dtype,
+            "backbone": {k: getattr(cfg, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                       "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                       "num_attention_heads", "intermediate_size",
+                                                       "layer_norm_eps")},
+            "encoder": {"output_dim": 64}, "decoder": {"output_dim": 100 * n}}
+    m = VideoMAE(conf).to(DEV)
+    m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_vit_params(cfg, 64, n).items()})
+    return m
+
+
+def test_c5_fp8_encoder_geometry_forward_backward(golden):
+    from vspike import poisson_nll_mean, _lib as L
+    from vspike.layout import modern_name
+    fx = golden("vit_base32f.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_frames=32, num_hidden_layers=1), 1, 1024
+    m = _model(cfg, n, "fp8")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=32)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(32, (B, 100, n))).to(DEV)
+    L.dispatch_reset()
+    out = m(px)
+    loss = poisson_nll_mean(out, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    counts = L.dispatch_counts()
+    assert counts["gemm_fp8"] == 4 * cfg.num_hidden_layers, counts      # qkv, proj, fc1, fc2 on MX-FP8
+    out_err = float(np.abs(out.detach().cpu().numpy() - fx["log_rates"]).max() / np.abs(fx["log_rates"]).max())
+    loss_err = abs(loss.item() - fx["loss"][0]) / abs(fx["loss"][0])
+    shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+    errs = {}
+    for name, which, slot, rows in m.layout.hf_items():
+        flat = m.enc_flat.grad if which == "enc" else m.head_flat.grad
+        t = (m.layout.enc if which == "enc" else m.layout.head).view(flat, slot)
+        k = modern_name(name)
+        g = (t if rows is None else t[rows]).detach().cpu().numpy().reshape(shapes[k])
+        errs[k] = cpu_ref.summary_rel_error(k, g, fx)
+    worst = max(errs, key=errs.get)
+    print(f"\n[C5 fp8] log-rate err {out_err:.3e}  loss err {loss_err:.3e}  worst grad {worst} {errs[worst]:.3e}")
+    assert out_err < FP8_OUT and loss_err < FP8_LOSS
+    bad = {k: v for k, v in errs.items() if v > FP8_GRAD}
+    assert not bad, bad
+
+
+def test_c5_fp8_is_closer_to_the_reference_than_a_wrong_model(golden):
+    """Guard against a bar that passes anything: the fp8 log-rates must be far closer to the
+    reference than the log-rates of the same model with one layer's weights perturbed by 10 %."""
+    from vspike import poisson_nll_mean  # noqa: F401
+    fx = golden("vit_base32f.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_frames=32, num_hidden_layers=1), 1, 1024
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=32)).to(DEV)
+    ref = fx["log_rates"]
+    m = _model(cfg, n, "fp8")
+    with torch.no_grad():
+        good = m(px).cpu().numpy()
+        w = m.layout.enc.view(m.enc_flat, "0.w_fc1")
+        w.mul_(1.1)
+        m.invalidate_lp()
+        bad = m(px).cpu().numpy()
+    e_good = np.abs(good - ref).max() / np.abs(ref).max()
+    e_bad = np.abs(bad - ref).max() / np.abs(ref).max()
+    print(f"\n[C5 fp8] err {e_good:.3e} vs perturbed model {e_bad:.3e}")
+    assert e_good < 0.5 * e_bad
