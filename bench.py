@@ -103,38 +103,65 @@ def _cpu_model_name():
     return "unknown"
 
 
+def _cpu_share():
+    """CPUs this process may actually use: the scheduler affinity, capped by a cgroup v2 cpu.max quota
+    (the GPU box gives a job a 16-CPU share of a 256-CPU host: os.cpu_count() counts the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(cfg, params, pixels, target, seconds):
     """BASELINE.md CPU plan (BASELINE.md:37): the oracle (torch-CPU fp32 restatement of the step) per
-    clip, fwd and fwd+bwd at B=1 and B=4, on `os.cpu_count()` threads, median of >= 5 runs after two
-    warm-ups per cell (the first call of a shape pays one-off costs: allocator growth, first-touch page
-    faults, oneDNN primitive creation; round 3's single warm-up left B=1 slower per clip than B=4).
-    The box's OMP_NUM_THREADS share (16) is timed the same way and reported beside it; `value` is
-    the B=4 fwd+bwd rate on the thread count that ran it faster.  Each cell reports its median, min
-    and max (the spread) and the cells are checked for monotonicity (fwd+bwd slower than fwd, B=4
-    no slower per clip than B=1 by more than the spread)."""
+    clip, fwd and fwd+bwd at B=1 and B=4, median of >= 5 runs after two warm-ups per cell (the first
+    call of a shape pays one-off costs: allocator growth, first-touch page faults, oneDNN primitive
+    creation; round 3's single warm-up left B=1 slower per clip than B=4).  Thread counts: the CPU
+    share this process has (affinity / cgroup quota; OMP_NUM_THREADS on the box) and os.cpu_count()
+    as BASELINE.md asks; the latter is skipped when one B=1 forward at that count takes more than
+    4x the share's (oversubscription: the box's 256-CPU count vs its 16-CPU quota), and recorded so.
+    `value` is the B=4 fwd+bwd rate of the faster count; every cell reports median, min and max
+    and the cells are checked for monotonicity."""
     from oracle import cpu_ref
-    counts = []
-    for t in (os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)):
-        if t > 0 and t not in counts:
-            counts.append(t)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or _cpu_share()
+    counts = [share] + ([os.cpu_count()] if (os.cpu_count() or 0) != share else [])
     P = cpu_ref.to_torch(params)
     t_start = time.perf_counter()
-    per_count, loss4 = {}, None
+    per_count, loss4, skipped = {}, None, {}
     for threads in counts:
         torch.set_num_threads(threads)
         res = {}
-        for B in (1, 4):
+
+        def cell(B, mode):
             px, y = pixels[:B], target[:B]
+
+            def run():
+                if mode == "fwd":
+                    with torch.no_grad():
+                        return cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
+                loss.backward()
+                for p in P.values():
+                    p.grad = None
+                return loss.detach()
+            return run
+        if threads != share:   # probe: one B=1 forward against the share's median
+            t0 = time.perf_counter()
+            cell(1, "fwd")()
+            probe = time.perf_counter() - t0
+            _progress(f"cpu baseline, {threads} threads: probe B=1 fwd {probe:.2f} s")
+            if probe > 4 * per_count[str(share)]["B1_fwd"]["max"] or time.perf_counter() - t_start > seconds:
+                skipped[str(threads)] = (f"one B=1 forward took {probe:.2f} s against "
+                                         f"{per_count[str(share)]['B1_fwd']['s_per_clip']:.2f} s on {share} threads "
+                                         "(oversubscribed: the process's CPU quota is smaller than the host's count)")
+                continue
+        for B in (1, 4):
             for mode in ("fwd", "fwd_bwd"):
-                def run():
-                    if mode == "fwd":
-                        with torch.no_grad():
-                            return cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
-                    loss = cpu_ref.poisson_nll_mean(cpu_ref.videomae_plugin_forward(px, P, cfg, False), y)
-                    loss.backward()
-                    for p in P.values():
-                        p.grad = None
-                    return loss.detach()
+                run = cell(B, mode)
                 for _ in range(2):                                   # warm-ups
                     loss = run()
                 if B == 4 and mode == "fwd":
@@ -151,18 +178,15 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
         res["monotone"] = bool(c("B1_fwd_bwd") > c("B1_fwd") and c("B4_fwd_bwd") > c("B4_fwd") and
                                c("B4_fwd") <= res["B1_fwd"]["max"] and c("B4_fwd_bwd") <= res["B1_fwd_bwd"]["max"])
         per_count[str(threads)] = res
-        if time.perf_counter() - t_start > seconds:
-            break                                   # bounded: the first count (os.cpu_count()) always runs
     elapsed = time.perf_counter() - t_start
     best = min(per_count, key=lambda k: per_count[k]["B4_fwd_bwd"]["s_per_clip"])
     value = 1.0 / per_count[best]["B4_fwd_bwd"]["s_per_clip"]
     out = {"value": round(value, 4), "unit": "clips/sec", "cores": int(best), "kind": "port",
            "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of 5 after 2 warm-ups, "
-                     f"{best} threads (also timed: {', '.join(k for k in per_count if k != best) or 'none'}); "
-                     f"{elapsed:.1f} s of CPU work in all",
-           "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(),
+                     f"{best} threads; {elapsed:.1f} s of CPU work in all",
+           "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(), "cpu_share": _cpu_share(),
                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
-           "detail": per_count}
+           "detail": per_count, "skipped": skipped}
     return out, loss4
 
 

@@ -60,7 +60,16 @@ def test_quant_mxfp8_matches_recipe(dtype, M, K):
     torch.cuda.synchronize()
     qr, sr = mx_ref(x)
     assert torch.equal(s, sr)
-    assert torch.equal(q, qr), int((q != qr).sum())
+    bad = (q != qr).nonzero()
+    if len(bad):
+        scaled = (x.float().view(M, K // 32, 32) * torch.ldexp(torch.ones(M, K // 32, device=DEV),
+                                                               127 - s.int())[..., None]).view(M, K)
+        for r, c in bad[:12].tolist():
+            print(f"  mismatch ({r},{c}): x*2^-e = {scaled[r, c].item()!r} ours {q[r, c].item():#04x} "
+                  f"({q[r, c:c + 1].view(torch.float8_e4m3fn).float().item()!r}) torch {qr[r, c].item():#04x} "
+                  f"({qr[r, c:c + 1].view(torch.float8_e4m3fn).float().item()!r})")
+    print(f"\n[quant {M}x{K} {dtype}] code mismatches vs torch.float8_e4m3fn: {len(bad)} of {M * K}")
+    assert torch.equal(q, qr), len(bad)
     # the format's own error bound: |deq - x| <= 2^-4 |x| (+ the smallest subnormal step of the block)
     d = dequant(q, s)
     xd = x.double()

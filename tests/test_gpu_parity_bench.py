@@ -130,10 +130,10 @@ def test_vit_tiny12_bench_geometry_loss_curve(golden, dtype):
 
 
 # kernel paths the benched bf16 step takes at M = B * 1568 = 25,088 token rows (vspike.h VS_PATH_*):
-# W-resident qkv / fc1, proj + LayerNorm2 fused, row-slab N <= 192 products (fc2, dX, patch
-# embedding), the wide row-slab GELU' product, the dW tiles, the skinny head, flash attention
-BENCH_PATHS_BF16 = ("gemm_wres", "gemm_ln_fwd", "gemm_slab", "gemm_wslab", "gemm_dw", "gemm_skinny", "attn_fwd",
-                    "attn_bwd")
+# W-resident qkv, proj + LayerNorm2 fused, row-slab N <= 192 products (dX, patch embedding), the
+# fused MLP forward and its recomputing GELU' backward, the dW tiles, the skinny head, flash attention
+BENCH_PATHS_BF16 = ("gemm_wres", "gemm_ln_fwd", "gemm_slab", "mlp_fwd", "mlp_bwd", "gemm_dw", "gemm_skinny",
+                    "attn_fwd", "attn_bwd")
 
 
 @contextlib.contextmanager
