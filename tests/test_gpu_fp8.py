@@ -33,15 +33,20 @@ def mx_ref(x):
     e = e + ((bits & 0x7FFFFF) != 0).int()
     e = torch.where(((bits >> 23) & 0xFF) == 0, torch.full_like(e, -126), e).clamp(-126, 127)
     e = torch.where(amax > 0, e, torch.zeros_like(e))
-    inv = torch.ldexp(torch.ones_like(amax), -e)
+    inv = ((127 - e) << 23).view(torch.float32)       # 2^-e exactly (torch.ldexp is not exact)
     q = (xb * inv[..., None]).to(torch.float8_e4m3fn).view(torch.uint8).view(M, K)
     return q, (e + 127).to(torch.uint8)
+
+
+def _pow2(e):
+    """2^e exactly (f64), e an integer tensor in [-126, 127]."""
+    return ((e.long() + 1023) << 52).view(torch.float64)
 
 
 def dequant(q, s):
     M, K = q.shape
     v = q.view(torch.float8_e4m3fn).double().view(M, K // 32, 32)
-    return (v * torch.ldexp(torch.ones_like(s, dtype=torch.float64), s.long() - 127)[..., None]).view(M, K)
+    return (v * _pow2(s.long() - 127)[..., None]).view(M, K)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -62,8 +67,7 @@ def test_quant_mxfp8_matches_recipe(dtype, M, K):
     assert torch.equal(s, sr)
     bad = (q != qr).nonzero()
     if len(bad):
-        scaled = (x.float().view(M, K // 32, 32) * torch.ldexp(torch.ones(M, K // 32, device=DEV),
-                                                               127 - s.int())[..., None]).view(M, K)
+        scaled = (x.double().view(M, K // 32, 32) * _pow2(127 - s.long())[..., None]).view(M, K)
         for r, c in bad[:12].tolist():
             print(f"  mismatch ({r},{c}): x*2^-e = {scaled[r, c].item()!r} ours {q[r, c].item():#04x} "
                   f"({q[r, c:c + 1].view(torch.float8_e4m3fn).float().item()!r}) torch {qr[r, c].item():#04x} "
@@ -73,8 +77,57 @@ def test_quant_mxfp8_matches_recipe(dtype, M, K):
     # the format's own error bound: |deq - x| <= 2^-4 |x| (+ the smallest subnormal step of the block)
     d = dequant(q, s)
     xd = x.double()
-    step = torch.ldexp(torch.ones_like(s, dtype=torch.float64), s.long() - 127 - 9).repeat_interleave(32, 1)
+    step = _pow2(s.long() - 127 - 9).repeat_interleave(32, 1)
     assert bool(((d - xd).abs() <= xd.abs() * 2.0 ** -4 + step).all())
+
+
+def test_gemm_mxfp8_operand_and_scale_map():
+    """Structured inputs that expose the 32x32x64 f8 MFMA's operand / scale map: (a) random e4m3
+    codes with unit scales (data pairing only); (b) all-ones data with a distinct scale per
+    (row, k-block) (which scale meets which k-block)."""
+    from vspike import ops
+    g = torch.Generator(device=DEV).manual_seed(7)
+    M, N, K = 64, 128, 256
+    # (a) codes of values in [-4, 4] (exact in e4m3), unit scales
+    av = (torch.randint(-8, 9, (M, K), device=DEV, generator=g).float() / 2).to(torch.float8_e4m3fn)
+    bv = (torch.randint(-8, 9, (N, K), device=DEV, generator=g).float() / 2).to(torch.float8_e4m3fn)
+    one_a = torch.full((M, K // 32), 127, dtype=torch.uint8, device=DEV)
+    one_b = torch.full((N, K // 32), 127, dtype=torch.uint8, device=DEV)
+    c = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(av.view(torch.uint8), one_a, bv.view(torch.uint8), one_b, c)
+    torch.cuda.synchronize()
+    ref = av.double() @ bv.double().t()
+    ea = float((c.double() - ref).abs().max())
+    print(f"\n[mxfp8 map] (a) unit scales: max abs err {ea}")
+    # (b) all ones, scale of A (row m, block kb) = 2^(kb % 4) * 2^(4 (m % 2)) ... distinct per block
+    ones = torch.ones(M, K, device=DEV).to(torch.float8_e4m3fn).view(torch.uint8)
+    onesb = torch.ones(N, K, device=DEV).to(torch.float8_e4m3fn).view(torch.uint8)
+    kb = torch.arange(K // 32, device=DEV)
+    sa = (127 + kb[None, :] + 8 * (torch.arange(M, device=DEV)[:, None] % 2)).to(torch.uint8)
+    c2 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(ones, sa, onesb, one_b, c2)
+    torch.cuda.synchronize()
+    want = 32.0 * _pow2(sa.long() - 127).sum(1)
+    print(f"[mxfp8 map] (b) A-scale per block: got rows 0,1 = {c2[0, 0].item()}, {c2[1, 0].item()}; "
+          f"want {want[0].item()}, {want[1].item()}")
+    # (c) B scales per block
+    sb = (127 + kb[None, :] + 8 * (torch.arange(N, device=DEV)[:, None] % 2)).to(torch.uint8)
+    c3 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(ones, one_a, onesb, sb, c3)
+    torch.cuda.synchronize()
+    wantb = 32.0 * _pow2(sb.long() - 127).sum(1)
+    print(f"[mxfp8 map] (c) B-scale per block: got cols 0,1 = {c3[0, 0].item()}, {c3[0, 1].item()}; "
+          f"want {wantb[0].item()}, {wantb[1].item()}")
+    # (d) one k-block of A nonzero at a time (unit scales): which k positions pair
+    for blk in range(K // 32):
+        a1 = torch.zeros(M, K, device=DEV)
+        a1[:, blk * 32:(blk + 1) * 32] = 1.0
+        c4 = torch.empty(M, N, device=DEV)
+        ops.gemm_mxfp8(a1.to(torch.float8_e4m3fn).view(torch.uint8), one_a, bv.view(torch.uint8), one_b, c4)
+        torch.cuda.synchronize()
+        r4 = a1.double() @ bv.double().t()
+        print(f"[mxfp8 map] (d) only k-block {blk}: max abs err {float((c4.double() - r4).abs().max())}")
+    assert ea == 0.0
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(6272, 2304, 768, "bias"), (3136, 768, 768, "bias_res"),
