@@ -127,6 +127,40 @@ def test_gemm_mxfp8_operand_and_scale_map():
         torch.cuda.synchronize()
         r4 = a1.double() @ bv.double().t()
         print(f"[mxfp8 map] (d) only k-block {blk}: max abs err {float((c4.double() - r4).abs().max())}")
+    # (e) subnormal e4m3 codes (exponent field 0), unit scales
+    sub = torch.randint(1, 8, (M, K), device=DEV, generator=g).to(torch.uint8) | \
+        (torch.randint(0, 2, (M, K), device=DEV, generator=g).to(torch.uint8) << 7)
+    c5 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(sub, one_a, bv.view(torch.uint8), one_b, c5)
+    torch.cuda.synchronize()
+    r5 = sub.view(torch.float8_e4m3fn).double() @ bv.double().t()
+    print(f"[mxfp8 map] (e) subnormal A codes: max abs err {float((c5.double() - r5).abs().max())} "
+          f"(ref max {float(r5.abs().max())})")
+    # (f) scales below 1 (E8M0 110..126), all-ones data
+    sa_lo = (110 + kb[None, :] + 8 * (torch.arange(M, device=DEV)[:, None] % 2)).to(torch.uint8)
+    c6 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(ones, sa_lo, onesb, one_b, c6)
+    torch.cuda.synchronize()
+    want6 = 32.0 * _pow2(sa_lo.long() - 127).sum(1)
+    print(f"[mxfp8 map] (f) scales < 1: got rows 0,1 = {c6[0, 0].item()}, {c6[1, 0].item()}; "
+          f"want {want6[0].item()}, {want6[1].item()}")
+    # (g) quantised random data, unit scales substituted (data path of real codes)
+    x = torch.randn(M, K, device=DEV, generator=g)
+    xq = torch.empty(M, K, dtype=torch.uint8, device=DEV)
+    xs = torch.empty(M, K // 32, dtype=torch.uint8, device=DEV)
+    ops.quant_mxfp8(x, xq, xs)
+    c7 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(xq, one_a, bv.view(torch.uint8), one_b, c7)
+    torch.cuda.synchronize()
+    r7 = xq.view(torch.float8_e4m3fn).double() @ bv.double().t()
+    print(f"[mxfp8 map] (g) real codes, unit scales: max abs err {float((c7.double() - r7).abs().max())} "
+          f"(ref max {float(r7.abs().max())}); codes {xq[0, :8].tolist()} scales {xs[0].tolist()}")
+    c8 = torch.empty(M, N, device=DEV)
+    ops.gemm_mxfp8(xq, xs, bv.view(torch.uint8), one_b, c8)
+    torch.cuda.synchronize()
+    r8 = dequant(xq, xs) @ bv.double().t()
+    print(f"[mxfp8 map] (h) real codes + scales: max abs err {float((c8.double() - r8).abs().max())} "
+          f"(ref max {float(r8.abs().max())}); c {c8[0, :4].tolist()} ref {r8[0, :4].tolist()}")
     assert ea == 0.0
 
 
