@@ -173,6 +173,12 @@ int vs_gemm_mxfp8(const vs_gemm_desc* d, const void* scale_a, int64_t ld_scale_a
 int vs_mlp_fused_ok(int64_t M, int64_t D, int64_t F);
 int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
                const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx, void* stream);
+/* vs_mlp_fwd plus the next block's LayerNorm1 on x_out in the epilogue (eps; h_out bf16 [M, D], row
+ * mean / rstd): mv:419-445's layernorm_before of block i+1 fused into block i's output (D = 192). */
+int vs_mlp_fwd_ln(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
+                  const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx,
+                  const float* ln_g, const float* ln_b, float eps, void* h_out, int64_t ld_h_out, float* mean_out,
+                  float* rstd_out, void* stream);
 int vs_mlp_bwd_da(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
                   const void* w2, const void* dy, int64_t lddy, void* da, int64_t ldda, void* a, int64_t lda,
                   void* stream);
@@ -322,6 +328,14 @@ typedef struct vs_vit_layer {
   /* ABI v6: dtype VS_FP8 (bf16 block with MX-FP8 forward products, BASELINE C5) needs this scratch,
      vs_vit_fp8_workspace_bytes(M, D, F) bytes, 256-B aligned; unused otherwise */
   void* fp8_ws; int64_t fp8_ws_bytes;
+  /* ABI v7: the NEXT block's LayerNorm1 produced by this block's fused MLP epilogue (optional; all
+     five set or all NULL): next_ln_g/b [D] f32 gamma/beta, next_h1 [M, D] bf16, next_mean1 /
+     next_rstd1 [M] f32 (the next block's h1 / mean1 / rstd1).  ln1_ready != 0: this block's h1 /
+     mean1 / rstd1 were written that way by the previous block, so its own LayerNorm1 launch is
+     skipped (the values are those of LN1(x_in) either way) */
+  const float* next_ln_g; const float* next_ln_b;
+  void* next_h1; float* next_mean1; float* next_rstd1;
+  int32_t ln1_ready; int32_t reserved7;
 } vs_vit_layer;
 size_t vs_vit_fp8_workspace_bytes(int64_t M, int64_t D, int64_t F);
 

@@ -113,3 +113,35 @@ def test_mlp_fused_ok_shapes():
     assert ops.mlp_fused_ok(200704, 192, 768)
     assert not ops.mlp_fused_ok(25088, 768, 3072)     # ViT-Base: the two-GEMM path
     assert not ops.mlp_fused_ok(100, 192, 100)
+
+
+@pytest.mark.parametrize("M", [200704, 12345, 100])
+def test_mlp_fwd_ln_next_layernorm(M):
+    """vs_mlp_fwd_ln: the fused MLP plus the NEXT block's LayerNorm1 on its output rows (eps 1e-12):
+    x' as vs_mlp_fwd writes it (bitwise), h within bf16 rounding of the fp64 LayerNorm of x', row
+    mean / rstd within 1e-5 relative."""
+    import ctypes
+    from vspike import ops, _lib as L
+    D, F = 192, 768
+    h2, w1, b1, w2, b2, y = _operands(M, D, F, seed=M + 3)
+    g = torch.Generator(device=DEV).manual_seed(M)
+    gam = torch.randn(D, device=DEV, generator=g) * 0.3 + 1
+    bet = torch.randn(D, device=DEV, generator=g) * 0.1
+    out, out_ref = torch.empty(M, D, device=DEV), torch.empty(M, D, device=DEV)
+    hn = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.mlp_fwd(h2, w1, b1, w2, b2, y, out_ref)
+    L.check(L.lib().vs_mlp_fwd_ln(M, D, F, h2.data_ptr(), D, w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                                  b2.data_ptr(), y.data_ptr(), D, out.data_ptr(), D, gam.data_ptr(), bet.data_ptr(),
+                                  ctypes.c_float(1e-12), hn.data_ptr(), D, mean.data_ptr(), rstd.data_ptr(),
+                                  L.stream()), "vs_mlp_fwd_ln")
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref)
+    x = out.double()
+    mu = x.mean(1)
+    var = ((x - mu[:, None]) ** 2).mean(1)
+    rs = 1.0 / torch.sqrt(var + 1e-12)
+    href = (x - mu[:, None]) * rs[:, None] * gam.double() + bet.double()
+    assert _maxrel(hn, href) < 8e-3
+    assert float(((mean.double() - mu).abs() / x.abs().max()).max()) < 1e-5
+    assert float(((rstd.double() - rs).abs() / rs).max()) < 1e-5

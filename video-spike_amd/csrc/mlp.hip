@@ -40,6 +40,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base, int
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(n * ld * es), 0x00020000);
 }
 
+// sum over lanes l and l ^ 32 (the two halves of a token's row) without LDS
+__device__ __forceinline__ float pair_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ u32x4v mlp_pack8(const float* v) {
   u32x4v u;
 #pragma unroll
@@ -119,7 +125,20 @@ __device__ __forceinline__ void mlp_stage1(const char* st, int lane, const u32x4
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-template <int D>
+// The next block's LayerNorm1 on the rows this epilogue owns (LNF): h = LN(x'; g, b, eps) in bf16
+// with its row mean / rstd (two-pass variance, as ln_fwd_vec_kernel), so that block skips its own
+// LayerNorm launch (x' is not read back).
+struct MlpLnOut {
+  const float* g;
+  const float* b;
+  float eps;
+  bf16_t* h;
+  int64_t ldh;
+  float* mean;
+  float* rstd;
+};
+
+template <int D, bool LNF>
 __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t* __restrict__ h2, int64_t ldh,
                                                                     const bf16_t* __restrict__ w1,
                                                                     const float* __restrict__ b1,
@@ -127,11 +146,13 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
                                                                     const float* __restrict__ b2,
                                                                     const float* __restrict__ y, int64_t ldy,
                                                                     float* __restrict__ xo, int64_t ldx, int64_t M,
-                                                                    int F) {
+                                                                    int F, MlpLnOut ln) {
   using G = MlpGeom<D>;
   __shared__ __attribute__((aligned(16))) char smem[2 * G::STG];
   __shared__ __attribute__((aligned(16))) float b1s[kMlpMaxF];
   __shared__ __attribute__((aligned(16))) float b2s[D];
+  __shared__ __attribute__((aligned(16))) float lngs[LNF ? D : 4];
+  __shared__ __attribute__((aligned(16))) float lnbs[LNF ? D : 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rr = lane & 31, h = lane >> 5;
   const int nch = F / kMlpFC;
@@ -142,6 +163,12 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   mlp_dma_chunk<D>(w1, w2, 0, smem, wave, o1, o2);  // chunk 0 of the first round -> stage 0
   for (int i = tid; i < F; i += 64 * kMlpWaves) b1s[i] = b1[i];
   if (tid < D) b2s[tid] = b2[tid];
+  if constexpr (LNF) {
+    if (tid < D) {
+      lngs[tid] = ln.g[tid];
+      lnbs[tid] = ln.b[tid];
+    }
+  }
 
   // h2 fragments of a round: lane (token rr, half h) holds d = 16 s + 8 h .. + 7 of its token
   u32x4v xf[G::KS1];
@@ -215,7 +242,47 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r0), rxo, ox, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r1), rxo, ox + 16, 0, 0);
+        if constexpr (LNF) {  // keep x' in the accumulators for the LayerNorm below
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[T][8 * j2 + j] = r0[j];
+            acc[T][8 * j2 + 4 + j] = r1[j];
+          }
+        }
       }
+    if constexpr (LNF) {
+      // token rr's row: this lane's 96 values + lane rr ^ 32's 96
+      float sm = 0.f;
+#pragma unroll
+      for (int T = 0; T < G::NT; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sm += acc[T][i];
+      const float mu = pair_sum(sm) * (1.0f / D);
+      float sq = 0.f;
+#pragma unroll
+      for (int T = 0; T < G::NT; ++T)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          acc[T][i] -= mu;
+          sq += acc[T][i] * acc[T][i];
+        }
+      const float rs = rsqrtf(pair_sum(sq) * (1.0f / D) + ln.eps);
+      const auto rh = mlp_rsrc(ln.h + row0 * ln.ldh, M - row0, ln.ldh, 2);
+#pragma unroll
+      for (int T = 0; T < G::NT; ++T)
+#pragma unroll
+        for (int j2 = 0; j2 < 2; ++j2) {
+          const int d0 = 32 * T + 16 * j2 + 8 * h;
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc[T][8 * j2 + j] * rs * lngs[d0 + j] + lnbs[d0 + j];
+          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(v), rh, (uint32_t)((rr * ln.ldh + d0) * 2), 0, 0);
+        }
+      if (h == 0 && row0 + rr < M) {
+        ln.mean[row0 + rr] = mu;
+        ln.rstd[row0 + rr] = rs;
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
 }
@@ -346,9 +413,22 @@ extern "C" int vs_mlp_fused_ok(int64_t M, int64_t D, int64_t F) {
              : 0;
 }
 
+extern "C" int vs_mlp_fwd_ln(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1,
+                             const float* b1, const void* w2, const float* b2, const float* y, int64_t ldy,
+                             float* x_out, int64_t ldx, const float* ln_g, const float* ln_b, float eps, void* h_out,
+                             int64_t ld_h_out, float* mean_out, float* rstd_out, void* stream);
+
 extern "C" int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1, const float* b1,
                           const void* w2, const float* b2, const float* y, int64_t ldy, float* x_out, int64_t ldx,
                           void* stream) {
+  return vs_mlp_fwd_ln(M, D, F, h2, ldh, w1, b1, w2, b2, y, ldy, x_out, ldx, nullptr, nullptr, 0.f, nullptr, 0, nullptr,
+                       nullptr, stream);
+}
+
+extern "C" int vs_mlp_fwd_ln(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, const void* w1,
+                             const float* b1, const void* w2, const float* b2, const float* y, int64_t ldy,
+                             float* x_out, int64_t ldx, const float* ln_g, const float* ln_b, float eps, void* h_out,
+                             int64_t ld_h_out, float* mean_out, float* rstd_out, void* stream) {
   VS_REQUIRE(vs_mlp_fused_ok(M, D, F), "vs_mlp_fwd: needs D = 192, F % 64 == 0, F <= 3072");
   VS_REQUIRE(h2 && w1 && b1 && w2 && b2 && y && x_out, "vs_mlp_fwd: null pointer");
   VS_REQUIRE(ldh >= D && ldh % 8 == 0 && ldy >= D && ldy % 4 == 0 && ldx >= D && ldx % 4 == 0 &&
@@ -358,11 +438,26 @@ extern "C" int vs_mlp_fwd(int64_t M, int64_t D, int64_t F, const void* h2, int64
   VS_REQUIRE(M * ldy * 4 < (int64_t(1) << 31) && M * ldx * 4 < (int64_t(1) << 31) && M * ldh * 2 < (int64_t(1) << 31),
              "vs_mlp_fwd: operand too large for 32-bit buffer offsets");
   hipStream_t s = (hipStream_t)stream;
+  // bytes: h2 (bf16) + y, x' (f32) per element, both weights, the biases; with the LayerNorm: + h (bf16)
+  // per element and mean / rstd per row
   ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM, s,
-                    (double)M * (double)D * (2.0 + 4.0 + 4.0) + (double)F * (double)D * 4.0 + (double)(F + D) * 4.0);
+                    (double)M * (double)D * (2.0 + 4.0 + 4.0 + (ln_g ? 2.0 : 0.0)) + (ln_g ? (double)M * 8.0 : 0.0) +
+                        (double)F * (double)D * 4.0 + (double)(F + D) * 4.0);
+  const bool lnf = ln_g != nullptr;
+  VS_REQUIRE(!lnf || (ln_b && h_out && mean_out && rstd_out && ld_h_out >= D && ld_h_out % 8 == 0 && aligned16(h_out) &&
+                      M * ld_h_out * 2 < (int64_t(1) << 31)),
+             "vs_mlp_fwd_ln: the LayerNorm output needs g, b, an aligned bf16 h and mean / rstd");
+  MlpLnOut ln = {ln_g, ln_b, eps, (bf16_t*)h_out, ld_h_out, mean_out, rstd_out};
   count_path(VS_PATH_MLP_FWD);
-  hipLaunchKernelGGL(mlp_fwd_kernel<192>, dim3((unsigned)mlp_grid(M)), dim3(64 * kMlpWaves), 0, s, (const bf16_t*)h2,
-                     ldh, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, y, ldy, x_out, ldx, M, (int)F);
+  if (lnf) {
+    hipLaunchKernelGGL((mlp_fwd_kernel<192, true>), dim3((unsigned)mlp_grid(M)), dim3(64 * kMlpWaves), 0, s,
+                       (const bf16_t*)h2, ldh, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, y, ldy, x_out, ldx, M,
+                       (int)F, ln);
+  } else {
+    hipLaunchKernelGGL((mlp_fwd_kernel<192, false>), dim3((unsigned)mlp_grid(M)), dim3(64 * kMlpWaves), 0, s,
+                       (const bf16_t*)h2, ldh, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, y, ldy, x_out, ldx, M,
+                       (int)F, ln);
+  }
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

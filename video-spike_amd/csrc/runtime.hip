@@ -93,8 +93,9 @@ ScopedTimer::~ScopedTimer() {
 
 // 2: vs_vit_layer_grad.flags; 3: .chain; 4: bf16-mode a_pre holds gelu'(pre), d_h may be bf16,
 // knobs / dispatch counters / build id; 5: a_pre == NULL selects the fused MLP (vs_mlp_*);
-// 6: vs_vit_layer.fp8_ws / fp8_ws_bytes and dtype VS_FP8 (MX-FP8 forward products)
-extern "C" int vs_version(void) { return 6; }
+// 6: vs_vit_layer.fp8_ws / fp8_ws_bytes and dtype VS_FP8 (MX-FP8 forward products);
+// 7: vs_vit_layer.next_ln_* / ln1_ready (the next block's LayerNorm1 in the fused MLP epilogue)
+extern "C" int vs_version(void) { return 7; }
 extern "C" const char* vs_build_id(void) { return VS_BUILD_ID; }
 
 extern "C" int vs_knob_get(int k) {

@@ -109,6 +109,8 @@ static int check_layer(const vs_vit_layer* L) {
   VS_REQUIRE(!mlp_fused(L) || (L->dtype == VS_BF16 && vs_mlp_fused_ok(L->batch * L->tokens, L->hidden, L->mlp) &&
                                L->a_act),
              "vs_vit_layer: a_pre == NULL (fused MLP) needs bf16, D = 192, F % 64 == 0 and an a_act scratch");
+  VS_REQUIRE(!L->next_ln_g || (mlp_fused(L) && L->next_ln_b && L->next_h1 && L->next_mean1 && L->next_rstd1),
+             "vs_vit_layer: next_ln_* (the next block's LayerNorm1) needs the fused MLP and all five pointers");
   return VS_OK;
 }
 
@@ -127,7 +129,8 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
   const int T = f8 ? VS_BF16 : L->dtype;
   auto product = [&](const vs_gemm_desc& g) { return f8 ? fp8_product(L, g, stream) : vs_gemm(&g, stream); };
   const int64_t M = L->batch * L->tokens, D = L->hidden, F = L->mlp;
-  VS_CALL(vs_layernorm_fwd(T, M, D, L->x_in, D, L->ln1_g, L->ln1_b, L->ln_eps, L->h1, D, L->mean1, L->rstd1, stream));
+  if (!L->ln1_ready)  // else the previous block's fused MLP epilogue wrote h1 / mean1 / rstd1
+    VS_CALL(vs_layernorm_fwd(T, M, D, L->x_in, D, L->ln1_g, L->ln1_b, L->ln_eps, L->h1, D, L->mean1, L->rstd1, stream));
   {
     vs_gemm_desc g = gdesc(T, T, true, true, M, 3 * D, D, L->h1, D, L->w_qkv, D, L->qkv, 3 * D, VS_EPI_BIAS);
     TimerTag tag(VS_TIMER_FWD_QKV);
@@ -154,7 +157,9 @@ extern "C" int vs_vit_layer_fwd(const vs_vit_layer* L, void* stream) {
     VS_CALL(vs_layernorm_fwd(T, M, D, L->y, D, L->ln2_g, L->ln2_b, L->ln_eps, L->h2, D, L->mean2, L->rstd2, stream));
   if (mlp_fused(L)) {  // the whole MLP in one launch; nothing of the [M, F] intermediate is stored
     TimerTag tag(VS_TIMER_FWD_MLP);
-    return vs_mlp_fwd(M, D, F, L->h2, D, L->w_fc1, L->b_fc1, L->w_fc2, L->b_fc2, L->y, D, L->x_out, D, stream);
+    // with the next block's LayerNorm1 in the epilogue when the caller chained the blocks
+    return vs_mlp_fwd_ln(M, D, F, L->h2, D, L->w_fc1, L->b_fc1, L->w_fc2, L->b_fc2, L->y, D, L->x_out, D,
+                         L->next_ln_g, L->next_ln_b, L->ln_eps, L->next_h1, D, L->next_mean1, L->next_rstd1, stream);
   }
   {
     // bf16: a_pre holds gelu'(pre) (VS_EPI_GELU_GRAD), so the backward's GELU' product is a plain

@@ -65,7 +65,9 @@ class VitLayer(ctypes.Structure):
                 ("w_fc1", c_p), ("b_fc1", c_p), ("w_fc2", c_p), ("b_fc2", c_p),
                 ("x_in", c_p), ("h1", c_p), ("mean1", c_p), ("rstd1", c_p), ("qkv", c_p), ("attn_o", c_p),
                 ("lse", c_p), ("y", c_p), ("h2", c_p), ("mean2", c_p), ("rstd2", c_p), ("a_pre", c_p),
-                ("a_act", c_p), ("x_out", c_p), ("fp8_ws", c_p), ("fp8_ws_bytes", c_i64)]
+                ("a_act", c_p), ("x_out", c_p), ("fp8_ws", c_p), ("fp8_ws_bytes", c_i64),
+                ("next_ln_g", c_p), ("next_ln_b", c_p), ("next_h1", c_p), ("next_mean1", c_p), ("next_rstd1", c_p),
+                ("ln1_ready", c_i32), ("reserved7", c_i32)]
 
 
 class VitLayerGrad(ctypes.Structure):
@@ -112,6 +114,8 @@ PROTOTYPES = {
     "vs_gemm_ln_bwd": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
                                       c_p, c_p, c_p, c_p, c_p]),
     "vs_mlp_fused_ok": (ctypes.c_int, [c_i64, c_i64, c_i64]),
+    "vs_mlp_fwd_ln": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64,
+                                     c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_p]),
     "vs_quant_mxfp8": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]),
     "vs_gemm_mxfp8": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_p, c_i64, c_p, c_i64, c_p]),
     "vs_mlp_fwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p]),

@@ -49,6 +49,8 @@ _LN_FUSE_ROWS = 65536
 # recomputes the pre-activation) wherever the shape allows it (bf16, D = 192); VSPIKE_MLP_FUSE=0 keeps
 # the two-GEMM MLP with the stored gelu / gelu' pair (A/B)
 _MLP_FUSE = os.environ.get("VSPIKE_MLP_FUSE", "1") != "0"
+# ... with block i+1's LayerNorm1 computed in block i's fused MLP epilogue (VSPIKE_LN_CHAIN=0: off, A/B)
+_LN_CHAIN = os.environ.get("VSPIKE_LN_CHAIN", "1") != "0"
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "f32": torch.float32,
            "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
@@ -368,6 +370,14 @@ class VideoMAE(nn.Module):
             x_out = act[f"X{i}"] if save_encoder else act[f"X{i % 2}"]
             structs.append(self._layer_struct(i, B, x, x_out, act, f"L{j}.", enc_lp, enc32))
             x = x_out
+        if self._mlp_fused(B) and _LN_CHAIN:
+            # block i's fused MLP epilogue runs block i+1's LayerNorm1 (its h1 / mean1 / rstd1)
+            lay = self.layout.enc
+            for i in range(Lyr - 1):
+                s, t = structs[i], structs[i + 1]
+                s.next_ln_g, s.next_ln_b = lay.view(enc32, f"{i + 1}.ln1_g").data_ptr(), lay.view(enc32, f"{i + 1}.ln1_b").data_ptr()
+                s.next_h1, s.next_mean1, s.next_rstd1 = t.h1, t.mean1, t.rstd1
+                t.ln1_ready = 1
         new = {"act": act, "structs": structs, "enc_lp": enc_lp, "head_lp": head_lp, "x_final": x, "fused": fused,
                "x_flat_lp": act["x_lp"] if lp else x.view(B, N * D), "head_ws": act.get("head_ws"),
                "sig": sig, "owner": None}
