@@ -161,6 +161,57 @@ def test_gemm_mxfp8_operand_and_scale_map():
     r8 = dequant(xq, xs) @ bv.double().t()
     print(f"[mxfp8 map] (h) real codes + scales: max abs err {float((c8.double() - r8).abs().max())} "
           f"(ref max {float(r8.abs().max())}); c {c8[0, :4].tolist()} ref {r8[0, :4].tolist()}")
+    # (i) several tiles and k-steps: exact small codes, unit scales, M = 600 (3 row tiles, ragged),
+    # N = 256 (2 column tiles), K = 768 (6 k-steps): per tile / per k-step errors
+    M2, N2, K2 = 600, 256, 768
+    a2 = (torch.randint(-8, 9, (M2, K2), device=DEV, generator=g).float() / 2).to(torch.float8_e4m3fn)
+    b2 = (torch.randint(-8, 9, (N2, K2), device=DEV, generator=g).float() / 2).to(torch.float8_e4m3fn)
+    sa2 = torch.full((M2, K2 // 32), 127, dtype=torch.uint8, device=DEV)
+    sb2 = torch.full((N2, K2 // 32), 127, dtype=torch.uint8, device=DEV)
+    c9 = torch.empty(M2, N2, device=DEV)
+    ops.gemm_mxfp8(a2.view(torch.uint8), sa2, b2.view(torch.uint8), sb2, c9)
+    torch.cuda.synchronize()
+    r9 = a2.double() @ b2.double().t()
+    e9 = (c9.double() - r9).abs()
+    tiles = [[float(e9[i * 256:(i + 1) * 256, j * 128:(j + 1) * 128].max()) for j in range(2)] for i in range(3)]
+    print(f"[mxfp8 map] (i) 3x2 tiles, 6 k-steps, unit scales: max abs err per tile {tiles}")
+    for ks in range(K2 // 128):
+        a3 = torch.zeros(M2, K2, device=DEV)
+        a3[:, ks * 128:(ks + 1) * 128] = a2[:, ks * 128:(ks + 1) * 128].float()
+        c10 = torch.empty(M2, N2, device=DEV)
+        ops.gemm_mxfp8(a3.to(torch.float8_e4m3fn).view(torch.uint8), sa2, b2.view(torch.uint8), sb2, c10)
+        torch.cuda.synchronize()
+        r10 = a3.double() @ b2.double().t()
+        print(f"[mxfp8 map] (i) only k-step {ks}: max abs err {float((c10.double() - r10).abs().max())}")
+    # (j) which row's scale meets row m: data = ones in ONE k-block kb only, scale of row m = 2^(m - 40)
+    # (distinct per row): C[m, n] = 32 * 2^(src - 40) names the row src whose scale was applied
+    import math
+    for kbj in (0, 1, 2, 5):
+        a4 = torch.zeros(M, K, device=DEV)
+        a4[:, kbj * 32:(kbj + 1) * 32] = 1.0
+        sa4 = (87 + torch.arange(M, device=DEV)[:, None] + 0 * kb[None, :]).to(torch.uint8)
+        c11 = torch.empty(M, N, device=DEV)
+        ops.gemm_mxfp8(a4.to(torch.float8_e4m3fn).view(torch.uint8), sa4, onesb, one_b, c11)
+        torch.cuda.synchronize()
+        src = [round(math.log2(max(v, 1e-30) / 32.0)) + 40 for v in c11[:, 0].tolist()]
+        print(f"[mxfp8 map] (j) A k-block {kbj}: scale source row per row m: {src}")
+        sb4 = (87 + torch.arange(N, device=DEV)[:, None] + 0 * kb[None, :]).to(torch.uint8)
+        c12 = torch.empty(M, N, device=DEV)
+        ops.gemm_mxfp8(a4.to(torch.float8_e4m3fn).view(torch.uint8), one_a, onesb, sb4, c12)
+        torch.cuda.synchronize()
+        srcb = [round(math.log2(max(v, 1e-30) / 32.0)) + 40 for v in c12[0, :64].tolist()]
+        print(f"[mxfp8 map] (j) B k-block {kbj}: scale source col per col n < 64: {srcb}")
+    # (k) which k-block scale meets k position p: A = 1 at k = p only, scale of block kb = 2^kb
+    sak = (127 + kb[None, :] + 0 * torch.arange(M, device=DEV)[:, None]).to(torch.uint8)
+    blocks = []
+    for p in range(0, K, 4):
+        a5 = torch.zeros(M, K, device=DEV)
+        a5[:, p] = 1.0
+        c13 = torch.empty(M, N, device=DEV)
+        ops.gemm_mxfp8(a5.to(torch.float8_e4m3fn).view(torch.uint8), sak, onesb, one_b, c13)
+        torch.cuda.synchronize()
+        blocks.append(round(math.log2(max(float(c13[0, 0]), 1e-30))))
+    print(f"[mxfp8 map] (k) A scale block applied at k = 0, 4, 8, ...: {blocks}")
     assert ea == 0.0
 
 

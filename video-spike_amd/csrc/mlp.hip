@@ -30,7 +30,6 @@ namespace vs {
 constexpr int kMlpWaves = 8;
 constexpr int kMlpFC = 64;          // intermediate features per chunk
 constexpr int kMlpMaxF = 3072;
-constexpr int kMlpRound = 32 * kMlpWaves;  // tokens per workgroup round
 
 __device__ __forceinline__ int mlp_swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 __device__ __forceinline__ int mlp_cpos(int c, int r) { return (c & ~7) | ((c & 7) ^ ((r >> 1) & 7)); }
@@ -44,6 +43,33 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base, int
 __device__ __forceinline__ float pair_sum(float v) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// GELU for the fused bf16 MLP: x * sigmoid(x (k1 + k3 x^2 + k5 x^4)), a minimax fit of x * Phi(x)
+// (scipy Nelder-Mead on [-9, 9]): |gelu - x Phi(x)| <= 2.5e-5 everywhere (the tanh form: 4.7e-4;
+// A&S 7.1.26 in common.h: 1.5e-7 but twice the VALU), i.e. ~1 % of the bf16 rounding the result gets
+// anyway.  x^2 is clamped at 81 (the quartic turns negative past |x| = 11.1; sigmoid is saturated
+// there).  7 VALU + exp2 + rcp per value.  The backward uses the SAME function's exact derivative
+// s + x s (1 - s) u'(x) (|error vs Phi(x) + x phi(x)| <= 1.1e-4).
+constexpr float kGk1 = 1.59501577f, kGk3 = 7.40112920e-2f, kGk5 = -7.03033577e-4f;
+constexpr float kGl2e = 1.4426950408889634f;
+__device__ __forceinline__ float gelu_sp_s(float x, float& t) {  // sigmoid(u(x)); t = min(x^2, 81)
+  t = fminf(x * x, 81.f);
+  float p = fmaf(t, -kGk5 * kGl2e, -kGk3 * kGl2e);
+  p = fmaf(t, p, -kGk1 * kGl2e);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * p));
+}
+__device__ __forceinline__ float gelu_sp(float x) {
+  float t;
+  return x * gelu_sp_s(x, t);
+}
+__device__ __forceinline__ float gelu_sp_both(float x, float& grad) {
+  float t;
+  const float sg = gelu_sp_s(x, t);
+  float q = fmaf(t, 5.f * kGk5, 3.f * kGk3);
+  q = fmaf(t, q, kGk1);                      // u'(x)
+  grad = fmaf(x * fmaf(-sg, sg, sg), q, sg);  // s + x s (1 - s) u'
+  return x * sg;
 }
 
 __device__ __forceinline__ u32x4v mlp_pack8(const float* v) {
@@ -103,24 +129,54 @@ __device__ __forceinline__ void mlp_dma_chunk(const bf16_t* w1, const bf16_t* w2
   for (int k = 0; k < G::DMA2; ++k) glds16_asm_so(s2, o2[k], stage + G::W1B + 1024 * (wave * G::DMA2 + k));
 }
 
-// pre^T (two 32-row tiles of the chunk's 64 features x 32 tokens) = W1_c h2^T
-template <int D>
-__device__ __forceinline__ void mlp_stage1(const char* st, int lane, const u32x4v (&xf)[MlpGeom<D>::KS1],
-                                           f32x16 (&pre)[2]) {
-  using G = MlpGeom<D>;
-  const int rr = lane & 31, h = lane >> 5;
-  pre[0] = f32x16{};
-  pre[1] = f32x16{};
+// pre^T tile t (features 32 t .. of the chunk x 32 tokens) = W1_c h2^T: 12 MFMAs (D = 192)
+// Per-lane byte offsets of a 32x32x16 A-fragment read of k-step s from an image whose 16-B chunk c
+// of row r sits at (c & ~7) | ((c & 7) ^ ((r >> 1) & 7)): for c = 2 s + h the position is
+// 8 (s >> 2) + 2 ((s & 3) ^ (key >> 1)) + (h ^ (key & 1)), so 4 per-lane offsets (s & 3) plus the
+// immediate 128 (s >> 2) cover every k-step (and +32 rows per tile is an immediate too).
+__device__ __forceinline__ void mlp_frag_offsets(int lane, int row_bytes, uint32_t (&off)[4]) {
+  const int rr = lane & 31, h = lane >> 5, key = (rr >> 1) & 7;
 #pragma unroll
-  for (int s = 0; s < G::KS1; ++s) {
-    const int cp = mlp_cpos(2 * s + h, rr);
+  for (int j = 0; j < 4; ++j) off[j] = (uint32_t)(rr * row_bytes + 16 * (2 * (j ^ (key >> 1)) + (h ^ (key & 1))));
+}
+
+// the bias of pre^T tile t of chunk c in accumulator order (features c*64 + 32 t + 16 j2 + 8 h + j),
+// the W1 product's initial accumulator: the MFMA chain then yields h2 W1^T + b1 directly
+__device__ __forceinline__ f32x16 mlp_bias_acc(const float* b1s, int c, int t, int h) {
+  f32x16 a;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const bf16x8 wa = *(const bf16x8*)(st + (32 * t + rr) * (2 * D) + 16 * cp);
-      pre[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, __builtin_bit_cast(bf16x8, xf[s]), pre[t], 0, 0, 0);
+  for (int j2 = 0; j2 < 2; ++j2) {
+    const float* bb = b1s + c * kMlpFC + 32 * t + 16 * j2 + 8 * h;
+    const f32x4 bl = *(const f32x4*)bb, bh = *(const f32x4*)(bb + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[8 * j2 + j] = bl[j];
+      a[8 * j2 + 4 + j] = bh[j];
     }
   }
+  return a;
 }
+
+template <int D>
+__device__ __forceinline__ f32x16 mlp_s1(const char* st, const uint32_t (&off)[4], const u32x4v (&xf)[MlpGeom<D>::KS1],
+                                         int t, f32x16 pre) {
+  using G = MlpGeom<D>;
+#pragma unroll
+  for (int s = 0; s < G::KS1; ++s) {
+    const bf16x8 wa = *(const bf16x8*)(st + off[s & 3] + 32 * t * (2 * D) + 128 * (s >> 2));
+    pre = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, __builtin_bit_cast(bf16x8, xf[s]), pre, 0, 0, 0);
+  }
+  return pre;
+}
+
+// Software pipelining by pinned segments: hipcc's scheduler (and T19's sched_group_barrier, which it
+// ignored here) clusters a product's 12 MFMAs and puts the independent GELU work of the other tile
+// after them, so one wave alternates long MFMA-only and VALU-only stretches and the two waves of a
+// SIMD, aligned by the per-chunk barrier, do the same at the same time.  Each MFMA is therefore
+// emitted in its own segment (closed by sched_barrier(0)) together with a share of the VALU work
+// and the LDS read of the fragment two MFMAs ahead.
+// Values of a 16-value tile processed in segment i of 12: [i * 4 / 3, (i + 1) * 4 / 3)
+__device__ __forceinline__ constexpr int mlp_seg_lo(int i) { return i * 4 / 3; }
 
 // ---------------------------------------------------------------------------------------------
 // forward
@@ -156,8 +212,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rr = lane & 31, h = lane >> 5;
   const int nch = F / kMlpFC;
-  const int64_t nround = (M + kMlpRound - 1) / kMlpRound;
-  if ((int64_t)blockIdx.x >= nround) return;  // workgroup-uniform
+  if ((int64_t)blockIdx.x * 32 >= M) return;  // workgroup-uniform: no block at all
   uint32_t o1[G::DMA1], o2[G::DMA2];
   mlp_dma_offsets<D>(wave, lane, F, true, o1, o2);
   mlp_dma_chunk<D>(w1, w2, 0, smem, wave, o1, o2);  // chunk 0 of the first round -> stage 0
@@ -170,59 +225,105 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
     }
   }
 
+  // Rounds: in round r wave w owns the 32-token block b = r * 8 G + w G + blockIdx.x (blocks dealt
+  // over the workgroups first: the last, partial round gives single live waves to as many workgroups
+  // as it has blocks instead of filling a few, so it costs about half a round instead of a whole one).
+  const int64_t nb = (M + 31) / 32, Gs = gridDim.x;
+  auto blk = [&](int64_t r) { return r * Gs * kMlpWaves + (int64_t)wave * Gs + blockIdx.x; };
   // h2 fragments of a round: lane (token rr, half h) holds d = 16 s + 8 h .. + 7 of its token
   u32x4v xf[G::KS1];
-  auto load_x = [&](int64_t rd) {
-    const int64_t row0 = rd * kMlpRound + 32 * wave;
+  const uint32_t hxo = (uint32_t)((rr * ldh + 8 * h) * 2);
+  auto load_x = [&](int64_t r) {
+    const int64_t row0 = blk(r) * 32;
     const auto rx = mlp_rsrc(h2 + row0 * ldh, M - row0, ldh, 2);
 #pragma unroll
     for (int s = 0; s < G::KS1; ++s)
-      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)((rr * ldh + 16 * s + 8 * h) * 2), 0, 0);
+      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, hxo + 32 * s, 0, 0);
   };
-  load_x(blockIdx.x);
+  uint32_t off1[4], off2[4];
+  mlp_frag_offsets(lane, 2 * D, off1);
+  mlp_frag_offsets(lane, 128, off2);
+  auto pack16 = [&](const float (&g)[16], u32x4v& f0, u32x4v& f1) {
+    f0 = mlp_pack8(g);
+    f1 = mlp_pack8(g + 8);
+  };
+  // pre^T tile 1 (12 MFMAs) with the GELU of tile 0 (`p0` + bias -> g) spread over its segments
+  auto s1_act = [&](const char* st, const f32x16& p0, f32x16 p1, float (&g)[16]) {
+    bf16x8 wa = *(const bf16x8*)(st + off1[0] + 32 * (2 * D));
+#pragma unroll
+    for (int k = 0; k < G::KS1; ++k) {
+      const bf16x8 cur = wa;
+      if (k + 1 < G::KS1) wa = *(const bf16x8*)(st + off1[(k + 1) & 3] + 32 * (2 * D) + 128 * ((k + 1) >> 2));
+      p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, xf[k]), p1, 0, 0, 0);
+#pragma unroll
+      for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g[i] = gelu_sp(p0[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return p1;
+  };
+  // x'^T += W2_c a^T over k-steps 2 t, 2 t + 1 (12 MFMAs); optionally the GELU of the other tile
+  // (`pn` + bias -> g) spread over the segments
+  auto s2_act = [&](const char* st2, int t, const u32x4v& f0, const u32x4v& f1, f32x16 (&acc)[G::NT],
+                    const f32x16* pn, float (&g)[16]) {
+    bf16x8 wb = *(const bf16x8*)(st2 + off2[(2 * t) & 3]);
+#pragma unroll
+    for (int k = 0; k < 2 * G::NT; ++k) {
+      const int sk = 2 * t + k / G::NT, T = k % G::NT;
+      const bf16x8 cur = wb;
+      if (k + 1 < 2 * G::NT) {
+        const int s1 = 2 * t + (k + 1) / G::NT, T1 = (k + 1) % G::NT;
+        wb = *(const bf16x8*)(st2 + off2[s1 & 3] + 32 * T1 * 128);
+      }
+      acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, sk & 1 ? f1 : f0), acc[T], 0, 0, 0);
+      if (pn) {
+#pragma unroll
+        for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g[i] = gelu_sp((*pn)[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  load_x(0);
   int q = 0;  // chunk stream position: stage q & 1
-  for (int64_t rd = blockIdx.x; rd < nround; rd += gridDim.x) {
-    const bool more = rd + gridDim.x < nround;
+  for (int64_t r = 0; r * Gs * kMlpWaves + blockIdx.x < nb; ++r) {
+    const bool more = (r + 1) * Gs * kMlpWaves + blockIdx.x < nb;
+    const bool live = blk(r) < nb;  // wave-uniform
     f32x16 acc[G::NT];
 #pragma unroll
     for (int T = 0; T < G::NT; ++T) acc[T] = f32x16{};
-    for (int c = 0; c < nch; ++c, ++q) {
-      // this chunk's DMA pieces (every wave's) landed; every wave is done with the other stage
+    // one chunk: its DMA pieces (every wave's) landed, every wave is done with the other stage; the
+    // last chunk of a round (PF) also prefetches the next round's h2 fragments
+    auto chunk = [&](int c, auto pfc) {
+      constexpr bool PF = decltype(pfc)::value;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      const bool last = c + 1 == nch;
-      if (!last || more) mlp_dma_chunk<D>(w1, w2, last ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
-      const char* st = smem + (q & 1) * G::STG;
-      f32x16 pre[2];
-      mlp_stage1<D>(st, lane, xf, pre);
-      if (last && more) load_x(rd + gridDim.x);  // the fragments are dead after the last chunk's W1 product
-      // bias + GELU, as the next product's B fragments (k-step s = 2 t + j2: features 16 s + 8 h + j)
-      u32x4v af[4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int j2 = 0; j2 < 2; ++j2) {
-          const float* bb = b1s + c * kMlpFC + 32 * t + 16 * j2 + 8 * h;
-          const f32x4 bl = *(const f32x4*)bb, bh = *(const f32x4*)(bb + 4);
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_fast(pre[t][8 * j2 + j] + (j < 4 ? bl[j] : bh[j - 4]));
-          af[2 * t + j2] = mlp_pack8(v);
+      if (!PF || more) mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      if (live) {
+        const char* st = smem + (q & 1) * G::STG;
+        const char* st2 = st + G::W1B;
+        // software pipeline over the chunk's two 32-feature tiles: S1(t0) | S1(t1) + GELU(t0) |
+        // S2(t0) + GELU(t1) | S2(t1)
+        float g[16];
+        const f32x16 p0 = mlp_s1<D>(st, off1, xf, 0, mlp_bias_acc(b1s, c, 0, h));
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x16 p1 = s1_act(st, p0, mlp_bias_acc(b1s, c, 1, h), g);
+        u32x4v a0, a1, a2, a3;
+        pack16(g, a0, a1);
+        if constexpr (PF) {
+          if (more) load_x(r + 1);  // the fragments are dead after the last chunk's W1 products
         }
-      // x'^T += W2_c a^T
-      const char* st2 = st + G::W1B;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int T = 0; T < G::NT; ++T) {
-          const int p = 32 * T + rr;
-          const bf16x8 wb = *(const bf16x8*)(st2 + p * 128 + 16 * ((2 * s + h) ^ ((p >> 1) & 7)));
-          acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb, __builtin_bit_cast(bf16x8, af[s]), acc[T], 0, 0, 0);
-        }
+        __builtin_amdgcn_sched_barrier(0);
+        s2_act(st2, 0, a0, a1, acc, &p1, g);
+        pack16(g, a2, a3);
+        __builtin_amdgcn_sched_barrier(0);
+        s2_act(st2, 1, a2, a3, acc, nullptr, g);
       }
-    }
+      ++q;
+    };
+    for (int c = 0; c + 1 < nch; ++c) chunk(c, IC<0>{});
+    chunk(nch - 1, IC<1>{});
+    if (!live) continue;
     // epilogue: x' = y + acc + b2; lane (token rr, half h) holds d = 32 T + 16 j2 + 8 h .. + 7
-    const int64_t row0 = rd * kMlpRound + 32 * wave;
+    const int64_t row0 = blk(r) * 32;
     const auto ry = mlp_rsrc(y + row0 * ldy, M - row0, ldy, 4);
     const auto rxo = mlp_rsrc(xo + row0 * ldx, M - row0, ldx, 4);
 #pragma unroll
@@ -308,8 +409,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rr = lane & 31, h = lane >> 5;
   const int nch = F / kMlpFC;
-  const int64_t nround = (M + kMlpRound - 1) / kMlpRound;
-  if ((int64_t)blockIdx.x >= nround) return;
+  if ((int64_t)blockIdx.x * 32 >= M) return;
   uint32_t o1[G::DMA1], o2[G::DMA2];
   mlp_dma_offsets<D>(wave, lane, F, false, o1, o2);  // W2 image rows in natural d order
   mlp_dma_chunk<D>(w1, w2, 0, smem, wave, o1, o2);
@@ -328,66 +428,137 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
     return d * 128 + 16 * (cl ^ ((d >> 1) & 7)) + 2 * (f & 7);
   };
 
+  uint32_t off1[4];
+  mlp_frag_offsets(lane, 2 * D, off1);
+  const int64_t nb = (M + 31) / 32, Gs = gridDim.x;
+  auto blk = [&](int64_t r) { return r * Gs * kMlpWaves + (int64_t)wave * Gs + blockIdx.x; };
   u32x4v xf[G::KS1], yf[G::KS1];
-  auto load_xy = [&](int64_t rd) {
-    const int64_t row0 = rd * kMlpRound + 32 * wave;
+  const uint32_t xo = (uint32_t)((rr * ldh + 8 * h) * 2), yo = (uint32_t)((rr * lddy + 8 * h) * 2);
+  auto load_xy = [&](int64_t r) {
+    const int64_t row0 = blk(r) * 32;
     const auto rx = mlp_rsrc(h2 + row0 * ldh, M - row0, ldh, 2);
     const auto ry = mlp_rsrc(dy + row0 * lddy, M - row0, lddy, 2);
 #pragma unroll
     for (int s = 0; s < G::KS1; ++s) {
-      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, (uint32_t)((rr * ldh + 16 * s + 8 * h) * 2), 0, 0);
-      yf[s] = __builtin_amdgcn_raw_buffer_load_b128(ry, (uint32_t)((rr * lddy + 16 * s + 8 * h) * 2), 0, 0);
+      xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xo + 32 * s, 0, 0);
+      yf[s] = __builtin_amdgcn_raw_buffer_load_b128(ry, yo + 32 * s, 0, 0);
     }
   };
-  load_xy(blockIdx.x);
+  // the two 12-MFMA products of a chunk, each MFMA in a pinned segment with work(k) beside it
+  // (see mlp_seg_lo): pre^T tile t = W1_c h2^T, da^T tile t = W2_c^T dx'^T (transposed A reads)
+  auto s1_w = [&](const char* st, int t, f32x16 acc, auto&& work) {
+    bf16x8 wa = *(const bf16x8*)(st + off1[0] + 32 * t * (2 * D));
+#pragma unroll
+    for (int k = 0; k < G::KS1; ++k) {
+      const bf16x8 cur = wa;
+      if (k + 1 < G::KS1) wa = *(const bf16x8*)(st + off1[(k + 1) & 3] + 32 * t * (2 * D) + 128 * ((k + 1) >> 2));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, xf[k]), acc, 0, 0, 0);
+      work(k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+  };
+  typedef __attribute__((ext_vector_type(8))) short short8v;
+  // tr_addr(t, k, e) = trb[t][e] + 2048 k: the chunk XOR key (d >> 1) & 7 does not depend on k
+  uint32_t trb[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) trb[t][e] = (uint32_t)tr_addr(t, 0, e);
+  auto trw = [&](const char* st2, int t, int k) {
+    const short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + trb[t][0] + 2048 * k));
+    const short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + trb[t][1] + 2048 * k));
+    const short8v wv = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    return __builtin_bit_cast(bf16x8, wv);
+  };
+  auto da_w = [&](const char* st2, int t, auto&& work) {
+    f32x16 acc = f32x16{};
+    bf16x8 wa = trw(st2, t, 0);
+#pragma unroll
+    for (int k = 0; k < G::KS1; ++k) {
+      const bf16x8 cur = wa;
+      if (k + 1 < G::KS1) wa = trw(st2, t, k + 1);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, yf[k]), acc, 0, 0, 0);
+      work(k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+  };
+  auto store16 = [&](const __amdgpu_buffer_rsrc_t& rs, int64_t ld, int c, int t, const float (&v)[16]) {
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2) {
+      // every offset in voffset, soffset 0: a dwordx4 store whose soffset is an SGPR, followed at once
+      // by a VALU write of its data VGPRs, stored the NEW value of dwords 1.. in lanes 12-15 of each
+      // 16 on gfx950 (measured: da's dword 1 took the next segment's v_pk_fma result; hipcc inserts
+      // no wait state there), so the chunk offset is added to the lane offset instead
+      __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(v + 8 * j2), rs,
+                                             (uint32_t)((rr * ld + 8 * h) * 2) + (uint32_t)(c * kMlpFC * 2) +
+                                                 64 * t + 32 * j2,
+                                             0, 0);
+    }
+  };
+  load_xy(0);
   int q = 0;
-  for (int64_t rd = blockIdx.x; rd < nround; rd += gridDim.x) {
-    const bool more = rd + gridDim.x < nround;
-    const int64_t row0 = rd * kMlpRound + 32 * wave;
+  for (int64_t r = 0; r * Gs * kMlpWaves + blockIdx.x < nb; ++r) {
+    const bool more = (r + 1) * Gs * kMlpWaves + blockIdx.x < nb;
+    const bool live = blk(r) < nb;
+    const int64_t row0 = blk(r) * 32;
     const auto rda = mlp_rsrc(da + row0 * ldda, M - row0, ldda, 2);
     const auto raa = mlp_rsrc(aout + row0 * lda, M - row0, lda, 2);
-    for (int c = 0; c < nch; ++c, ++q) {
+    auto chunk = [&](int c, auto pfc) {
+      constexpr bool PF = decltype(pfc)::value;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      const bool last = c + 1 == nch;
-      if (!last || more) mlp_dma_chunk<D>(w1, w2, last ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
-      const char* st = smem + (q & 1) * G::STG;
-      f32x16 pre[2];
-      mlp_stage1<D>(st, lane, xf, pre);
-      // da^T (same register layout as pre^T) = W2_c^T dx'^T
-      f32x16 dac[2] = {f32x16{}, f32x16{}};
-      const char* st2 = st + G::W1B;
+      if (!PF || more) mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      if (live) {
+        const char* st = smem + (q & 1) * G::STG;
+        const char* st2 = st + G::W1B;
+        // S1(t0) | S1(t1) + act(t0) | da(t0) + act(t1) | da(t1) + da-product(t0) | da-product(t1)
+        float av[16], g0[16], g1[16];  // g0 / g1 become the da values in place
+        const f32x16 p0 = s1_w(st, 0, mlp_bias_acc(b1s, c, 0, h), [&](int) {});
+        const f32x16 p1 = s1_w(st, 1, mlp_bias_acc(b1s, c, 1, h), [&](int k) {
 #pragma unroll
-      for (int s = 0; s < G::KS1; ++s) {
+          for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) av[i] = gelu_sp_both(p0[i], g0[i]);
+        });
+        store16(raa, lda, c, 0, av);
+        if constexpr (PF) {  // h2 fragments are dead after the last chunk's W1 products
+          if (more) {
+            const int64_t nrow0 = blk(r + 1) * 32;
+            const auto rx = mlp_rsrc(h2 + nrow0 * ldh, M - nrow0, ldh, 2);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + tr_addr(t, s, 0)));
-          const short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st2 + tr_addr(t, s, 1)));
-          typedef __attribute__((ext_vector_type(8))) short short8v;
-          const short8v wv = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-          dac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wv),
-                                                            __builtin_bit_cast(bf16x8, yf[s]), dac[t], 0, 0, 0);
-        }
-      }
-      if (last && more) load_xy(rd + gridDim.x);
-      // lane (token rr, half h): features c*64 + 32 t + 16 j2 + 8 h .. + 7
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int j2 = 0; j2 < 2; ++j2) {
-          const int f0 = c * kMlpFC + 32 * t + 16 * j2 + 8 * h;
-          const f32x4 bl = *(const f32x4*)(b1s + f0), bh = *(const f32x4*)(b1s + f0 + 4);
-          float av[8], dv[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float gr;
-            av[j] = gelu_fast_both(pre[t][8 * j2 + j] + (j < 4 ? bl[j] : bh[j - 4]), gr);
-            dv[j] = dac[t][8 * j2 + j] * gr;
+            for (int s = 0; s < G::KS1; ++s)
+              xf[s] = __builtin_amdgcn_raw_buffer_load_b128(rx, xo + 32 * s, 0, 0);
           }
-          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(dv), rda, (uint32_t)((rr * ldda + f0) * 2), 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(av), raa, (uint32_t)((rr * lda + f0) * 2), 0, 0);
         }
-    }
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x16 d0 = da_w(st2, 0, [&](int k) {
+#pragma unroll
+          for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) av[i] = gelu_sp_both(p1[i], g1[i]);
+        });
+        store16(raa, lda, c, 1, av);
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x16 d1 = da_w(st2, 1, [&](int k) {
+#pragma unroll
+          for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g0[i] *= d0[i];
+        });
+        store16(rda, ldda, c, 0, g0);
+        if constexpr (PF) {  // dx' fragments are dead after the last chunk's W2 products
+          if (more) {
+            const int64_t nrow0 = blk(r + 1) * 32;
+            const auto ry = mlp_rsrc(dy + nrow0 * lddy, M - nrow0, lddy, 2);
+#pragma unroll
+            for (int s = 0; s < G::KS1; ++s)
+              yf[s] = __builtin_amdgcn_raw_buffer_load_b128(ry, yo + 32 * s, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) g1[i] *= d1[i];
+        store16(rda, ldda, c, 1, g1);
+      }
+      ++q;
+    };
+    for (int c = 0; c + 1 < nch; ++c) chunk(c, IC<0>{});
+    chunk(nch - 1, IC<1>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -398,8 +569,8 @@ static int mlp_grid(int64_t M) {
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n;
   }();
-  const int64_t rounds = (M + kMlpRound - 1) / kMlpRound;
-  return (int)(rounds < cus ? rounds : cus);
+  const int64_t blocks = (M + 31) / 32;  // every workgroup needs at least one 32-token block
+  return (int)(blocks < cus ? blocks : cus);
 }
 
 }  // namespace vs
