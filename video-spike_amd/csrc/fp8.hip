@@ -15,8 +15,9 @@
 // per wave: 2 x 2 tiles of 32 x 32), 128-deep k-steps (two 64-deep MFMA k-steps), 2-stage LDS-DMA
 // ring of 49.5 KB stages (fp8 rows of 128 B with a 16-B chunk XOR of (row >> 1) & 7; one dword of
 // scales per row); operand layout of the 32x32x64 f8 MFMA: lane (r = lane & 31, h = lane >> 5)
-// holds row r, k = 32 h .. 32 h + 31 (32 bytes), and its scale (byte 0 of the scale VGPR: the
-// instruction reads byte 0 whatever OPSEL says) is that row's scale of k-block h.
+// holds row r, k = 16 h .. 16 h + 15 in VGPRs 0-3 and k = 32 + 16 h .. in VGPRs 4-7 (32 bytes), and
+// its scale (byte 0 of the scale VGPR: the instruction reads byte 0 whatever OPSEL says) is that
+// row's scale of k-block h (block 0 = k 0-31 = VGPRs 0-3 of both halves, block 1 = VGPRs 4-7).
 #include "common.h"
 #include "gemm_common.h"
 
@@ -164,10 +165,15 @@ __global__ __launch_bounds__(512, 1) void gemm_mxfp8_kernel(const uint8_t* __res
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   const int rr = lane & 31, h = lane >> 5;
-  auto frag = [&](const char* img, int row, int kk) {  // 32 bytes: k = 64 kk + 32 h .. + 31 of `row`
-    const int key = (row >> 1) & 7, c0 = 4 * kk + 2 * h;
+  // 32 bytes of `row` for MFMA k-step kk: VGPRs 0-3 = k 64 kk + 16 h .. + 15 and VGPRs 4-7 =
+  // k 64 kk + 32 + 16 h .. + 15.  The instruction's 32-element scale block 0 is VGPRs 0-3 of BOTH lane
+  // halves (its scale from lane h = 0), block 1 VGPRs 4-7 (scale from lane h = 1): measured with a
+  // single nonzero k and a distinct scale per block (test_gpu_fp8.py map (k)).  A data-only test cannot
+  // see this (any k permutation shared by A and B gives the same product).
+  auto frag = [&](const char* img, int row, int kk) {
+    const int key = (row >> 1) & 7, c0 = 4 * kk + h;
     const u32x4v lo = *(const u32x4v*)(img + row * 128 + 16 * (c0 ^ key));
-    const u32x4v hi = *(const u32x4v*)(img + row * 128 + 16 * ((c0 + 1) ^ key));
+    const u32x4v hi = *(const u32x4v*)(img + row * 128 + 16 * ((c0 + 2) ^ key));
     return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   };
   auto compute = [&](const char* st) {

@@ -194,6 +194,11 @@ struct MlpLnOut {
   float* rstd;
 };
 
+// s_waitcnt vmcnt(N): every vector-memory op but the newest N has completed (they complete in order)
+template <int N>
+__device__ __forceinline__ void mlp_vmcnt_le() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
+}
 template <int D, bool LNF>
 __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t* __restrict__ h2, int64_t ldh,
                                                                     const bf16_t* __restrict__ w1,
@@ -282,21 +287,52 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  // The residual is the W2 product's initial accumulator: y of a round's tokens is loaded into acc
+  // right after the previous round's epilogue stored it (the loads then have chunk 0's W1 products to
+  // land), so the epilogue only adds b2 and stores.  Lane (token rr, half h) holds d = 32 T + 16 j2 +
+  // 8 h .. + 7 in acc[T][8 j2 ..].
+  f32x16 acc[G::NT];
+  auto load_y = [&](int64_t r) {
+    const int64_t row0 = blk(r) * 32;
+    const auto ry = mlp_rsrc(y + row0 * ldy, M - row0, ldy, 4);
+#pragma unroll
+    for (int T = 0; T < G::NT; ++T)
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2) {
+        const uint32_t oy = (uint32_t)((rr * ldy + 32 * T + 16 * j2 + 8 * h) * 4);
+        const f32x4 y0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy, 0, 0));
+        const f32x4 y1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy + 16, 0, 0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[T][8 * j2 + j] = y0[j];
+          acc[T][8 * j2 + 4 + j] = y1[j];
+        }
+      }
+  };
   load_x(0);
+  if (blk(0) < nb) load_y(0);
   int q = 0;  // chunk stream position: stage q & 1
+  // Vector-memory ops a live wave issues after the DMA of a round's chunk 0 (started at the previous
+  // round's last chunk): the h2 prefetch, the epilogue's stores, the next round's y loads.  Chunk 0
+  // waits for the DMA only (vmcnt(N) with N = the ops issued after it), not for those.
+  constexpr int kNX = G::KS1, kNS = 4 * G::NT + (LNF ? 2 * G::NT + 2 : 0), kNY = 4 * G::NT;
+  bool live_prev = false;
   for (int64_t r = 0; r * Gs * kMlpWaves + blockIdx.x < nb; ++r) {
     const bool more = (r + 1) * Gs * kMlpWaves + blockIdx.x < nb;
     const bool live = blk(r) < nb;  // wave-uniform
-    f32x16 acc[G::NT];
-#pragma unroll
-    for (int T = 0; T < G::NT; ++T) acc[T] = f32x16{};
     // one chunk: its DMA pieces (every wave's) landed, every wave is done with the other stage; the
     // last chunk of a round (PF) also prefetches the next round's h2 fragments
     auto chunk = [&](int c, auto pfc) {
       constexpr bool PF = decltype(pfc)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (c == 0 && live_prev && live) mlp_vmcnt_le<kNX + kNS + kNY>();
+      else if (c == 0 && live_prev) mlp_vmcnt_le<kNX + kNS>();
+      else mlp_vmcnt_le<0>();
       __syncthreads();
-      if (!PF || more) mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      // chunk 0 issues the next chunk's DMA after its first W2 tile: hipcc cannot see the asm DMA, and
+      // its wait for the y loads (the accumulators' first use, in that tile) would drain it too
+      const bool late_dma = !PF && c == 0;
+      auto dma_next = [&] { mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2); };
+      if (!late_dma && (!PF || more)) dma_next();
       if (live) {
         const char* st = smem + (q & 1) * G::STG;
         const char* st2 = st + G::W1B;
@@ -315,31 +351,34 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
         s2_act(st2, 0, a0, a1, acc, &p1, g);
         pack16(g, a2, a3);
         __builtin_amdgcn_sched_barrier(0);
+        if (late_dma) dma_next();
         s2_act(st2, 1, a2, a3, acc, nullptr, g);
+      } else if (late_dma) {
+        dma_next();
       }
       ++q;
     };
     for (int c = 0; c + 1 < nch; ++c) chunk(c, IC<0>{});
     chunk(nch - 1, IC<1>{});
-    if (!live) continue;
-    // epilogue: x' = y + acc + b2; lane (token rr, half h) holds d = 32 T + 16 j2 + 8 h .. + 7
+    if (!live) {  // (and every later round: blocks only grow)
+      live_prev = false;
+      continue;
+    }
+    // epilogue: x' = acc + b2 (acc started from y)
     const int64_t row0 = blk(r) * 32;
-    const auto ry = mlp_rsrc(y + row0 * ldy, M - row0, ldy, 4);
     const auto rxo = mlp_rsrc(xo + row0 * ldx, M - row0, ldx, 4);
 #pragma unroll
     for (int T = 0; T < G::NT; ++T)
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2) {
         const int d0 = 32 * T + 16 * j2 + 8 * h;
-        const uint32_t oy = (uint32_t)((rr * ldy + d0) * 4), ox = (uint32_t)((rr * ldx + d0) * 4);
-        const f32x4 y0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy, 0, 0));
-        const f32x4 y1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy + 16, 0, 0));
+        const uint32_t ox = (uint32_t)((rr * ldx + d0) * 4);
         const f32x4 c0 = *(const f32x4*)(b2s + d0), c1 = *(const f32x4*)(b2s + d0 + 4);
         f32x4 r0, r1;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          r0[j] = y0[j] + (acc[T][8 * j2 + j] + c0[j]);
-          r1[j] = y1[j] + (acc[T][8 * j2 + 4 + j] + c1[j]);
+          r0[j] = acc[T][8 * j2 + j] + c0[j];
+          r1[j] = acc[T][8 * j2 + 4 + j] + c1[j];
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r0), rxo, ox, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, r1), rxo, ox + 16, 0, 0);
@@ -384,6 +423,8 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
         ln.rstd[row0 + rr] = rs;
       }
     }
+    if (more && blk(r + 1) < nb) load_y(r + 1);
+    live_prev = live;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
 }
@@ -499,6 +540,13 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
   };
   load_xy(0);
   int q = 0;
+  // Vector-memory ops a live wave issues after a chunk's DMA (started one chunk earlier): that
+  // chunk's 8 stores of a / da (6 in chunk 0, whose DMA goes out after its first W2 tile: hipcc
+  // cannot see the asm DMA, and its waits for the prefetched h2 / dx' fragments would drain it), and
+  // in a round's last chunk also the next round's h2 / dx' prefetch.  The chunk start waits for the
+  // DMA only (vmcnt(N), N = those ops): the stores stay in flight.
+  constexpr int kNSt = 8, kNSt0 = 6, kNPf = 8 + 2 * G::KS1;
+  bool live_prev = false;
   for (int64_t r = 0; r * Gs * kMlpWaves + blockIdx.x < nb; ++r) {
     const bool more = (r + 1) * Gs * kMlpWaves + blockIdx.x < nb;
     const bool live = blk(r) < nb;
@@ -507,9 +555,14 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
     const auto raa = mlp_rsrc(aout + row0 * lda, M - row0, lda, 2);
     auto chunk = [&](int c, auto pfc) {
       constexpr bool PF = decltype(pfc)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (c > 1 && live) mlp_vmcnt_le<kNSt>();
+      else if (c == 1 && live) mlp_vmcnt_le<kNSt0>();
+      else if (c == 0 && live_prev) mlp_vmcnt_le<kNPf>();
+      else mlp_vmcnt_le<0>();
       __syncthreads();
-      if (!PF || more) mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2);
+      const bool late_dma = !PF && c == 0;
+      auto dma_next = [&] { mlp_dma_chunk<D>(w1, w2, PF ? 0 : c + 1, smem + ((q + 1) & 1) * G::STG, wave, o1, o2); };
+      if (!late_dma && (!PF || more)) dma_next();
       if (live) {
         const char* st = smem + (q & 1) * G::STG;
         const char* st2 = st + G::W1B;
@@ -537,6 +590,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
         });
         store16(raa, lda, c, 1, av);
         __builtin_amdgcn_sched_barrier(0);
+        if (late_dma) dma_next();
         const f32x16 d1 = da_w(st2, 1, [&](int k) {
 #pragma unroll
           for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g0[i] *= d0[i];
@@ -554,11 +608,14 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
 #pragma unroll
         for (int i = 0; i < 16; ++i) g1[i] *= d1[i];
         store16(rda, ldda, c, 1, g1);
+      } else if (late_dma) {
+        dma_next();
       }
       ++q;
     };
     for (int c = 0; c + 1 < nch; ++c) chunk(c, IC<0>{});
     chunk(nch - 1, IC<1>{});
+    live_prev = live;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
