@@ -254,11 +254,12 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   };
   // pre^T tile 1 (12 MFMAs) with the GELU of tile 0 (`p0` + bias -> g) spread over its segments
   auto s1_act = [&](const char* st, const f32x16& p0, f32x16 p1, float (&g)[16]) {
-    bf16x8 wa = *(const bf16x8*)(st + off1[0] + 32 * (2 * D));
+    auto rd = [&](int k) { return *(const bf16x8*)(st + off1[k & 3] + 32 * (2 * D) + 128 * (k >> 2)); };
+    bf16x8 wr[3] = {rd(0), rd(1), rd(1)};  // fragments two MFMAs ahead (LDS latency > one segment)
 #pragma unroll
     for (int k = 0; k < G::KS1; ++k) {
-      const bf16x8 cur = wa;
-      if (k + 1 < G::KS1) wa = *(const bf16x8*)(st + off1[(k + 1) & 3] + 32 * (2 * D) + 128 * ((k + 1) >> 2));
+      const bf16x8 cur = wr[k % 3];
+      if (k + 2 < G::KS1) wr[(k + 2) % 3] = rd(k + 2);
       p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, xf[k]), p1, 0, 0, 0);
 #pragma unroll
       for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g[i] = gelu_sp(p0[i]);
@@ -270,15 +271,16 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   // (`pn` + bias -> g) spread over the segments
   auto s2_act = [&](const char* st2, int t, const u32x4v& f0, const u32x4v& f1, f32x16 (&acc)[G::NT],
                     const f32x16* pn, float (&g)[16]) {
-    bf16x8 wb = *(const bf16x8*)(st2 + off2[(2 * t) & 3]);
+    auto rd = [&](int k) {
+      const int s1 = 2 * t + k / G::NT, T1 = k % G::NT;
+      return *(const bf16x8*)(st2 + off2[s1 & 3] + 32 * T1 * 128);
+    };
+    bf16x8 wr[3] = {rd(0), rd(1), rd(1)};
 #pragma unroll
     for (int k = 0; k < 2 * G::NT; ++k) {
       const int sk = 2 * t + k / G::NT, T = k % G::NT;
-      const bf16x8 cur = wb;
-      if (k + 1 < 2 * G::NT) {
-        const int s1 = 2 * t + (k + 1) / G::NT, T1 = (k + 1) % G::NT;
-        wb = *(const bf16x8*)(st2 + off2[s1 & 3] + 32 * T1 * 128);
-      }
+      const bf16x8 cur = wr[k % 3];
+      if (k + 2 < 2 * G::NT) wr[(k + 2) % 3] = rd(k + 2);
       acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, sk & 1 ? f1 : f0), acc[T], 0, 0, 0);
       if (pn) {
 #pragma unroll
@@ -488,11 +490,12 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
   // the two 12-MFMA products of a chunk, each MFMA in a pinned segment with work(k) beside it
   // (see mlp_seg_lo): pre^T tile t = W1_c h2^T, da^T tile t = W2_c^T dx'^T (transposed A reads)
   auto s1_w = [&](const char* st, int t, f32x16 acc, auto&& work) {
-    bf16x8 wa = *(const bf16x8*)(st + off1[0] + 32 * t * (2 * D));
+    auto rd = [&](int k) { return *(const bf16x8*)(st + off1[k & 3] + 32 * t * (2 * D) + 128 * (k >> 2)); };
+    bf16x8 wr[3] = {rd(0), rd(1), rd(1)};  // fragments two MFMAs ahead
 #pragma unroll
     for (int k = 0; k < G::KS1; ++k) {
-      const bf16x8 cur = wa;
-      if (k + 1 < G::KS1) wa = *(const bf16x8*)(st + off1[(k + 1) & 3] + 32 * t * (2 * D) + 128 * ((k + 1) >> 2));
+      const bf16x8 cur = wr[k % 3];
+      if (k + 2 < G::KS1) wr[(k + 2) % 3] = rd(k + 2);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, xf[k]), acc, 0, 0, 0);
       work(k);
       __builtin_amdgcn_sched_barrier(0);
@@ -514,11 +517,11 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
   };
   auto da_w = [&](const char* st2, int t, auto&& work) {
     f32x16 acc = f32x16{};
-    bf16x8 wa = trw(st2, t, 0);
+    bf16x8 wr[3] = {trw(st2, t, 0), trw(st2, t, 1), trw(st2, t, 1)};
 #pragma unroll
     for (int k = 0; k < G::KS1; ++k) {
-      const bf16x8 cur = wa;
-      if (k + 1 < G::KS1) wa = trw(st2, t, k + 1);
+      const bf16x8 cur = wr[k % 3];
+      if (k + 2 < G::KS1) wr[(k + 2) % 3] = trw(st2, t, k + 2);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, yf[k]), acc, 0, 0, 0);
       work(k);
       __builtin_amdgcn_sched_barrier(0);
