@@ -14,7 +14,8 @@ from vspike import build  # noqa: E402
 
 
 def main(variant, defines, srcs):
-    build.build(verbose=False)  # the product objects are current
+    if not os.environ.get("VB_NO_PRODUCT"):  # (VB_NO_PRODUCT=1: leave libvspike.so alone, e.g. while a
+        build.build(verbose=False)           # GPU call that ships it is pending)
     vdir = os.path.join(build.BUILD_DIR, variant)
     os.makedirs(vdir, exist_ok=True)
     redo = {os.path.splitext(s)[0] + ".o" for s in srcs} | {"runtime.o"}

@@ -199,6 +199,14 @@ template <int N>
 __device__ __forceinline__ void mlp_vmcnt_le() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
+#ifdef VS_MLP_STAMP
+// Diagnostic build only (-DVS_MLP_STAMP, scripts/stamp_mlp.py): per wave of the last forward launch
+// {total, chunk-start wait (vmcnt + barrier), epilogue, chunks} in shader-clock cycles.
+__device__ unsigned long long g_mlp_stamp[4 * 4096];
+#define MLP_CLK() __builtin_amdgcn_s_memtime()
+#else
+#define MLP_CLK() 0ull
+#endif
 template <int D, bool LNF>
 __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t* __restrict__ h2, int64_t ldh,
                                                                     const bf16_t* __restrict__ w1,
@@ -319,6 +327,8 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   // waits for the DMA only (vmcnt(N) with N = the ops issued after it), not for those.
   constexpr int kNX = G::KS1, kNS = 4 * G::NT + (LNF ? 2 * G::NT + 2 : 0), kNY = 4 * G::NT;
   bool live_prev = false;
+  unsigned long long t_wait = 0, t_epi = 0, n_chunks = 0;
+  const unsigned long long t_begin = MLP_CLK();
   for (int64_t r = 0; r * Gs * kMlpWaves + blockIdx.x < nb; ++r) {
     const bool more = (r + 1) * Gs * kMlpWaves + blockIdx.x < nb;
     const bool live = blk(r) < nb;  // wave-uniform
@@ -326,10 +336,13 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
     // last chunk of a round (PF) also prefetches the next round's h2 fragments
     auto chunk = [&](int c, auto pfc) {
       constexpr bool PF = decltype(pfc)::value;
+      const unsigned long long cw = MLP_CLK();
       if (c == 0 && live_prev && live) mlp_vmcnt_le<kNX + kNS + kNY>();
       else if (c == 0 && live_prev) mlp_vmcnt_le<kNX + kNS>();
       else mlp_vmcnt_le<0>();
       __syncthreads();
+      t_wait += MLP_CLK() - cw;
+      ++n_chunks;
       // chunk 0 issues the next chunk's DMA after its first W2 tile: hipcc cannot see the asm DMA, and
       // its wait for the y loads (the accumulators' first use, in that tile) would drain it too
       const bool late_dma = !PF && c == 0;
@@ -366,6 +379,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
       live_prev = false;
       continue;
     }
+    const unsigned long long ce = MLP_CLK();
     // epilogue: x' = acc + b2 (acc started from y)
     const int64_t row0 = blk(r) * 32;
     const auto rxo = mlp_rsrc(xo + row0 * ldx, M - row0, ldx, 4);
@@ -427,8 +441,23 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
     }
     if (more && blk(r + 1) < nb) load_y(r + 1);
     live_prev = live;
+    t_epi += MLP_CLK() - ce;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
+#ifdef VS_MLP_STAMP
+  if (lane == 0 && !LNF) {
+    unsigned long long* st = g_mlp_stamp + 4 * (blockIdx.x * kMlpWaves + wave);
+    st[0] = MLP_CLK() - t_begin;
+    st[1] = t_wait;
+    st[2] = t_epi;
+    st[3] = n_chunks;
+  }
+#else
+  (void)t_wait;
+  (void)t_epi;
+  (void)n_chunks;
+  (void)t_begin;
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -716,3 +745,10 @@ extern "C" int vs_mlp_bwd_da(int64_t M, int64_t D, int64_t F, const void* h2, in
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
+
+#ifdef VS_MLP_STAMP
+extern "C" int vs_dbg_mlp_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vs::g_mlp_stamp), (size_t)n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
