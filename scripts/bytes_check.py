@@ -33,6 +33,8 @@ BWD = [("dx_mlp", r"mlp_bwd_da_kernel"), ("dw_fc2", r"gemm_dw_kernel"), ("dw_fc1
        ("dx_fc1", r"gemm_bf16_slab_kernel"), ("dw_proj", r"gemm_dw_kernel"), ("dx_proj", r"gemm_bf16_slab_kernel"),
        ("attn_bwd", r"attn_rowprep_kernel"), ("dw_qkv", r"gemm_dw_kernel"), ("dx_qkv", r"gemm_bf16_slab_kernel")]
 
+ONLY = {"fwd_mlp": r"mlp_fwd_kernel"}
+
 
 def run(out):
     sys.path[:0] = [os.path.join(ROOT, "video-spike_amd"), ROOT]
@@ -102,6 +104,10 @@ def parse(pmc_dir, charged_json, out):
                                   nxt is not None and not re.search(nxt, names[j])):
             j += 1
         for k in range(i, j):
+            # the block's last forward class is followed by the head's forward (casts, GEMMs, loss)
+            # before the backward starts: count only the class's own kernel there
+            if cls in ONLY and not re.search(ONLY[cls], names[k]):
+                continue
             res[cls] += nbytes[k]
             kern[cls].append(names[k].split("(")[0])
         i = j
