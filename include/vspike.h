@@ -454,7 +454,8 @@ const char* vs_shard_last_error(void);
 #define VS_TIMER_DW_QKV   19   /* dWqkv += dqkv^T h1 (+ dbqkv) */
 #define VS_TIMER_FWD_MLP  20   /* the fused MLP forward (vs_mlp_fwd, a_pre == NULL)   (mv:370-399) */
 #define VS_TIMER_DX_MLP   21   /* the fused MLP backward's GELU' product (vs_mlp_bwd_da) */
-#define VS_TIMER_COUNT    22
+#define VS_TIMER_FP8_QUANT 22  /* the MX-FP8 forward's operand quantisation (vs_quant_mxfp8 of A and W) */
+#define VS_TIMER_COUNT    23
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
 int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */

@@ -430,11 +430,19 @@ def test_kernel_timers_per_product():
         got = {name: ops.timing_collect(t, with_bytes=True) for t, name in enumerate(L.TIMER_NAMES)}
     finally:
         ops.timing_enable(0)
-    for name in L.TIMER_NAMES[8:] + ("attn_fwd", "attn_bwd", "ln_fwd", "ln_bwd"):
+    Lh = cfg.num_hidden_layers
+    fused = m._mlp_fused(2)          # D = 192 bf16: the fused MLP kernels replace fc1 / fc2 fwd and dx_fc2
+    unused = {"fwd_fc1", "fwd_fc2", "dx_fc2"} if fused else {"fwd_mlp", "dx_mlp"}
+    unused |= {"fp8_quant"}          # compute_dtype fp8 only
+    for name in L.TIMER_NAMES[8:] + ("attn_fwd", "attn_bwd", "ln_bwd"):
         n, ms, nbytes = got[name]
-        want = 2 * cfg.num_hidden_layers if name.startswith("ln_") else cfg.num_hidden_layers
+        want = 0 if name in unused else (2 * Lh if name.startswith("ln_") else Lh)
         assert n == want, (name, n)
-        assert ms > 0 and nbytes > 0, (name, ms, nbytes)
+        if want:
+            assert ms > 0 and nbytes > 0, (name, ms, nbytes)
+    # LayerNorm forwards: LN1 + LN2 per layer, fewer where the fused MLP epilogue runs the next
+    # block's LN1 (vs_mlp_fwd_ln) or the proj product runs LN2 (vs_gemm_ln_fwd)
+    assert 1 <= got["ln_fwd"][0] <= 2 * Lh, got["ln_fwd"]
     # outside the block: patch-embed fwd + head (fwd, dX) in "gemm", patch dW + head dW in "gemm_dw"
     assert 0 < got["gemm"][0] <= 6 and 0 < got["gemm_dw"][0] <= 4, (got["gemm"], got["gemm_dw"])
 

@@ -313,6 +313,13 @@ __device__ __forceinline__ float pair_sum(float v) {
 }
 
 
+// VS_ATTN_DIAG (diagnostic builds only): bit 0 = the forward streams only its first two K/V tiles,
+// bit 1 = the backward (both passes) only its first two Q/dO or K/V slices: the rest of the tiles are
+// computed on stale LDS data, which times the kernels without their LDS-DMA fill (results WRONG)
+#ifndef VS_ATTN_DIAG
+#define VS_ATTN_DIAG 0
+#endif
+
 #ifdef VS_STAMP
 // Diagnostic build only (-DVS_STAMP): per wave {start, end} realtime ticks (100 MHz), HW ids, and
 // shader-clock cycles accumulated in the forward's barrier and vmcnt waits; read back with
@@ -599,7 +606,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt+1 landed
           __syncthreads();                                  // ... every wave's; all reads of `cur` retired
 #endif
-          if (kt + 2 < nkt) load_tile(kt + 2, cur);
+          if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
           ka = kread(nxt, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -607,7 +614,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
       } else if (kt + 1 < nkt) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (kt + 2 < nkt) load_tile(kt + 2, cur);
+        if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
       }
     };
     for (int kt = 0; kt < nkt; kt += 2) {
@@ -895,7 +902,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
     constexpr int BUF = decltype(bufc)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of slice it landed
     __syncthreads();                                  // ... and every wave's; buffer BUF^1 is free
-    if (it + 1 < nit) load_stage(it + 1, BUF ? stg0 : stg1);
+    if (it + 1 < nit && !((VS_ATTN_DIAG & 2) && it >= 1)) load_stage(it + 1, BUF ? stg0 : stg1);
     const char* st = BUF ? stg1 : stg0;
     slice(st, 0);
     __builtin_amdgcn_sched_barrier(0);  // keep the two slices' S/dP accumulators from overlapping
@@ -1045,7 +1052,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
     constexpr int BUF = decltype(bufc)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kt + 1 < nkt) load_tile(kt + 1, BUF ? kv0 : kv1);
+    if (kt + 1 < nkt && !((VS_ATTN_DIAG & 2) && kt >= 1)) load_tile(kt + 1, BUF ? kv0 : kv1);
     const char* cur = BUF ? kv1 : kv0;
     sub(cur, 0, kt * 64);
     if (kt * 64 + 32 < N) sub(cur, 1, kt * 64 + 32);

@@ -12,7 +12,7 @@
 // GEMM (vs_gemm_mxfp8): C[M, N] = sum_k A[m, k] B[n, k] (both k-contiguous fp8, nn.Linear layout for
 // B) with scales sa[M][K/32], sb[N][K/32]; the f32 tile then runs the same epilogue as vs_gemm
 // (bias, GELU + stored gelu', residual, bf16 / f32 output).  256 x 128 tile, 8 waves (4 x 2, 64 x 64
-// per wave: 2 x 2 tiles of 32 x 32), 128-deep k-steps (two 64-deep MFMA k-steps), 2-stage LDS-DMA
+// per wave: 2 x 2 tiles of 32 x 32), 128-deep k-steps (two 64-deep MFMA k-steps), 3-stage LDS-DMA
 // ring of 49.5 KB stages (fp8 rows of 128 B with a 16-B chunk XOR of (row >> 1) & 7; one dword of
 // scales per row); operand layout of the 32x32x64 f8 MFMA: lane (r = lane & 31, h = lane >> 5)
 // holds row r, k = 16 h .. 16 h + 15 in VGPRs 0-3 and k = 32 + 16 h .. in VGPRs 4-7 (32 bytes), and
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mxfp8_kernel(const uint8_t* __res
                                                             const uint8_t* __restrict__ sb, int64_t ldsb, int64_t K,
                                                             GridMap g, EpiParams e) {
   constexpr int LDT = kFp8BN + 4;
-  constexpr int SMEM = 2 * kFp8Stage > (kFp8BM / 2) * LDT * 4 ? 2 * kFp8Stage : (kFp8BM / 2) * LDT * 4;
+  constexpr int SMEM = 3 * kFp8Stage > (kFp8BM / 2) * LDT * 4 ? 3 * kFp8Stage : (kFp8BM / 2) * LDT * 4;  // 148.5 KB
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   int nt, mt, split;
   map_block(g, nt, mt, split);
@@ -208,19 +208,28 @@ __global__ __launch_bounds__(512, 1) void gemm_mxfp8_kernel(const uint8_t* __res
                                                                       scb[j]);
     }
   };
+  // 3-stage ring with one step in flight across each barrier (as gemm_bf16_big_kernel): a wave's
+  // pieces per step are 4 (A) + 2 (B) + 1 scale dword piece for waves 0-5
   auto step = [&](int t, auto sc) {
-    constexpr int S = decltype(sc)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of step t landed
+    constexpr int S = decltype(sc)::value;  // == t % 3
+    if (t + 1 < nk) {
+      if (wid < 6) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                      // every wave's; step t-1's stage is free
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < nk) issue(t + 1, smem + (1 - S) * kFp8Stage);
+    if (t + 2 < nk) issue(t + 2, smem + ((S + 2) % 3) * kFp8Stage);
     compute(smem + S * kFp8Stage);
   };
   issue(0, smem);
-  for (int t = 0; t < nk; t += 2) {
+  if (nk > 1) issue(1, smem + kFp8Stage);
+  for (int t = 0; t < nk; t += 3) {
     step(t, IC<0>{});
     if (t + 1 < nk) step(t + 1, IC<1>{});
+    if (t + 2 < nk) step(t + 2, IC<2>{});
   }
   // epilogue: the f32 tile staged in two 128-row halves, 8-column groups per thread (vs_gemm's epilogue)
   float* stg = (float*)smem;

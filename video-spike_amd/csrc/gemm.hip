@@ -1512,7 +1512,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
   using OB = OperandBf16<128, BKC>;
   constexpr int STAGE = OA::BYTES + OB::BYTES;  // 48 KB
   constexpr int LDT = 128 + 4;
-  constexpr int SMEM = CMax<2 * STAGE, 128 * LDT * 4>::v;
+  constexpr int SMEM = CMax<3 * STAGE, 128 * LDT * 4>::v;  // 3-stage ring: 144 KB
+  // DMA pieces (1 KB wave-instructions) one wave issues per stage: the counted wait of a step
+  constexpr int PPW = OA::PIECES / 8 + OB::PIECES / 8;
+  static_assert(PPW == 6, "vmcnt below assumes 6 pieces per wave and stage");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   int nt, mt, split;
@@ -1546,19 +1549,26 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
+  // 3-stage ring, two steps in flight (guide §5 "Pipelining across barriers": a stage stays in flight
+  // across the barrier): step t waits for ITS pieces only (vmcnt(6) leaves step t+1's 6 in flight),
+  // then the raw barrier makes every wave's pieces of t visible and every wave's reads of t-1 done,
+  // so step t+2 may refill t-1's stage.
   auto step = [&](int t, auto sc) {
-    constexpr int S = decltype(sc)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of step t landed
+    constexpr int S = decltype(sc)::value;  // == t % 3
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                       // every wave's; step t-1's stage is free
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 1 < nk) issue(t + 1, smem + (1 - S) * STAGE);
+    if (t + 2 < nk) issue(t + 2, smem + ((S + 2) % 3) * STAGE);
     compute(smem + S * STAGE);
   };
   issue(0, smem);
-  for (int t = 0; t < nk; t += 2) {
+  if (nk > 1) issue(1, smem + STAGE);
+  for (int t = 0; t < nk; t += 3) {
     step(t, IC<0>{});
     if (t + 1 < nk) step(t + 1, IC<1>{});
+    if (t + 2 < nk) step(t + 2, IC<2>{});
   }
   float* stg = (float*)smem;
   constexpr int CPR = 128 / 8;  // 8-column groups per row: 32 rows per pass of 512 threads

@@ -89,8 +89,11 @@ static Fp8Ws fp8_ws(const vs_vit_layer* L) {
 // the block-scaled GEMM with the given epilogue (the epilogue fields of g; g.a / g.b are replaced)
 static int fp8_product(const vs_vit_layer* L, vs_gemm_desc g, void* stream) {
   const Fp8Ws w = fp8_ws(L);
-  VS_CALL(vs_quant_mxfp8(VS_BF16, g.M, g.K, g.a, g.lda, w.aq, g.K, w.as, g.K / 32, stream));
-  VS_CALL(vs_quant_mxfp8(VS_BF16, g.N, g.K, g.b, g.ldb, w.wq, g.K, w.ws, g.K / 32, stream));
+  {
+    TimerTag tag(VS_TIMER_FP8_QUANT);  // the product's timer then holds the GEMM alone
+    VS_CALL(vs_quant_mxfp8(VS_BF16, g.M, g.K, g.a, g.lda, w.aq, g.K, w.as, g.K / 32, stream));
+    VS_CALL(vs_quant_mxfp8(VS_BF16, g.N, g.K, g.b, g.ldb, w.wq, g.K, w.ws, g.K / 32, stream));
+  }
   g.dtype = VS_FP8;
   g.a = w.aq; g.lda = g.K;
   g.b = w.wq; g.ldb = g.K;

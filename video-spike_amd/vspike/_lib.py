@@ -26,7 +26,9 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
                "fwd_qkv", "fwd_proj", "fwd_fc1", "fwd_fc2", "dx_fc2", "dx_fc1", "dx_proj", "dx_qkv",
                "dw_fc2", "dw_fc1", "dw_proj", "dw_qkv",
                # the fused MLP (a_pre == NULL in vs_vit_layer): forward, backward GELU' product
-               "fwd_mlp", "dx_mlp")
+               "fwd_mlp", "dx_mlp",
+               # the MX-FP8 forward's operand quantisation (compute_dtype fp8)
+               "fp8_quant")
 
 # vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
