@@ -72,6 +72,55 @@ __device__ __forceinline__ float gelu_sp_both(float x, float& grad) {
   return x * sg;
 }
 
+// The same GELU over a 16-value tile, spread over the 12 MFMA segments of a product by STAGE: in
+// segment k every value advances one step of the chain, so a segment carries 16 independent
+// operations instead of the 1-2 dependent chains of 9 that left the wave waiting on VALU latency
+// (stages 5-6 / 8-9 split the exp / rcp so no segment holds 16 transcendentals).
+struct GeluStages {
+  float t[16], p[16];
+};
+__device__ __forceinline__ void gelu_stage(int k, const f32x16& x, GeluStages& s, float (&g)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (k == 0) s.t[i] = x[i] * x[i];
+    if (k == 1) s.t[i] = fminf(s.t[i], 81.f);
+    if (k == 2) s.p[i] = fmaf(s.t[i], -kGk5 * kGl2e, -kGk3 * kGl2e);
+    if (k == 3) s.p[i] = fmaf(s.t[i], s.p[i], -kGk1 * kGl2e);
+    if (k == 4) s.p[i] = x[i] * s.p[i];
+    if ((k == 5 && i < 8) || (k == 6 && i >= 8)) s.p[i] = __builtin_amdgcn_exp2f(s.p[i]);
+    if (k == 7) s.p[i] = 1.f + s.p[i];
+    if ((k == 8 && i < 8) || (k == 9 && i >= 8)) s.p[i] = __builtin_amdgcn_rcpf(s.p[i]);
+    if (k == 10) g[i] = x[i] * s.p[i];
+  }
+}
+
+// ... and gelu with its derivative (the backward), same staging: a = x s, grad = s + x s (1 - s) u'(x)
+__device__ __forceinline__ void gelu_both_stage(int k, const f32x16& x, GeluStages& s, float (&a)[16],
+                                                float (&grad)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (k == 0) s.t[i] = x[i] * x[i];
+    if (k == 1) s.t[i] = fminf(s.t[i], 81.f);
+    if (k == 2) {
+      s.p[i] = fmaf(s.t[i], -kGk5 * kGl2e, -kGk3 * kGl2e);
+      grad[i] = fmaf(s.t[i], 5.f * kGk5, 3.f * kGk3);
+    }
+    if (k == 3) {
+      s.p[i] = fmaf(s.t[i], s.p[i], -kGk1 * kGl2e);
+      grad[i] = fmaf(s.t[i], grad[i], kGk1);  // u'(x), kept in grad until stage 11
+    }
+    if (k == 4) s.p[i] = x[i] * s.p[i];
+    if ((k == 5 && i < 8) || (k == 6 && i >= 8)) s.p[i] = __builtin_amdgcn_exp2f(s.p[i]);
+    if (k == 7) s.p[i] = 1.f + s.p[i];
+    if ((k == 8 && i < 8) || (k == 9 && i >= 8)) s.p[i] = __builtin_amdgcn_rcpf(s.p[i]);
+    if (k == 10) {
+      a[i] = x[i] * s.p[i];
+      s.t[i] = fmaf(-s.p[i], s.p[i], s.p[i]);  // s (1 - s)
+    }
+    if (k == 11) grad[i] = fmaf(x[i] * s.t[i], grad[i], s.p[i]);
+  }
+}
+
 __device__ __forceinline__ u32x4v mlp_pack8(const float* v) {
   u32x4v u;
 #pragma unroll
@@ -262,6 +311,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   };
   // pre^T tile 1 (12 MFMAs) with the GELU of tile 0 (`p0` + bias -> g) spread over its segments
   auto s1_act = [&](const char* st, const f32x16& p0, f32x16 p1, float (&g)[16]) {
+    GeluStages gs;
     auto rd = [&](int k) { return *(const bf16x8*)(st + off1[k & 3] + 32 * (2 * D) + 128 * (k >> 2)); };
     bf16x8 wr[3] = {rd(0), rd(1), rd(1)};  // fragments two MFMAs ahead (LDS latency > one segment)
 #pragma unroll
@@ -269,8 +319,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
       const bf16x8 cur = wr[k % 3];
       if (k + 2 < G::KS1) wr[(k + 2) % 3] = rd(k + 2);
       p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, xf[k]), p1, 0, 0, 0);
-#pragma unroll
-      for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g[i] = gelu_sp(p0[i]);
+      gelu_stage(k, p0, gs, g);
       __builtin_amdgcn_sched_barrier(0);
     }
     return p1;
@@ -279,6 +328,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   // (`pn` + bias -> g) spread over the segments
   auto s2_act = [&](const char* st2, int t, const u32x4v& f0, const u32x4v& f1, f32x16 (&acc)[G::NT],
                     const f32x16* pn, float (&g)[16]) {
+    GeluStages gs;
     auto rd = [&](int k) {
       const int s1 = 2 * t + k / G::NT, T1 = k % G::NT;
       return *(const bf16x8*)(st2 + off2[s1 & 3] + 32 * T1 * 128);
@@ -290,10 +340,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
       const bf16x8 cur = wr[k % 3];
       if (k + 2 < 2 * G::NT) wr[(k + 2) % 3] = rd(k + 2);
       acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, __builtin_bit_cast(bf16x8, sk & 1 ? f1 : f0), acc[T], 0, 0, 0);
-      if (pn) {
-#pragma unroll
-        for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) g[i] = gelu_sp((*pn)[i]);
-      }
+      if (pn) gelu_stage(k, *pn, gs, g);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -601,10 +648,8 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
         // S1(t0) | S1(t1) + act(t0) | da(t0) + act(t1) | da(t1) + da-product(t0) | da-product(t1)
         float av[16], g0[16], g1[16];  // g0 / g1 become the da values in place
         const f32x16 p0 = s1_w(st, 0, mlp_bias_acc(b1s, c, 0, h), [&](int) {});
-        const f32x16 p1 = s1_w(st, 1, mlp_bias_acc(b1s, c, 1, h), [&](int k) {
-#pragma unroll
-          for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) av[i] = gelu_sp_both(p0[i], g0[i]);
-        });
+        GeluStages gs;
+        const f32x16 p1 = s1_w(st, 1, mlp_bias_acc(b1s, c, 1, h), [&](int k) { gelu_both_stage(k, p0, gs, av, g0); });
         store16(raa, lda, c, 0, av);
         if constexpr (PF) {  // h2 fragments are dead after the last chunk's W1 products
           if (more) {
@@ -616,10 +661,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        const f32x16 d0 = da_w(st2, 0, [&](int k) {
-#pragma unroll
-          for (int i = mlp_seg_lo(k); i < mlp_seg_lo(k + 1); ++i) av[i] = gelu_sp_both(p1[i], g1[i]);
-        });
+        const f32x16 d0 = da_w(st2, 0, [&](int k) { gelu_both_stage(k, p1, gs, av, g1); });
         store16(raa, lda, c, 1, av);
         __builtin_amdgcn_sched_barrier(0);
         if (late_dma) dma_next();
