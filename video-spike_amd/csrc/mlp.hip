@@ -349,6 +349,10 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
   // land), so the epilogue only adds b2 and stores.  Lane (token rr, half h) holds d = 32 T + 16 j2 +
   // 8 h .. + 7 in acc[T][8 j2 ..].
   f32x16 acc[G::NT];
+  // per-lane byte bases of the y / x' / h rows (the (T, j2) group adds an immediate: 24 precomputed
+  // offsets per lane were spilled around the round loop)
+  const uint32_t yb = (uint32_t)((rr * ldy + 8 * h) * 4), xb = (uint32_t)((rr * ldx + 8 * h) * 4);
+  const uint32_t hb = LNF ? (uint32_t)((rr * ln.ldh + 8 * h) * 2) : 0u;
   auto load_y = [&](int64_t r) {
     const int64_t row0 = blk(r) * 32;
     const auto ry = mlp_rsrc(y + row0 * ldy, M - row0, ldy, 4);
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
     for (int T = 0; T < G::NT; ++T)
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2) {
-        const uint32_t oy = (uint32_t)((rr * ldy + 32 * T + 16 * j2 + 8 * h) * 4);
+        const uint32_t oy = yb + 4 * (32 * T + 16 * j2);  // lane base + an immediate
         const f32x4 y0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy, 0, 0));
         const f32x4 y1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy + 16, 0, 0));
 #pragma unroll
@@ -435,7 +439,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
 #pragma unroll
       for (int j2 = 0; j2 < 2; ++j2) {
         const int d0 = 32 * T + 16 * j2 + 8 * h;
-        const uint32_t ox = (uint32_t)((rr * ldx + d0) * 4);
+        const uint32_t ox = xb + 4 * (32 * T + 16 * j2);
         const f32x4 c0 = *(const f32x4*)(b2s + d0), c1 = *(const f32x4*)(b2s + d0 + 4);
         f32x4 r0, r1;
 #pragma unroll
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_fwd_kernel(const bf16_t
           float v[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = acc[T][8 * j2 + j] * rs * lngs[d0 + j] + lnbs[d0 + j];
-          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(v), rh, (uint32_t)((rr * ln.ldh + d0) * 2), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(mlp_pack8(v), rh, hb + 2 * (32 * T + 16 * j2), 0, 0);
         }
       if (h == 0 && row0 + rr < M) {
         ln.mean[row0 + rr] = mu;
