@@ -313,6 +313,19 @@ __device__ __forceinline__ float pair_sum(float v) {
 }
 
 
+// VS_ATTN_PRIO (diagnostic builds): every 32x32x16 MFMA issued at raised wave priority
+// (s_setprio 1 / 0 around it), so a wave with an MFMA ready wins the issue port over VALU work
+__device__ __forceinline__ f32x16 mfma32p(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+#ifdef VS_ATTN_PRIO
+  __builtin_amdgcn_s_setprio(1);
+  const f32x16 r = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+  return r;
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
 // VS_ATTN_DIAG (diagnostic builds only): bit 0 = the forward streams only its first two K/V tiles,
 // bit 1 = the backward (both passes) only its first two Q/dO or K/V slices: the rest of the tiles are
 // computed on stale LDS data, which times the kernels without their LDS-DMA fill (results WRONG)
@@ -480,7 +493,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-        oacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.v[2 * s + dt], s == 0 ? pa : pb, oacc[dt], 0, 0, 0);
+        oacc[dt] = mfma32p(f.v[2 * s + dt], s == 0 ? pa : pb, oacc[dt]);
   };
 
   // Softmax of one 32-key block.  acc = log2-domain scores s (Q pre-scaled by c; the MFMA chain
@@ -562,12 +575,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
       const char* nxt = BUF ? smem0 : smem1;
       bf16x8 b0, b1;
       if (active) {
-        f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka.k[0], qf[0], zero16, 0, 0, 0);
+        f32x16 sa = mfma32p(ka.k[0], qf[0], zero16);
         __builtin_amdgcn_sched_barrier(0);
         const VFrag va = vread(cur, 0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int s = 1; s < 4; ++s) sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka.k[s], qf[s], sa, 0, 0, 0);
+        for (int s = 1; s < 4; ++s) sa = mfma32p(ka.k[s], qf[s], sa);
         const KFrag kb = kread(cur, 1);
         __builtin_amdgcn_sched_barrier(0);
         bf16x8 a0, a1;
@@ -575,9 +588,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
         f32x16 sb;
         VFrag vb;
         if constexpr (SW) {
-          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
+          sb = mfma32p(kb.k[0], qf[0], zero16);
 #pragma unroll
-          for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+          for (int s = 1; s < 4; ++s) sb = mfma32p(kb.k[s], qf[s], sb);
           __builtin_amdgcn_sched_barrier(0);
           vb = vread(cur, 1);
           __builtin_amdgcn_sched_barrier(0);
@@ -585,12 +598,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
           __builtin_amdgcn_sched_barrier(0);
         } else {
           pv(va, a0, a1);
-          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[0], qf[0], zero16, 0, 0, 0);
+          sb = mfma32p(kb.k[0], qf[0], zero16);
           __builtin_amdgcn_sched_barrier(0);
           vb = vread(cur, 1);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int s = 1; s < 4; ++s) sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb.k[s], qf[s], sb, 0, 0, 0);
+          for (int s = 1; s < 4; ++s) sb = mfma32p(kb.k[s], qf[s], sb);
         }
         softmax(safec, sb, kt * 64 + 32, false, b0, b1);
         __builtin_amdgcn_sched_barrier(0);
@@ -852,7 +865,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(sQ + sub * 4096 + roff[s]), kf[s], acc, 0, 0, 0);
+      acc = mfma32p(*(const bf16x8*)(sQ + sub * 4096 + roff[s]), kf[s], acc);
     bf16x8 pbs[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -864,7 +877,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];
-        dvacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sD, o0, o1), pb, dvacc[dt], 0, 0, 0);
+        dvacc[dt] = mfma32p(tr_pair(sD, o0, o1), pb, dvacc[dt]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -875,7 +888,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)(sD + sub * 4096 + roff[s]), vf[s], acc, 0, 0, 0);
+      acc = mfma32p(*(const bf16x8*)(sD + sub * 4096 + roff[s]), vf[s], acc);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       float ds[8];  // dS = P * (dP - delta) from the bf16 P of the dV product (carried packed: 8 VGPRs)
@@ -890,7 +903,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];
-        dkacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_pair(sQ, o0, o1), db, dkacc[dt], 0, 0, 0);
+        dkacc[dt] = mfma32p(tr_pair(sQ, o0, o1), db, dkacc[dt]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1023,8 +1036,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
     for (int s = 0; s < 4; ++s) {
       const bf16x8 ka = *(const bf16x8*)(sK + kb * 4096 + roff[s]);
       const bf16x8 va = *(const bf16x8*)(sV + kb * 4096 + roff[s]);
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
-      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dpacc, 0, 0, 0);
+      sacc = mfma32p(ka, qf[s], sacc);
+      dpacc = mfma32p(va, df[s], dpacc);
     }
     if (key0 + 32 > N) {
 #pragma unroll
@@ -1041,7 +1054,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
       for (int dt = 0; dt < 2; ++dt) {
         const int o = kb * 4096 + s2 * 2048;
         const bf16x8 ka = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
-        dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, db, dqacc[dt], 0, 0, 0);
+        dqacc[dt] = mfma32p(ka, db, dqacc[dt]);
       }
     }
   };
@@ -1183,7 +1196,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_pp(char* __restrict__ stg0, char* 
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = pack8f(pv + 8 * s2);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 * s2 + dt], pb, acc[dt], 0, 0, 0);
+      for (int dt = 0; dt < 2; ++dt) acc[dt] = mfma32p(f[2 * s2 + dt], pb, acc[dt]);
     }
   };
   auto slice = [&](const char* st) {
@@ -1200,8 +1213,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_pp(char* __restrict__ stg0, char* 
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {  // S(a), S(b): two independent chains, interleaved
-      xa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s], kf[s], xa, 0, 0, 0);
-      xb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], kf[s], xb, 0, 0, 0);
+      xa = mfma32p(fa[s], kf[s], xa);
+      xb = mfma32p(fb[s], kf[s], xb);
     }
     __builtin_amdgcn_sched_barrier(0);
     tr4(sD, 0, fa);  // dO(a)^T for dV(a)
@@ -1213,7 +1226,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_pp(char* __restrict__ stg0, char* 
     rowc(sE, 0, xa);
     mma_p(fa, pa, dvacc);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) xa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], vf[s], xa, 0, 0, 0);
+    for (int s = 0; s < 4; ++s) xa = mfma32p(fb[s], vf[s], xa);
     __builtin_amdgcn_sched_barrier(0);
     tr4(sD, 1, fa);  // dO(b)^T
     rows4(sD, 1, fb);  // dO(b) rows
@@ -1223,7 +1236,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_pp(char* __restrict__ stg0, char* 
     rowc(sE, 1, xb);
     mma_p(fa, pb, dvacc);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) xb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], vf[s], xb, 0, 0, 0);
+    for (int s = 0; s < 4; ++s) xb = mfma32p(fb[s], vf[s], xb);
     __builtin_amdgcn_sched_barrier(0);
     tr4(sQ, 0, fa);  // Q(a)^T, Q(b)^T for dK
     tr4(sQ, 1, fb);
@@ -1360,7 +1373,7 @@ __device__ __forceinline__ void attn_bwd_dq_pp(char* __restrict__ kv0, char* __r
       for (int r = 0; r < 8; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[8 * s2 + r]) * dpacc[8 * s2 + r];
       const bf16x8 db = pack8f(ds);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) dqacc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 * s2 + dt], db, dqacc[dt], 0, 0, 0);
+      for (int dt = 0; dt < 2; ++dt) dqacc[dt] = mfma32p(f[2 * s2 + dt], db, dqacc[dt]);
     }
   };
   // one 64-key tile: key blocks a (0..31) and b (32..63; keys past N masked to p = 0, so every tile
@@ -1382,13 +1395,13 @@ __device__ __forceinline__ void attn_bwd_dq_pp(char* __restrict__ kv0, char* __r
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[s], s == 0 ? sinit : sa, 0, 0, 0);
-      da = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], df[s], s == 0 ? dinit : da, 0, 0, 0);
+      sa = mfma32p(ka[s], qf[s], s == 0 ? sinit : sa);
+      da = mfma32p(va[s], df[s], s == 0 ? dinit : da);
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb_[s], qf[s], s == 0 ? sinit : sb, 0, 0, 0);
-      db = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb[s], df[s], s == 0 ? dinit : db, 0, 0, 0);
+      sb = mfma32p(kb_[s], qf[s], s == 0 ? sinit : sb);
+      db = mfma32p(vb[s], df[s], s == 0 ? dinit : db);
     }
     __builtin_amdgcn_sched_barrier(0);
     ktr4(sK, 0, ka);

@@ -1543,10 +1543,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
       for (int i = 0; i < 4; ++i) af[i] = OA::frag(sa, wr * 64 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = OB::frag(sb, wc * 64 + j * 16, kk, lane);
+#ifdef VS_GEMM_PRIO  // diagnostic builds: the MFMA cluster at raised wave priority
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#ifdef VS_GEMM_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   };
   // 3-stage ring, two steps in flight (guide §5 "Pipelining across barriers": a stage stays in flight
