@@ -33,6 +33,11 @@ constexpr int kMlpMaxF = 3072;
 
 __device__ __forceinline__ int mlp_swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 __device__ __forceinline__ int mlp_cpos(int c, int r) { return (c & ~7) | ((c & 7) ^ ((r >> 1) & 7)); }
+// chunk XOR key of the backward's W2 image (read only by ds_read_b64_tr_b16): a 32-lane group reads
+// rows d0 .. d0 + 3 (d0 % 4 == 0), 4 chunks of one half-row each, and rows d and d + 2 share banks
+// (256 B apart); bit 2 of the key = bit 1 of the row puts them in opposite half-rows (the (d >> 1) & 7
+// key mapped them onto the same chunks: 2-way conflicts, 30 % of the LDS cycles in the PMC)
+__device__ __forceinline__ int mlp_key_tr(int d) { return (((d >> 1) & 1) << 2) | ((d >> 2) & 3); }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base, int64_t rows_left, int64_t ld, int es) {
   const int64_t n = rows_left > 0 ? rows_left : 0;
@@ -160,7 +165,7 @@ __device__ __forceinline__ void mlp_dma_offsets(int wave, int lane, int64_t F, b
     const int P = 64 * (wave * G::DMA2 + k) + lane;
     const int p = P / 8, cp = P % 8;
     const int d = fwd_w2_perm ? 32 * (p >> 5) + mlp_swap23(p & 31) : p;
-    const int cl = cp ^ ((p >> 1) & 7);
+    const int cl = cp ^ (fwd_w2_perm ? (p >> 1) & 7 : mlp_key_tr(p));
     o2[k] = (uint32_t)(((int64_t)d * F + 8 * cl) * 2);
   }
 }
@@ -548,7 +553,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
     const int d = 16 * s + 8 * hh + 4 * e + qrow;  // image row (natural order)
     const int f = 32 * t + fq;                     // first column of the quad
     const int cl = f >> 3;
-    return d * 128 + 16 * (cl ^ ((d >> 1) & 7)) + 2 * (f & 7);
+    return d * 128 + 16 * (cl ^ mlp_key_tr(d)) + 2 * (f & 7);
   };
 
   uint32_t off1[4];
@@ -583,7 +588,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
     return acc;
   };
   typedef __attribute__((ext_vector_type(8))) short short8v;
-  // tr_addr(t, k, e) = trb[t][e] + 2048 k: the chunk XOR key (d >> 1) & 7 does not depend on k
+  // tr_addr(t, k, e) = trb[t][e] + 2048 k: the chunk XOR key mlp_key_tr(d) reads bits 1-3 of d = 16 k + ..., not k
   uint32_t trb[2][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
