@@ -772,7 +772,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
                                                    bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
                                                    float scale) {
   constexpr int QT = kBwdQT;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int nb128 = (N + 127) / 128, kb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
@@ -809,30 +809,34 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
 
   // LDS-DMA: wave w fills Q pieces 2w, 2w+1 and dO pieces 2w, 2w+1 (8 rows x 128 B each); lane L
   // loads the source chunk that belongs at position L & 7 of its row; waves 0 / 1 fill nlse2 / ndel.
+  // per-lane DMA source offsets of rows prow / prow + 8 of a Q / dO slice, computed once (SGPR-base +
+  // 32-bit-offset asm DMA: the per-slice 64-bit address arithmetic cost ~40 VALU per slice)
+  const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+  const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
+  const uint32_t gq0 = (uint32_t)(prow * 2 * ldq) + cq0, gq1 = (uint32_t)((prow + 8) * 2 * ldq) + cq1;
+  const uint32_t gd0 = (uint32_t)(prow * 2 * lddo) + cq0, gd1 = (uint32_t)((prow + 8) * 2 * lddo) + cq1;
   auto load_stage = [&](int it, char* dst) {
-    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;  // recomputed per stage: no live VGPRs
-    const uint32_t cq0 = (uint32_t)((ppos ^ swz_rt(prow)) << 4), cq1 = (uint32_t)((ppos ^ swz_rt(prow + 8)) << 4);
-    const uint32_t gq0 = (uint32_t)(prow * 2 * ldq) + cq0, gq1 = (uint32_t)((prow + 8) * 2 * ldq) + cq1;
-    const uint32_t gd0 = (uint32_t)(prow * 2 * lddo) + cq0, gd1 = (uint32_t)((prow + 8) * 2 * lddo) + cq1;
     const int q0 = it * 64;
     const char* qs = (const char*)(Qp + (int64_t)q0 * ldq);
     const char* ds = (const char*)(Dp + (int64_t)q0 * lddo);
     char* dq_ = dst + wid * 2048;
     char* dd_ = dst + QT + wid * 2048;
     if (q0 + 64 <= N) {
-      glds16(qs + vopaque(gq0), dq_);
-      glds16(qs + vopaque(gq1), dq_ + 1024);
-      glds16(ds + vopaque(gd0), dd_);
-      glds16(ds + vopaque(gd1), dd_ + 1024);
+      glds16_asm_so(qs, gq0, dq_);
+      glds16_asm_so(qs, gq1, dq_ + 1024);
+      glds16_asm_so(ds, gd0, dd_);
+      glds16_asm_so(ds, gd1, dd_ + 1024);
     } else {  // partial last slice: rows past N re-read row N-1 (their nlse2 = -inf zeroes them)
       const int r0 = q0 + prow < N ? prow : N - 1 - q0, r1 = q0 + prow + 8 < N ? prow + 8 : N - 1 - q0;
-      glds16(qs + (int64_t)r0 * 2 * ldq + cq0, dq_);
-      glds16(qs + (int64_t)r1 * 2 * ldq + cq1, dq_ + 1024);
-      glds16(ds + (int64_t)r0 * 2 * lddo + cq0, dd_);
-      glds16(ds + (int64_t)r1 * 2 * lddo + cq1, dd_ + 1024);
+      glds16_asm_so(qs, (uint32_t)(r0 * 2 * ldq) + cq0, dq_);
+      glds16_asm_so(qs, (uint32_t)(r1 * 2 * ldq) + cq1, dq_ + 1024);
+      glds16_asm_so(ds, (uint32_t)(r0 * 2 * lddo) + cq0, dd_);
+      glds16_asm_so(ds, (uint32_t)(r1 * 2 * lddo) + cq1, dd_ + 1024);
     }
-    if (wid == 0) glds4((const char*)(NL + q0) + vopaque(4 * lane), dst + 2 * QT);
-    else if (wid == 1) glds4((const char*)(ND + q0) + vopaque(4 * lane), dst + 2 * QT + 256);
+    // every DMA of the stage in the asm form: a compiler-visible one in flight makes hipcc wait
+    // vmcnt(0) before the next LDS read, draining the prefetch of slice it + 1 under slice it
+    if (wid == 0) glds4_asm_so(NL + q0, 4 * lane, dst + 2 * QT);
+    else if (wid == 1) glds4_asm_so(ND + q0, 4 * lane, dst + 2 * QT + 256);
   };
 
   // per-lane LDS offsets: row reads of query qrow (+32 per sub-slice), chunk 2s+hh; transposed
@@ -956,7 +960,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
                                                  bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
                                                  float scale) {
   constexpr int TILE = 64 * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, hh = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
   const int nb128 = (N + 127) / 128, qb = blk % nb128;
   const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
   const int64_t row0 = (int64_t)b * N;
@@ -1010,23 +1014,31 @@ __device__ __forceinline__ void attn_bwd_dq_body(char* __restrict__ kv0, char* _
   }
 
   const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  // per-lane DMA source offsets of rows prow / prow + 8 of a K (or V: base + vdelta) tile, computed
+  // once: the DMA is the SGPR-base + 32-bit-offset asm form (the per-tile 64-bit address arithmetic
+  // and the rows-past-N selects cost ~45 VALU per tile); the partial last tile clamps separately
+  const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+  const uint32_t ko0 = (uint32_t)(prow * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
+  const uint32_t ko1 = (uint32_t)((prow + 8) * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
   auto load_tile = [&](int kt, char* buf) {
-    const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
-    const int cc0 = (ppos ^ swz_rt(prow)) << 4, cc1 = (ppos ^ swz_rt(prow + 8)) << 4;
     const char* kb_ = (const char*)Kp + kt * tile_bytes;
     char* dk = buf + wid * 2048;
     char* dv = buf + TILE + wid * 2048;
-    int r0 = prow, r1 = prow + 8;
-    if ((kt + 1) * 64 > N) {  // partial last tile: rows past N re-read row N-1 (masked below)
-      r0 = kt * 64 + r0 < N ? r0 : N - 1 - kt * 64;
-      r1 = kt * 64 + r1 < N ? r1 : N - 1 - kt * 64;
+    if ((kt + 1) * 64 <= N) {
+      glds16_asm_so(kb_, ko0, dk);
+      glds16_asm_so(kb_, ko1, dk + 1024);
+      glds16_asm_so(kb_ + vdelta, ko0, dv);
+      glds16_asm_so(kb_ + vdelta, ko1, dv + 1024);
+    } else {  // partial last tile: rows past N re-read row N-1 (masked below)
+      const int r0 = kt * 64 + prow < N ? prow : N - 1 - kt * 64;
+      const int r1 = kt * 64 + prow + 8 < N ? prow + 8 : N - 1 - kt * 64;
+      const uint32_t c0 = (uint32_t)(r0 * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
+      const uint32_t c1 = (uint32_t)(r1 * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
+      glds16_asm_so(kb_, c0, dk);
+      glds16_asm_so(kb_, c1, dk + 1024);
+      glds16_asm_so(kb_ + vdelta, c0, dv);
+      glds16_asm_so(kb_ + vdelta, c1, dv + 1024);
     }
-    const char* s0 = kb_ + vopaque((uint32_t)(r0 * 2 * ldq + cc0));
-    const char* s1 = kb_ + vopaque((uint32_t)(r1 * 2 * ldq + cc1));
-    glds16(s0, dk);
-    glds16(s1, dk + 1024);
-    glds16(s0 + vdelta, dv);
-    glds16(s1 + vdelta, dv + 1024);
   };
 
   auto sub = [&](const char* sK, int kb, int key0) {
