@@ -478,14 +478,14 @@ def main():
                 # forward products: the 5 PF MX-FP8 peak)
                 fl = 2.0 * B * N * prod
                 pk = PEAK_FP8_TFLOPS if (args.dtype == "fp8" and name.startswith("fwd_")) else peak_mfma
-                tf = fl / avg_s / 1e12
+                tf = fl * Lyr / (ms / args.profile_steps / 1e3) / 1e12   # one product per layer per step
                 ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2), "mfma_peak": pk,
                             "mfma_frac": round(tf / pk, 4)})
             if name in ("fwd_mlp", "dx_mlp"):
                 # the fused MLP kernels sit near the ridge (~300 flop/B): their MFMA side as well
                 # (fwd: h2 W1^T and a W2^T; dx: h2 W1^T recomputed and dy W2 = 4 M D F flop per launch)
                 fl = 4.0 * B * N * bb.hidden_size * bb.intermediate_size
-                tf = fl / avg_s / 1e12
+                tf = fl * Lyr / (ms / args.profile_steps / 1e3) / 1e12
                 ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2),
                             "mfma_frac": round(tf / peak_mfma, 4)})
         ent.update({"ms_per_step": round(ms / args.profile_steps, 4), "launches_per_step": round(per_step, 2),
