@@ -125,7 +125,16 @@ def _single_process_grads(layers, dtype):
     m.zero_grad(set_to_none=True)
     poisson_nll_mean(m(px.to(DEV)), y.to(DEV)).backward()
     torch.cuda.synchronize()
-    return m.enc_flat.grad.detach().cpu(), m.head_flat.grad.detach().cpu()
+    return m.enc_flat.grad.detach().cpu(), m.head_flat.grad.detach().cpu(), m.layout
+
+
+def _worst_slots(layout, got, want, k=4):
+    """The parameter slots whose gradients differ most (for the failure message)."""
+    errs = []
+    for name, s in layout.slots.items():
+        g, w = got[s.offset:s.offset + s.numel], want[s.offset:s.offset + s.numel]
+        errs.append((float((g - w).norm() / w.norm().clamp_min(1e-30)), name))
+    return sorted(errs, reverse=True)[:k]
 
 
 @pytest.mark.parametrize("mode,layers,dtype,tol", [
@@ -144,13 +153,17 @@ def test_two_ranks_equal_single_process_batch(mode, layers, dtype, tol):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), mode, layers, dtype, out), nprocs=world, join=True)
-    ge, gh = _single_process_grads(layers, dtype)
+    ge, gh, lay = _single_process_grads(layers, dtype)
     for r in range(world):
         e, h = out[r]
-        for got, want, what in ((e, ge, "encoder"), (h, gh, "head")):
+        for got, want, what, ly in ((e, ge, "encoder", lay.enc), (h, gh, "head", lay.head)):
             err = float((got - want).norm() / want.norm())
             print(f"\n[{mode} {dtype} rank {r}] {what} grad rel err {err:.2e}")
-            assert err < tol, (mode, r, what, err)
+            if err >= tol:   # which slots, and is the single-process reference itself reproducible?
+                ge2 = _single_process_grads(layers, dtype)[0]
+                assert err < tol, (mode, r, what, err, _worst_slots(ly, got, want),
+                                   "ranks equal", torch.equal(out[0][0], out[1][0]),
+                                   "single-process rerun equal", torch.equal(ge2, ge))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 

@@ -861,49 +861,37 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(char* __restrict__ stg0, char
     const char* sD = st + QT;
     const float* sL = (const float*)(st + 2 * QT) + sub * 32 + 4 * hh;
     const float* sE = (const float*)(st + 2 * QT + 256) + sub * 32 + 4 * hh;
-    f32x16 acc;
+    // dP first, then S: both accumulators live together (the 158-VGPR body has the room since the
+    // DMA offsets were hoisted), so dS = P * dP takes P in f32 straight from the exp2 instead of
+    // unpacking the bf16 P of the dV product (16 fewer VALU per 32 x 32 unit)
+    f32x16 dpa, acc;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
+      const float4 e4 = *(const float4*)(sE + 8 * g);
+      dpa[4 * g] = e4.x; dpa[4 * g + 1] = e4.y; dpa[4 * g + 2] = e4.z; dpa[4 * g + 3] = e4.w;
       const float4 l4 = *(const float4*)(sL + 8 * g);
       acc[4 * g] = l4.x; acc[4 * g + 1] = l4.y; acc[4 * g + 2] = l4.z; acc[4 * g + 3] = l4.w;
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
+      dpa = mfma32p(*(const bf16x8*)(sD + sub * 4096 + roff[s]), vf[s], dpa);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
       acc = mfma32p(*(const bf16x8*)(sQ + sub * 4096 + roff[s]), kf[s], acc);
-    bf16x8 pbs[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      float p[8];
+      float p[8], ds[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) p[r] = __builtin_amdgcn_exp2f(acc[8 * s2 + r]);
-      const bf16x8 pb = pack8f(p);
-      pbs[s2] = pb;
+      for (int r = 0; r < 8; ++r) {
+        p[r] = __builtin_amdgcn_exp2f(acc[8 * s2 + r]);
+        ds[r] = p[r] * dpa[8 * s2 + r];  // dS = P * (dP - delta)
+      }
+      const bf16x8 pb = pack8f(p), db = pack8f(ds);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];
         dvacc[dt] = mfma32p(tr_pair(sD, o0, o1), pb, dvacc[dt]);
       }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 e4 = *(const float4*)(sE + 8 * g);
-      acc[4 * g] = e4.x; acc[4 * g + 1] = e4.y; acc[4 * g + 2] = e4.z; acc[4 * g + 3] = e4.w;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = mfma32p(*(const bf16x8*)(sD + sub * 4096 + roff[s]), vf[s], acc);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float ds[8];  // dS = P * (dP - delta) from the bf16 P of the dV product (carried packed: 8 VGPRs)
-      const uint4 u = __builtin_bit_cast(uint4, pbs[s2]);
-      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float pr = __uint_as_float((r & 1) ? (w[r >> 1] & 0xffff0000u) : (w[r >> 1] << 16));
-        ds[r] = pr * acc[8 * s2 + r];
-      }
-      const bf16x8 db = pack8f(ds);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const int o0 = sub * 4096 + s2 * 2048 + toff[dt][0], o1 = sub * 4096 + s2 * 2048 + toff[dt][1];

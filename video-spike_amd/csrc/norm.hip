@@ -6,7 +6,8 @@
 // RPW rows in flight (all loads issued before the first reduction) to hide HBM latency — the
 // first version with one row per wave measured 64 us for a 25,088 x 192 backward (~4x its
 // byte floor).  The backward reduces dgamma/dbeta per block in LDS: one f32 atomic per column
-// per block.
+// per block, or (with the workspace, as the ViT block passes it) one partial row per block that
+// ln_partsum_kernel adds in a fixed order: bit-identical reruns.
 #include <algorithm>
 
 #include <cstdlib>
@@ -81,7 +82,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
                                                      const float* __restrict__ g, const float* __restrict__ dres,
                                                      int64_t lddres, float* __restrict__ dx, int64_t lddx,
                                                      bf16_t* __restrict__ dx_lp, float* __restrict__ dg,
-                                                     float* __restrict__ db, int64_t rows, int cols) {
+                                                     float* __restrict__ db, float* __restrict__ part, int64_t rows,
+                                                     int cols) {
   __shared__ float red[2][4][64 * VPL];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float inv = 1.f / (float)cols;
@@ -148,8 +150,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     const int i = c >> 6, l = c & 63;
     const float a = (red[0][0][i * 64 + l] + red[0][1][i * 64 + l]) + (red[0][2][i * 64 + l] + red[0][3][i * 64 + l]);
     const float bb = (red[1][0][i * 64 + l] + red[1][1][i * 64 + l]) + (red[1][2][i * 64 + l] + red[1][3][i * 64 + l]);
-    unsafeAtomicAdd(dg + c, a);
-    unsafeAtomicAdd(db + c, bb);
+    if (part) {  // partial row of this block; ln_partsum_kernel adds the rows in a fixed order
+      part[(int64_t)blockIdx.x * 2 * cols + c] = a;
+      part[(int64_t)blockIdx.x * 2 * cols + cols + c] = bb;
+    } else {
+      unsafeAtomicAdd(dg + c, a);
+      unsafeAtomicAdd(db + c, bb);
+    }
   }
 }
 
@@ -391,13 +398,17 @@ static void launch_fwd(int64_t rows, int64_t cols, const float* x, int64_t ldx, 
 template <int VPL, typename TD>
 static void launch_bwd(int64_t rows, int64_t cols, const TD* dy, int64_t lddy, const float* x, int64_t ldx,
                        const float* mean, const float* rstd, const float* gamma, const float* dres, int64_t lddres,
-                       float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta, hipStream_t s) {
+                       float* dx, int64_t lddx, void* dx_lp, float* dgamma, float* dbeta, float* part,
+                       hipStream_t s) {
   constexpr int RPW = VPL <= 4 ? 4 : (VPL <= 8 ? 2 : 1);
   int64_t nb = cdiv(rows, 4 * RPW * 2);  // ~2 row-groups per wave: amortises the column reduction
-  if (nb > 2048) nb = 2048;
+  if (nb > (part ? kLnBwdBlocks : 2048)) nb = part ? kLnBwdBlocks : 2048;   // (part: one row per block)
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL((ln_bwd_kernel<VPL, RPW, TD>), dim3((unsigned)nb), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd,
-                     gamma, dres, lddres, dx, lddx, (bf16_t*)dx_lp, dgamma, dbeta, rows, (int)cols);
+                     gamma, dres, lddres, dx, lddx, (bf16_t*)dx_lp, dgamma, dbeta, part, rows, (int)cols);
+  if (part)
+    hipLaunchKernelGGL(ln_partsum_kernel, dim3((unsigned)cdiv(2 * cols, 16)), dim3(1024), 0, s, part, (int)nb,
+                       (int)cols, dgamma, dbeta);
 }
 
 }  // namespace vs
@@ -495,7 +506,7 @@ static int layernorm_bwd_t(int64_t rows, int64_t cols, const TD* dy, int64_t ldd
     return VS_OK;
   }
 #define B_(V) launch_bwd<V, TD>(rows, cols, dy, lddy, x, ldx, mean, rstd, gamma, dres, lddres, dx, lddx, dx_lp, dgamma, \
-                                dbeta, s)
+                                dbeta, (float*)workspace, s)
   VS_LN_DISPATCH(B_);
 #undef B_
   VS_LAUNCH_CHECK();
