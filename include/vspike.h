@@ -234,6 +234,18 @@ int vs_patch_embed_fwd(int64_t B, int64_t F, int64_t C, int64_t H, int64_t W, in
                        const float* pixels, const void* weight, const float* bias, const float* pos, int64_t D,
                        float* out, void* cols, void* stream);
 
+/* The patch embedding's weight gradient without the im2col tensor (mv:176-181; replaces
+ * vs_patch_im2col + the dW = dx^T cols product of vs_gemm): dweight[d, k] (+)= sum_m dx[m, d] X[m, k],
+ * dbias[d] (+)= sum_m dx[m, d] (dbias may be NULL), X the tubelet gather of vs_patch_embed_fwd read
+ * straight from the f32 pixels and rounded to bf16 as vs_patch_im2col rounds it.  dx: [B*n_tok, lddx]
+ * bf16, D a multiple of 64; dweight: [D, ldw] f32 (k < C*512).  The token reduction is split and the
+ * splits are added in a fixed order through `workspace` (>= vs_patch_embed_dw_workspace_bytes):
+ * bitwise equal to im2col + vs_gemm's dW product.  Tubelet 2, patch 16, < 2^24 tokens. */
+size_t vs_patch_embed_dw_workspace_bytes(int64_t tokens, int64_t D, int64_t K);
+int vs_patch_embed_dw(int64_t B, int64_t F, int64_t C, int64_t H, int64_t W, int64_t tubelet, int64_t patch,
+                      const float* pixels, const void* dx, int64_t lddx, int64_t D, float* dweight, int64_t ldw,
+                      float* dbias, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Fixed sinusoid position table (mv:101-112), f32 [n_pos, dim] (computed in f64, rounded). */
 int vs_sinusoid_table(int64_t n_pos, int64_t dim, float* out, void* stream);
 
@@ -486,6 +498,7 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 #define VS_PATH_MLP_FWD      18   /* vs_mlp_fwd: fused fc1 + GELU + fc2 + residual */
 #define VS_PATH_MLP_BWD      19   /* vs_mlp_bwd_da: fused recompute + GELU' product */
 #define VS_PATH_GEMM_FP8     20   /* vs_gemm_mxfp8: block-scaled fp8 MFMA GEMM */
+#define VS_PATH_PATCH_DW     21   /* vs_patch_embed_dw: patch dW with the tubelet gather in its B-load */
 #define VS_PATH_COUNT        24
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);

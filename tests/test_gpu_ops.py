@@ -875,6 +875,43 @@ def test_patch_embed_fused_matches_im2col_gemm(knobs, D, geo):
         assert rel(out, ref.double()) < 1e-5
 
 
+@pytest.mark.parametrize("D", [64, 128, 192])
+@pytest.mark.parametrize("geo", [(2, 16, 3, 224, 224), (3, 8, 3, 112, 112), (1, 4, 1, 32, 48), (128, 16, 3, 224, 224)])
+def test_patch_embed_dw_matches_im2col_dw(D, geo):
+    """vs_patch_embed_dw (the tubelet gather in the dW kernel's B-operand load, no cols) against
+    vs_patch_im2col + the dW product of vs_gemm on the same inputs: the same bf16 operand rounding,
+    split plan, MFMA order and fixed-order split reduce, so dW and db agree to the last bit (both
+    accumulate into non-zero gradients); and against fp64.  Geometries: 2 bench clips, a ragged token
+    count (3 x 4 x 7 x 7 = 1,176: a partial last 64-token step), 12 tokens (one partial step), and the
+    bench's 128 clips (200,704 tokens) with D = 192."""
+    from vspike import ops, _lib as L
+    B, F, C, H, W = geo
+    if B == 128 and D != 192:
+        pytest.skip("bench batch at the ViT-Tiny width only")
+    t, p = 2, 16
+    n_tok = (F // t) * (H // p) * (W // p)
+    M, K = B * n_tok, C * t * p * p
+    g = torch.Generator(device=DEV).manual_seed(93)
+    px = torch.randn(B, F, C, H, W, device=DEV, generator=g)
+    dx = torch.randn(M, D, device=DEV, generator=g).to(torch.bfloat16)
+    dw0 = torch.randn(D, K, device=DEV, generator=g)
+    db0 = torch.randn(D, device=DEV, generator=g)
+    dw, db = dw0.clone(), db0.clone()
+    L.dispatch_reset()
+    ops.patch_embed_dw(px, dx, dw, db, t, p)
+    assert L.dispatch_counts()["patch_dw"] == 1
+    cols = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+    ops.patch_im2col(px, cols, t, p)
+    dw2, db2 = dw0.clone(), db0.clone()
+    ops.linear_dw(dx, cols, dw2, db=db2)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    if M <= 4096:
+        r64 = dw0.double() + dx.double().t() @ cols.double()
+        assert rel(dw, r64) < 1e-5
+        assert rel(db, db0.double() + dx.double().sum(0)) < 1e-5
+
+
 def test_sinusoid_table_matches_oracle():
     from oracle import cpu_ref
     from vspike import ops

@@ -133,7 +133,7 @@ def test_vit_tiny12_bench_geometry_loss_curve(golden, dtype):
 # W-resident qkv, proj + LayerNorm2 fused, row-slab N <= 192 products (dX, patch embedding), the
 # fused MLP forward and its recomputing GELU' backward, the dW tiles, the skinny head, flash attention
 BENCH_PATHS_BF16 = ("gemm_wres", "gemm_ln_fwd", "gemm_slab", "mlp_fwd", "mlp_bwd", "gemm_dw", "gemm_skinny",
-                    "attn_fwd", "attn_bwd")
+                    "attn_fwd", "attn_bwd", "patch_fused", "patch_dw")
 
 
 @contextlib.contextmanager

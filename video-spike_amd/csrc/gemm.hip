@@ -2391,6 +2391,41 @@ extern "C" int vs_patch_embed_fwd(int64_t B, int64_t F, int64_t C, int64_t H, in
   return VS_OK;
 }
 
+extern "C" size_t vs_patch_embed_dw_workspace_bytes(int64_t tokens, int64_t D, int64_t K) {
+  return vs::dw_workspace_bytes(D, K, tokens);
+}
+
+// The patch embedding's weight gradient without cols (mv:176-181): dW[D][K] += dx^T gather(pixels),
+// db[D] += column sums of dx — gemm_dw_kernel with the tubelet gather in its B-operand load
+// (gemm_dw.hip), bitwise equal to vs_patch_im2col + the dW product of vs_gemm.
+extern "C" int vs_patch_embed_dw(int64_t B, int64_t F, int64_t C, int64_t H, int64_t W, int64_t tubelet, int64_t patch,
+                                 const float* pixels, const void* dx, int64_t lddx, int64_t D, float* dweight,
+                                 int64_t ldw, float* dbias, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace vs;
+  VS_REQUIRE(pixels && dx && dweight && workspace, "vs_patch_embed_dw: null pointer");
+  VS_REQUIRE(tubelet == 2 && patch == 16, "vs_patch_embed_dw: built for tubelet 2, patch 16");
+  VS_REQUIRE(B > 0 && F % 2 == 0 && H % 16 == 0 && W % 16 == 0 && C >= 1 && C <= 8,
+             "vs_patch_embed_dw: frames / size must divide by the tubelet / patch");
+  VS_REQUIRE(D % 64 == 0 && D >= 64 && D <= 1024 && lddx % 8 == 0 && lddx >= D && ldw >= C * 512,
+             "vs_patch_embed_dw: D must be a multiple of 64, dx rows 16-byte aligned");
+  VS_REQUIRE(aligned16(pixels) && aligned16(dx) && aligned16(workspace), "vs_patch_embed_dw: pointers must be 16-byte aligned");
+  const int64_t n_tok = (F / 2) * (H / 16) * (W / 16), M = B * n_tok, K = C * 512;
+  VS_REQUIRE(M < (1ll << 24), "vs_patch_embed_dw: more than 2^24 tokens per launch");
+  VS_REQUIRE(B * F * C * H * W < (1ll << 40), "vs_patch_embed_dw: batch too large");
+  VS_REQUIRE((size_t)workspace_bytes >= dw_workspace_bytes(D, K, M), "vs_patch_embed_dw: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  // algorithmic bytes: the pixels once (f32), dx (bf16), dW / db read + written
+  ScopedTimer timer(g_timer_tag >= 0 ? g_timer_tag : VS_TIMER_GEMM_DW, s,
+                    (double)M * (double)K * 4.0 + (double)M * (double)D * 2.0 + (double)D * (double)K * 8.0 +
+                        (dbias ? (double)D * 8.0 : 0.0));
+  PatchDwGeo g;
+  g.F = (int)F; g.C = (int)C; g.H = (int)H; g.W = (int)W;
+  g.n_tok = (int)n_tok; g.HpWp = (int)((H / 16) * (W / 16)); g.Wp = (int)(W / 16);
+  g.inv_ntok = 1.0f / (float)g.n_tok; g.inv_hpwp = 1.0f / (float)g.HpWp; g.inv_wp = 1.0f / (float)g.Wp;
+  count_path(VS_PATH_PATCH_DW);
+  return launch_patch_dw((const bf16_t*)dx, lddx, D, pixels, g, M, K, dweight, ldw, dbias, (float*)workspace, s);
+}
+
 extern "C" int vs_gemm_ln_fwd(const vs_gemm_desc* d, const float* gamma, const float* beta, float eps, void* h,
                               int64_t ldh, float* mean, float* rstd, void* stream) {
   using namespace vs;

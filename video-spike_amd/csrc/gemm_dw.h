@@ -21,9 +21,21 @@ struct DwPlan {
   int64_t part_floats, sum_floats;
 };
 
+// the patch embedding's weight gradient with the tubelet gather in the B-operand load (no cols):
+// pixels f32 (B, F, C, H, W), tubelet 2, patch 16; token m = (b, f', hp, wp), column k = (c, t, i, j)
+struct PatchDwGeo {
+  int F, C, H, W;
+  int n_tok, HpWp, Wp;
+  float inv_ntok, inv_hpwp, inv_wp;  // float reciprocals (token index < 2^24, corrected by one step)
+};
+
 DwPlan plan_dw(int64_t M, int64_t N, int64_t K);
 size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int launch_dw(const vs_gemm_desc* d, hipStream_t s);
+// dW[D][K] += dx^T gather(px), db[D] += column sums of dx (bf16 dx [tokens][lddx]); the plan of
+// dw_workspace_bytes(D, K, tokens)
+int launch_patch_dw(const bf16_t* dx, int64_t lddx, int64_t D, const float* px, const PatchDwGeo& g, int64_t tokens,
+                    int64_t K, float* dw, int64_t ldw, float* db, float* ws, hipStream_t s);
 
 // skinny split-K (M <= 64, N <= 256, both operands K-contiguous, bf16 or f32): partials [splits][M][N] in the workspace
 bool skinny_ok(const vs_gemm_desc* d);

@@ -78,15 +78,26 @@ __device__ __forceinline__ bf16x8 dw_frag(const char* img, int rb, int kk, int l
 // and computed once, so a step's DMA is one SGPR base per operand + NA + NB instructions.
 // Partial tiles are stored in tile-fragment order: float4 ((rowfrag * BN/16 + colfrag) * 64 + lane),
 // rowfrag / colfrag = the 16-row / 16-column block within the tile.
-template <int BM, int BN, int SUMS, int NSTG>
+//
+// PX (the patch embedding's dW, mv:176-181): B is not a tensor but the tubelet gather of the f32
+// pixels — column n = (c, t, i, j) of token m = (b, f', hp, wp) is px[b][2f'+t][c][16hp+i][16wp+j].
+// A lane's 16-B piece of a B image (token row krow, 8 columns n..n+7 = 8 adjacent pixels of one
+// image row) is two 16-B global loads at a step-invariant column offset plus the token's base,
+// converted to bf16 (RNE, as im2col) and written to the LDS position the DMA would fill: the MFMA
+// side and the reduction are the plain kernel's, so the result is bitwise im2col + dW.  The loads of
+// step s + 1 are issued (asm, counted waits) before step s's MFMAs and written to LDS after them;
+// the A operand (dx) keeps the LDS-DMA, two steps ahead.  NSTG = 3.
+template <int BM, int BN, int SUMS, int NSTG, bool PX = false>
 __global__ __launch_bounds__(512, 1) void gemm_dw_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t M,
                                                          const bf16_t* __restrict__ B, int64_t ldb, int64_t N,
                                                          int64_t K, DwGrid g, float* __restrict__ part,
-                                                         float* __restrict__ sums) {
+                                                         float* __restrict__ sums, const float* __restrict__ px,
+                                                         PatchDwGeo pg) {
   constexpr int NA = BM / 64, NB = BN / 64, NI = NA + NB;  // 64-column LDS images per stage
   constexpr int IMG = 8192;
   constexpr int STAGE = NI * IMG;
-  constexpr int PER = NI;                 // DMA wave-instructions per wave per stage
+  constexpr int PER = PX ? NA : NI;       // DMA wave-instructions per wave per stage
+  static_assert(!PX || NSTG == 3, "the gather variant runs the 3-stage ring");
   constexpr int WM = BM / 4, FI = WM / 16, WN = BN / 2, FJ = WN / 16, CF = BN / 16;
   static_assert(NSTG >= 2 && NSTG <= 4, "2- to 4-stage ring");
   __shared__ __attribute__((aligned(16))) char st0[STAGE];
@@ -130,17 +141,67 @@ __global__ __launch_bounds__(512, 1) void gemm_dw_kernel(const bf16_t* __restric
   auto issue = [&](int s, char* stg) {
     const int64_t k0 = (int64_t)(ks0 + s) * 64;
     const char* ba = (const char*)(A + k0 * lda);
-    const char* bb = (const char*)(B + k0 * ldb);
+    const char* bb = PX ? ba : (const char*)(B + k0 * ldb);
     if (K - k0 >= 64) {
 #pragma unroll
-      for (int j = 0; j < NI; ++j) glds16_asm_so(j < NA ? ba : bb, off[j], stg + j * IMG + wid * 1024);
+      for (int j = 0; j < PER; ++j) glds16_asm_so(j < NA ? ba : bb, off[j], stg + j * IMG + wid * 1024);
     } else {  // the reduction's last, partial step: token rows past K re-read row K-1 (zeroed in LDS)
       const int kv = (int)(K - k0);
       const int kk = krow < kv ? krow : kv - 1;
 #pragma unroll
-      for (int j = 0; j < NI; ++j)
+      for (int j = 0; j < PER; ++j)
         glds16_asm_so(j < NA ? ba : bb, (uint32_t)(((int64_t)kk * (j < NA ? lda : ldb) + col_of(j)) * 2),
                       stg + j * IMG + wid * 1024);
+    }
+  };
+  // PX: this lane's pixel offset of its 8 columns in B image jb (step-invariant), and the token base
+  typedef __attribute__((ext_vector_type(4))) float f4v;
+  const int64_t plane = (int64_t)pg.H * pg.W;
+  uint32_t coff[NB];
+#pragma unroll
+  for (int jb = 0; jb < NB; ++jb) {
+    const int n = (int)n0 + jb * 64 + cch * 8;   // columns n .. n + 7: pixels j = n & 15 .. + 7 of one image row
+    coff[jb] = PX ? (uint32_t)((((n >> 8) & 1) * pg.C + (n >> 9)) * plane + ((n >> 4) & 15) * pg.W + (n & 15)) : 0u;
+  }
+  auto tok_base = [&](int64_t m) -> int64_t {
+    const int mi = (int)m;
+    int b = (int)((float)mi * pg.inv_ntok);
+    b -= b * pg.n_tok > mi;
+    b += (b + 1) * pg.n_tok <= mi;
+    const int n = mi - b * pg.n_tok;
+    int fp = (int)((float)n * pg.inv_hpwp);
+    fp -= fp * pg.HpWp > n;
+    fp += (fp + 1) * pg.HpWp <= n;
+    const int r = n - fp * pg.HpWp;
+    int hp = (int)((float)r * pg.inv_wp);
+    hp -= hp * pg.Wp > r;
+    hp += (hp + 1) * pg.Wp <= r;
+    const int wp = r - hp * pg.Wp;
+    return ((int64_t)b * pg.F + 2 * fp) * pg.C * plane + (int64_t)(16 * hp) * pg.W + 16 * wp;
+  };
+  auto gather = [&](int s, f4v (&r)[2 * NB]) {
+    const int64_t k0 = (int64_t)(ks0 + s) * 64;
+    const int64_t m = k0 + krow < K ? k0 + krow : K - 1;   // rows past K: finite re-reads, zeroed in LDS
+    const float* tb = px + tok_base(m);
+#pragma unroll
+    for (int jb = 0; jb < NB; ++jb) {
+      const float* p = tb + coff[jb];
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[2 * jb]) : "v"(p) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(r[2 * jb + 1]) : "v"(p) : "memory");
+    }
+  };
+  // after the counted wait: tie the registers to it (no use is scheduled above the wait), convert, store
+  auto bwrite = [&](char* stg, f4v (&r)[2 * NB]) {
+#pragma unroll
+    for (int q = 0; q < 2 * NB; ++q) asm volatile("" : "+v"(r[q]));
+#pragma unroll
+    for (int jb = 0; jb < NB; ++jb) {
+      uint4 u;
+      u.x = (uint32_t)f2bf(r[2 * jb][0]) | ((uint32_t)f2bf(r[2 * jb][1]) << 16);
+      u.y = (uint32_t)f2bf(r[2 * jb][2]) | ((uint32_t)f2bf(r[2 * jb][3]) << 16);
+      u.z = (uint32_t)f2bf(r[2 * jb + 1][0]) | ((uint32_t)f2bf(r[2 * jb + 1][1]) << 16);
+      u.w = (uint32_t)f2bf(r[2 * jb + 1][2]) | ((uint32_t)f2bf(r[2 * jb + 1][3]) << 16);
+      *(uint4*)(stg + (NA + jb) * IMG + wid * 1024 + lane * 16) = u;
     }
   };
   auto compute = [&](const char* stg) {
@@ -187,6 +248,31 @@ __global__ __launch_bounds__(512, 1) void gemm_dw_kernel(const bf16_t* __restric
     constexpr int S = decltype(sc)::value;
     char* cur = stage_ptr(S);
     char* far = stage_ptr((S + NSTG - 1) % NSTG);  // the stage step s - 1 used
+    if constexpr (PX) {
+      // A of step s landed at the previous step's gather wait; only A of s + 1 may be in flight
+      if (s + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // step s's images complete (B written last step); step s-1's stage free
+      asm volatile("" ::: "memory");
+      const int64_t k0 = (int64_t)(ks0 + s) * 64;
+      if (K - k0 < 64) {
+        zero_tail(cur, (int)(K - k0));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      f4v r[2 * NB];
+      if (s + 1 < nk) gather(s + 1, r);
+      if (s + 2 < nk) issue(s + 2, far);
+      compute(cur);
+      if (s + 1 < nk) {  // B of step s + 1: its loads, then (maybe) A of s + 2 are outstanding
+        if (s + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bwrite(stage_ptr((S + 1) % NSTG), r);
+      }
+      return;
+    }
     // steps s+1 .. s+NSTG-2 may stay in flight
     const int ahead = nk - 1 - s;
     if (NSTG >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
@@ -205,9 +291,22 @@ __global__ __launch_bounds__(512, 1) void gemm_dw_kernel(const bf16_t* __restric
     if (s + NSTG - 1 < nk) issue(s + NSTG - 1, far);
     compute(cur);
   };
+  if constexpr (PX) {  // prologue: B of step 0 gathered and written, A of steps 0, 1 in flight
+    f4v r[2 * NB];
+    gather(0, r);
+    issue(0, st0);
+    if (nk > 1) {
+      issue(1, st1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NA) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+    }
+    bwrite(st0, r);
+  } else {
 #pragma unroll
-  for (int i = 0; i < NSTG - 1; ++i)
-    if (i < nk) issue(i, stage_ptr(i));
+    for (int i = 0; i < NSTG - 1; ++i)
+      if (i < nk) issue(i, stage_ptr(i));
+  }
   for (int s = 0; s < nk; s += NSTG) {
     step(s, IC<0>{});
     if (s + 1 < nk) step(s + 1, IC<1 % NSTG>{});
@@ -635,21 +734,22 @@ size_t dw_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   return (size_t)(p.part_floats + p.sum_floats + 64) * 4;
 }
 
-template <int BM, int BN, int SUMS, bool TRANS>
+template <int BM, int BN, int SUMS, bool TRANS, bool PX = false>
 static void launch_dw_t(const bf16_t* a, int64_t lda, int64_t Ma, const bf16_t* b, int64_t ldb, int64_t Nb, int64_t K,
-                        const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s) {
+                        const DwPlan& p, float* part, float* sums, float* c, int64_t ldc, float* bias, hipStream_t s,
+                        const float* px = nullptr, const PatchDwGeo& pg = PatchDwGeo{}) {
   const unsigned nwg = (unsigned)(p.g.tiles_m * p.g.tiles_n * p.g.splits);
   if constexpr ((BM + BN) / 64 * 8192 * 4 <= 131072) {
-    if (p.stages == 4) {
+    if (!PX && p.stages == 4) {
       hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 4>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
-                         part, sums);
+                         part, sums, px, pg);
     } else {
-      hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
-                         part, sums);
+      hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3, PX>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K,
+                         p.g, part, sums, px, pg);
     }
   } else {
-    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
-                       part, sums);
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, SUMS, 3, PX>), dim3(nwg), dim3(512), 0, s, a, lda, Ma, b, ldb, Nb, K, p.g,
+                       part, sums, px, pg);
   }
   const int tiles = p.g.tiles_m * p.g.tiles_n;
   int64_t sum_len = 0, sum_w = 1;
@@ -713,6 +813,27 @@ int launch_dw(const vs_gemm_desc* d, hipStream_t s) {
 #undef DW_BN
 #undef DW_BM
 #undef DW_
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+int launch_patch_dw(const bf16_t* dx, int64_t lddx, int64_t D, const float* px, const PatchDwGeo& pg, int64_t tokens,
+                    int64_t K, float* dw, int64_t ldw, float* db, float* ws, hipStream_t s) {
+  const DwPlan p = plan_dw(D, K, tokens);
+  VS_REQUIRE(p.valid && !p.swap && K % p.BN == 0, "vs_patch_embed_dw: no gather dW plan for this shape");
+  float* part = ws;
+  float* sums = part + p.part_floats;
+#define PD_(BM_, BN_)                                                                                               \
+  do {                                                                                                            \
+    if (db) launch_dw_t<BM_, BN_, 1, false, true>(dx, lddx, D, nullptr, 0, K, tokens, p, part, sums, dw, ldw, db, s, \
+                                                  px, pg);                                                        \
+    else launch_dw_t<BM_, BN_, 0, false, true>(dx, lddx, D, nullptr, 0, K, tokens, p, part, sums, dw, ldw, db, s,    \
+                                               px, pg);                                                           \
+  } while (0)
+  if (p.BM == 64) { if (p.BN == 128) PD_(64, 128); else PD_(64, 64); }
+  else if (p.BM == 128) { if (p.BN == 128) PD_(128, 128); else PD_(128, 64); }
+  else { if (p.BN == 128) PD_(192, 128); else PD_(192, 64); }
+#undef PD_
   VS_LAUNCH_CHECK();
   return VS_OK;
 }

@@ -33,7 +33,7 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
 # vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
               "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
-              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8")
+              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8", "patch_dw")
 PATH_COUNT = 24
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
@@ -131,6 +131,9 @@ PROTOTYPES = {
     "vs_sinusoid_table": (ctypes.c_int, [c_i64, c_i64, c_p, c_p]),
     "vs_patch_embed_fwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64,
                                           c_p, c_p, c_p]),
+    "vs_patch_embed_dw_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "vs_patch_embed_dw": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_p,
+                                         c_i64, c_p, c_p, c_i64, c_p]),
     "vs_colsum": (ctypes.c_int, [c_i32, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
     "vs_cast": (ctypes.c_int, [c_i32, c_i32, c_i64, c_p, c_p, c_p]),
     "vs_poisson_workspace_bytes": (c_sz, [c_i64]),

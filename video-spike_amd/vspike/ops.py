@@ -262,6 +262,32 @@ def patch_embed_fused_ok(cfg, dtype) -> bool:
             cfg.hidden_size in (64, 128, 192) and cfg.num_channels <= 8 and L.knob_get("no_patch_fused") == 0)
 
 
+def patch_embed_dw_workspace_bytes(tokens, D, K):
+    return int(lib().vs_patch_embed_dw_workspace_bytes(tokens, D, K))
+
+
+def patch_dw_ok(cfg, dtype) -> bool:
+    """Shapes the gather weight gradient covers (else im2col + the dW product of vs_gemm)."""
+    return (dtype == torch.bfloat16 and cfg.tubelet_size == 2 and cfg.patch_size == 16 and cfg.hidden_size % 64 == 0
+            and cfg.num_channels <= 8 and L.knob_get("no_patch_fused") == 0)
+
+
+def patch_embed_dw(pixels, dx, dweight, dbias, tubelet, patch, workspace=None):
+    """dweight[D, C*t*p*p] += dx^T X and dbias[D] += column sums of dx, X the tubelet gather of the f32
+    pixels (B, F, C, H, W) read in the operand load (vs_patch_embed_dw); dx bf16 [B*n_tok, D]."""
+    require_device(pixels, dx, dweight)
+    B, F, C, H, W = pixels.shape
+    D = dx.shape[1]
+    K = dweight.shape[1]
+    if workspace is None:
+        workspace = torch.empty(patch_embed_dw_workspace_bytes(dx.shape[0], D, K) // 4 + 4, dtype=torch.float32,
+                                device=dx.device)
+    check(lib().vs_patch_embed_dw(B, F, C, H, W, tubelet, patch, pixels.data_ptr(), dx.data_ptr(), dx.stride(0), D,
+                                  dweight.data_ptr(), dweight.stride(0), ptr(dbias), workspace.data_ptr(),
+                                  workspace.numel() * 4, stream()), "vs_patch_embed_dw")
+    return dweight
+
+
 def sinusoid_table(n_pos, dim, device):
     out = torch.empty(n_pos, dim, dtype=torch.float32, device=device)
     check(lib().vs_sinusoid_table(n_pos, dim, out.data_ptr(), stream()), "vs_sinusoid_table")

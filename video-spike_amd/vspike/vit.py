@@ -335,11 +335,11 @@ class VideoMAE(nn.Module):
         M = B * N
         lp = dt != torch.float32
         ar = Arena()
-        # patch embedding: the fused gather GEMM when no weight gradient follows (frozen encoder /
-        # inference: 49.9 us vs 61.8 us for im2col + GEMM at C2); when the encoder trains the dW
-        # product needs the gathered rows, and im2col + GEMM (61.8 us) beats the fused kernel with its
-        # cols side output (79.9 us) — profiles/r03_v2_microbench_patch.txt
-        fused = ops.patch_embed_fused_ok(cfg, dt) and not save_encoder
+        # patch embedding: the fused gather GEMM (49.9 us vs 61.8 us for im2col + GEMM at C2,
+        # profiles/r03_v2_microbench_patch.txt); when the encoder trains, its weight gradient gathers
+        # the pixels again in its own operand load (vs_patch_embed_dw), so no cols tensor exists in
+        # bf16 at all.  fp32 (and shapes outside the fused kernels) keep im2col + GEMM.
+        fused = ops.patch_embed_fused_ok(cfg, dt) and (not save_encoder or ops.patch_dw_ok(cfg, dt))
         if not fused:
             ar.add("cols", (M, cfg.patch_dim), dt)
         ar.add("x0", (M, D), torch.float32)
@@ -423,7 +423,7 @@ class VideoMAE(nn.Module):
                  bias=lh.view(head32, "enc_b"), workspace=ent["head_ws"])
         ops.linear(z, lh.view(head32, "dec_w"), r, bias=lh.view(head32, "dec_b"))
         state = _FwdState(act=act, structs=ent["structs"], enc_lp=enc_lp, head_lp=head_lp, x_flat_lp=x_flat_lp,
-                          x_final=ent["x_final"], B=B)
+                          x_final=ent["x_final"], B=B, pixels=pixels if "cols" not in act else None)
         ent["owner"] = weakref.ref(state)
         return r.view(B, 100, -1), state
 
@@ -470,7 +470,8 @@ class VideoMAE(nn.Module):
             # head dZ = dr dec_w over K = 100 * neurons: split-K partials summed in a fixed order
             ar.add("dz_ws", (max(ops.splitk_workspace_bytes(torch.float32, B, lay.enc_out, lay.out_dim), 16) // 4 + 64,),
                    torch.float32)
-            pws = ops.splitk_workspace_bytes(dt, D, cfg.patch_dim, M)
+            pws = max(ops.splitk_workspace_bytes(dt, D, cfg.patch_dim, M),
+                      ops.patch_embed_dw_workspace_bytes(M, D, cfg.patch_dim) if lp and D % 64 == 0 else 0)
             if pws:
                 ar.add("patch_ws", (pws // 4 + 64,), torch.float32)
             ar.add("ln_ws", (ops.layernorm_bwd_workspace_bytes(B * N, D) // 4 + 64,), torch.float32)
@@ -556,7 +557,10 @@ class VideoMAE(nn.Module):
         if prev is not None:
             self._ready(self.enc_flat, *lay.layer_ranges[prev])
         # patch embedding: dW = dx0^T cols, db = colsum(dx0); the position table is fixed
-        if lp:   # bias gradient fused as row sums of dx^T (fixed-order, like every block's dW)
+        if "cols" not in act:   # cols = the tubelet gather of the pixels, done in the dW's operand load
+            ops.patch_embed_dw(st["pixels"], dx_lp, Ge("patch_w"), Ge("patch_b"), cfg.tubelet_size, cfg.patch_size,
+                               workspace=g["patch_ws"])
+        elif lp:   # bias gradient fused as row sums of dx^T (fixed-order, like every block's dW)
             ops.linear_dw(dx_lp, act["cols"], Ge("patch_w"), db=Ge("patch_b"), workspace=g.get("patch_ws"))
         else:
             ops.linear_dw(dx, act["cols"], Ge("patch_w"), db=Ge("patch_b"))
