@@ -85,6 +85,16 @@ def test_gpu_only_entry_points_reject_bad_args_without_launching(built_lib):
     assert b"dtype" in lib.vs_last_error()
     assert lib.vs_attn_fwd(1, 1, 10, 1, 32, None, 192, None, 64, None, 0.125, None) == -1
     assert b"head dim" in lib.vs_last_error()
+    # the gather weight gradient: null operands, then a tubelet it is not built for
+    assert lib.vs_patch_embed_dw(2, 16, 3, 224, 224, 2, 16, None, None, 192, 192, None, 1536, None, None, 0, None) == -1
+    assert b"null pointer" in lib.vs_last_error()
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.addressof(buf)
+    assert lib.vs_patch_embed_dw(2, 16, 3, 224, 224, 4, 16, p, p, 192, 192, p, 1536, None, p, 0, None) == -1
+    assert b"tubelet 2" in lib.vs_last_error()
+    assert lib.vs_patch_embed_dw(2, 16, 3, 224, 224, 2, 16, p, p, 96, 96, p, 1536, None, p, 0, None) == -1
+    assert b"multiple of 64" in lib.vs_last_error()
+    assert lib.vs_patch_embed_dw_workspace_bytes(200704, 192, 1536) > 0
 
 
 def test_product_ops_refuse_cpu_tensors(built_lib):
