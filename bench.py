@@ -81,6 +81,12 @@ def parse():
                          "(scripts/c3_curve.py), and non-finite scores send attention down its safe-softmax redo")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="budget of the CPU-oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 sub-record (ViT-Base/16 at 128 clips, n = 512) the default C2 run appends")
+    ap.add_argument("--c3-batch", type=int, default=None, help="C3 sub-record clips per GPU (default: the train config's 128)")
+    ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-warmup", type=int, default=3)
+    ap.add_argument("--c3-profile-steps", type=int, default=2)
     ap.add_argument("--graph", action="store_true",
                     help="time the step as a hipGraph replay (vspike.graph.GraphedStep; N=1 only).  Off by default: "
                          "on MI355X the replay measured 6.20 vs 5.62 ms/step eager (DESIGN.md section 7)")
@@ -116,24 +122,42 @@ def _cpu_share():
     return n
 
 
-def cpu_baseline(cfg, params, pixels, target, seconds):
+def _pin_threads(n):
+    """Pin this process to n CPUs of its affinity set (the oracle's OpenMP pool then stays on the
+    same cores for every cell); returns the previous set, or None where affinity is unavailable."""
+    if not hasattr(os, "sched_getaffinity"):
+        return None
+    old = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, sorted(old)[:max(1, n)])
+    except OSError:
+        return None
+    return old
+
+
+def cpu_baseline(cfg, params, pixels, target, seconds, reps=10):
     """BASELINE.md CPU plan (BASELINE.md:37): the oracle (torch-CPU fp32 restatement of the step) per
-    clip, fwd and fwd+bwd at B=1 and B=4, median of >= 5 runs after two warm-ups per cell (the first
-    call of a shape pays one-off costs: allocator growth, first-touch page faults, oneDNN primitive
-    creation; round 3's single warm-up left B=1 slower per clip than B=4).  Thread counts: the CPU
-    share this process has (affinity / cgroup quota; OMP_NUM_THREADS on the box) and os.cpu_count()
-    as BASELINE.md asks; the latter is skipped when one B=1 forward at that count takes more than
-    4x the share's (oversubscription: the box's 256-CPU count vs its 16-CPU quota), and recorded so.
-    `value` is the B=4 fwd+bwd rate of the faster count; every cell reports median, min and max
-    and the cells are checked for monotonicity."""
+    clip, fwd and fwd+bwd at B=1 and B=4.  Round 4's harness ran each cell's 5 repetitions back to
+    back and left B=1 fwd+bwd FASTER than B=1 fwd (cells measured minutes apart under different
+    host load / clock).  Now: the process is pinned to its CPU share (one core per OpenMP thread),
+    every cell gets two warm-ups (allocator growth, first-touch page faults, oneDNN primitive
+    creation), then `reps` ROUNDS each run all four cells once in a rotating order, so every cell
+    sees the same host conditions; a cell's value is the median over the rounds.  Thread counts:
+    the CPU share (affinity / cgroup quota; OMP_NUM_THREADS on the box) and os.cpu_count() as
+    BASELINE.md asks; the latter is skipped when one B=1 forward at that count takes more than 4x
+    the share's (oversubscription: the box's 256-CPU count vs its 16-CPU quota), and recorded so.
+    `value` is the B=4 fwd+bwd rate of the faster count; cells report median, min and max and are
+    checked for monotonicity (fwd+bwd dearer than fwd at each batch)."""
     from oracle import cpu_ref
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or _cpu_share()
     counts = [share] + ([os.cpu_count()] if (os.cpu_count() or 0) != share else [])
     P = cpu_ref.to_torch(params)
     t_start = time.perf_counter()
     per_count, loss4, skipped = {}, None, {}
+    cells = [(1, "fwd"), (1, "fwd_bwd"), (4, "fwd"), (4, "fwd_bwd")]
     for threads in counts:
         torch.set_num_threads(threads)
+        old_aff = _pin_threads(threads) if threads == share else None
         res = {}
 
         def cell(B, mode):
@@ -159,21 +183,27 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
                                          f"{per_count[str(share)]['B1_fwd']['s_per_clip']:.2f} s on {share} threads "
                                          "(oversubscribed: the process's CPU quota is smaller than the host's count)")
                 continue
-        for B in (1, 4):
-            for mode in ("fwd", "fwd_bwd"):
-                run = cell(B, mode)
-                for _ in range(2):                                   # warm-ups
-                    loss = run()
-                if B == 4 and mode == "fwd":
-                    loss4 = float(loss)
-                ts = []
-                for _ in range(5):
-                    t0 = time.perf_counter()
-                    run()
-                    ts.append((time.perf_counter() - t0) / B)
-                res[f"B{B}_{mode}"] = {"s_per_clip": round(statistics.median(ts), 4), "min": round(min(ts), 4),
-                                       "max": round(max(ts), 4), "runs": len(ts)}
-                _progress(f"cpu baseline, {threads} threads, B={B} {mode}: {res[f'B{B}_{mode}']}")
+        runs = {c: cell(*c) for c in cells}
+        for c in cells:                                              # warm-ups
+            for _ in range(2):
+                loss = runs[c]()
+            if c == (4, "fwd"):
+                loss4 = float(loss)
+        ts = {c: [] for c in cells}
+        for r in range(reps):                                        # interleaved rounds
+            order = cells[r % len(cells):] + cells[:r % len(cells)]
+            for c in order:
+                t0 = time.perf_counter()
+                runs[c]()
+                ts[c].append((time.perf_counter() - t0) / c[0])
+            if (r + 1) % 2 == 0:
+                _progress(f"cpu baseline, {threads} threads: round {r + 1}/{reps}")
+        for (B, mode), t in ts.items():
+            res[f"B{B}_{mode}"] = {"s_per_clip": round(statistics.median(t), 4), "min": round(min(t), 4),
+                                   "max": round(max(t), 4), "runs": len(t)}
+            _progress(f"cpu baseline, {threads} threads, B={B} {mode}: {res[f'B{B}_{mode}']}")
+        if old_aff is not None:
+            os.sched_setaffinity(0, old_aff)
         c = lambda k: res[k]["s_per_clip"]  # noqa: E731
         # fwd+bwd must cost more than fwd at each batch (the per-clip cost across batches is the CPU's
         # own batching effect: on the box B=4 runs the forward cheaper per clip and the backward dearer
@@ -186,8 +216,9 @@ def cpu_baseline(cfg, params, pixels, target, seconds):
     best = min(per_count, key=lambda k: per_count[k]["B4_fwd_bwd"]["s_per_clip"])
     value = 1.0 / per_count[best]["B4_fwd_bwd"]["s_per_clip"]
     out = {"value": round(value, 4), "unit": "clips/sec", "cores": int(best), "kind": "port",
-           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of 5 after 2 warm-ups, "
-                     f"{best} threads; {elapsed:.1f} s of CPU work in all",
+           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of {reps} interleaved rounds "
+                     f"(all four cells per round) after 2 warm-ups per cell, {best} threads pinned to "
+                     f"{best} cores; {elapsed:.1f} s of CPU work in all",
            "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(), "cpu_share": _cpu_share(),
                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
            "detail": per_count, "skipped": skipped}
@@ -212,8 +243,9 @@ def _reference_grads(model):
 # makes bench.py exit non-zero after printing its line
 PARITY_TOL = {"fp32": {"log_rates": 1e-4, "loss": 1e-5, "grad": 1e-3},
               "bf16": {"log_rates": 7e-3, "loss": 1e-4, "grad": 1e-2},
-              # MX-FP8 forward products (3 mantissa bits): the bars of tests/test_gpu_c5.py
-              "fp8": {"log_rates": 6e-2, "loss": 1e-2, "grad": 1.5e-1}}
+              # MX-FP8 forward products (3 mantissa bits): oracle/tolerances.py, the bars tests/test_gpu_c5.py
+              # uses too (filled in by full_batch_parity, which imports the oracle package)
+              "fp8": None}
 
 
 def full_batch_parity(ccfg, params, pixels, target, gpu, args):
@@ -248,6 +280,9 @@ def full_batch_parity(ccfg, params, pixels, target, gpu, args):
         errs[k] = float(np.linalg.norm((g - r).ravel()) / max(np.linalg.norm(r.ravel()), 1e-30))
     worst = max(errs, key=errs.get) if errs else None
     tol = PARITY_TOL[args.dtype]
+    if tol is None:
+        from oracle.tolerances import FP8_GRAD, FP8_LOSS, FP8_OUT
+        tol = {"log_rates": FP8_OUT, "loss": FP8_LOSS, "grad": FP8_GRAD}
     ok = e_out < tol["log_rates"] and e_loss < tol["loss"] and (not errs or errs[worst] < tol["grad"])
     return {"what": f"one fwd+bwd of the whole benched batch ({pixels.shape[0]} clips, the timed step's dispatch) at "
                     "the initial weights: HIP path vs the CPU fp32 oracle (oracle/cpu_ref.py)",
@@ -322,6 +357,245 @@ def _param_digest(model, dev):
     return torch.stack(vals).to(dev)
 
 
+def _setup(spec, dev, rank):
+    """Model, config, criterion and the synthetic batch of one workload (spec: model, neurons, dtype,
+    frames, freeze, lr, loss, batch)."""
+    from vspike import VideoMAE, load_run_config, make_criterion
+    cfg_dir = os.path.join(ROOT, "video-spike_amd", "config")
+    config = load_run_config(os.path.join(cfg_dir, "model", spec["model"] + ".yaml"),
+                             os.path.join(cfg_dir, "train", "vmae_video.yaml"))
+    config["model"]["decoder"]["output_dim"] = 100 * spec["neurons"]       # src/train.py:41
+    config["model"]["compute_dtype"] = spec["dtype"]
+    if spec.get("frames"):
+        bbk = dict(config["model"].get("backbone") or {})
+        bbk["num_frames"] = spec["frames"]
+        config["model"]["backbone"] = bbk
+    config["model"]["freeze_encoder"] = bool(spec["freeze"])
+    if spec.get("lr") is not None:
+        config["optimizer"]["lr"] = spec["lr"]
+    config["training"]["loss"] = spec["loss"]
+    criterion = make_criterion(config)
+    torch.manual_seed(1234)                      # identical replicas (GradExchange also broadcasts)
+    model = VideoMAE(config["model"]).to(dev)
+    bb = model.backbone
+    B = spec["batch"] if spec.get("batch") else int(config["training"]["train_batch_size"])
+    g = torch.Generator(device=dev).manual_seed(100 + rank)             # each rank its own clips
+    pixels = torch.randn(B, bb.num_frames, bb.num_channels, bb.image_size, bb.image_size, device=dev, generator=g)
+    lam = torch.exp(torch.randn(B, 100, spec["neurons"], device=dev, generator=g) - 2.0).clamp(0.01, 5.0)
+    target = torch.poisson(lam, generator=g)
+    return config, criterion, model, B, pixels, target
+
+
+def _barrier_sync(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def _train_and_time(model, config, criterion, pixels, target, world, rank, dev, steps, warmup, profile_steps,
+                    graph=False, tag=""):
+    """W warm-up steps, EXACTLY `steps` timed steps between barrier + synchronize (max over ranks),
+    then the instrumented pass (per-kernel hipEvent timers, dW products in order)."""
+    from vspike import ops
+    from vspike import _lib as L
+    from vspike.dp import GradExchange
+    from vspike.trainer import build_optimizer, Trainer
+    total = warmup + steps + profile_steps + (1 if profile_steps > 0 else 0)  # + the pass's re-warm step
+    opt, sched = build_optimizer(model, config, total_steps=total, world=world)
+    exchange = GradExchange(model) if world > 1 else None
+    trainer = Trainer(model, opt, sched, criterion=criterion, exchange=exchange)
+    for _ in range(warmup):
+        trainer.step(pixels, target)
+    _barrier_sync(world)
+    if rank == 0:
+        _progress(f"{tag}warm-up done ({warmup} steps); timing {steps} steps")
+    L.dispatch_reset()
+    step_fn = trainer.step
+    if graph:
+        if world > 1:
+            raise SystemExit("bench.py --graph: the data-parallel exchange is not captured (N=1 only)")
+        from vspike.graph import GraphedStep
+        graphed = GraphedStep(trainer, pixels, target)     # the capture counts one step's dispatch
+        step_fn = graphed.step
+        _barrier_sync(world)
+    t0 = time.perf_counter()
+    losses = []
+    for _ in range(steps):
+        losses.append(step_fn(pixels, target))
+    _barrier_sync(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(losses[-1].item())
+    dispatch = {k: round(v / (1 if graph else steps), 2) for k, v in L.dispatch_counts().items() if v}
+    replicas_equal = None
+    if world > 1:   # every rank ends with the same weights (the exchange kept the replicas in sync)
+        hi = _param_digest(model, dev)
+        lo = -hi
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)       # max and min over ranks agree iff all equal
+        dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+        replicas_equal = bool(torch.equal(hi, -lo))
+
+    # ---- instrumented pass (not part of `value`): every kernel class timed on its own stream
+    kern = {}
+    if profile_steps > 0:
+        # side stream off for this pass: a weight-gradient product overlapped with the main stream's
+        # kernels is timed from its launch to its end, including the time it waits for CUs that an
+        # attention launch holds (2-3x its own duration); in order, every launch is timed alone
+        serial = hasattr(model, "set_side_stream")
+        if serial:
+            model.set_side_stream(False)
+        trainer.step(pixels, target)
+        _barrier_sync(world)
+        ops.timing_enable((1 << len(L.TIMER_NAMES)) - 1)
+        for _ in range(profile_steps):
+            trainer.step(pixels, target)
+        _barrier_sync(world)
+        for tid, name in enumerate(L.TIMER_NAMES):
+            kern[name] = ops.timing_collect(tid, with_bytes=True)
+        ops.timing_enable(0)
+        if serial:
+            model.set_side_stream(True)
+    return {"elapsed": elapsed, "final_loss": final_loss, "dispatch": dispatch, "replicas_equal": replicas_equal,
+            "kern": kern, "trainer": trainer}
+
+
+def _roofline(kern, profile_steps, bb, B, dtype):
+    """Per-kernel-class entries against their bounds, and the dominant one (most kernel time per step)."""
+    N, H, Lyr = bb.num_tokens, bb.num_attention_heads, bb.num_hidden_layers
+    D0, F0 = bb.hidden_size, bb.intermediate_size
+    fwd_flop = 4.0 * B * H * N * N * 64                 # QK^T + PV per launch (one layer)
+    peak_mfma = PEAK_F32_TFLOPS if dtype == "fp32" else PEAK_BF16_TFLOPS   # fp8: attention + backward are bf16
+    roof_all = {}
+    for name, (n, ms, nbytes) in kern.items():
+        if not n:
+            continue
+        per_step = n / profile_steps
+        avg_s = ms / n / 1e3
+        if name in ("attn_fwd", "attn_bwd"):
+            work = fwd_flop if name == "attn_fwd" else 2.5 * fwd_flop      # BASELINE.md convention
+            ach = work / avg_s / 1e12
+            ent = {"bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 2), "peak": peak_mfma,
+                   "frac": round(ach / peak_mfma, 4), "work_per_launch": work}
+        else:
+            ach = nbytes / (ms / 1e3) / 1e9                                 # bytes-weighted over launches
+            ent = {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                   "frac": round(ach / PEAK_HBM_GBS, 4), "work_per_launch": round(nbytes / n, 0)}
+            prod = {"fwd_qkv": 3 * D0 * D0, "fwd_proj": D0 * D0, "fwd_fc1": F0 * D0, "fwd_fc2": D0 * F0,
+                    "dx_qkv": 3 * D0 * D0, "dx_proj": D0 * D0, "dx_fc1": F0 * D0, "dx_fc2": D0 * F0,
+                    "dw_qkv": 3 * D0 * D0, "dw_proj": D0 * D0, "dw_fc1": F0 * D0, "dw_fc2": D0 * F0}.get(name)
+            if prod is not None:
+                # the product's MFMA side (2 M N K flop per launch) against the peak of its dtype (the fp8
+                # forward products: the 5 PF MX-FP8 peak)
+                fl = 2.0 * B * N * prod
+                pk = PEAK_FP8_TFLOPS if (dtype == "fp8" and name.startswith("fwd_")) else peak_mfma
+                tf = fl * Lyr / (ms / profile_steps / 1e3) / 1e12   # one product per layer per step
+                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2), "mfma_peak": pk,
+                            "mfma_frac": round(tf / pk, 4)})
+            if name in ("fwd_mlp", "dx_mlp"):
+                # the fused MLP kernels sit near the ridge (~300 flop/B): their MFMA side as well
+                # (fwd: h2 W1^T and a W2^T; dx: h2 W1^T recomputed and dy W2 = 4 M D F flop per launch)
+                fl = 4.0 * B * N * D0 * F0
+                tf = fl * Lyr / (ms / profile_steps / 1e3) / 1e12
+                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2),
+                            "mfma_frac": round(tf / peak_mfma, 4)})
+        ent.update({"ms_per_step": round(ms / profile_steps, 4), "launches_per_step": round(per_step, 2),
+                    "avg_launch_us": round(1e3 * ms / n, 2)})
+        roof_all[name] = ent
+    if not roof_all:
+        return roof_all, None
+    dom = max(roof_all, key=lambda k: roof_all[k]["ms_per_step"])
+    r = roof_all[dom]
+    traffic, tsrc = _traffic_lookup(dom, r["launches_per_step"]) if dom in TRAFFIC_CLASSES else (None, None)
+    roofline = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
+                "frac": r["frac"], "traffic": traffic, "traffic_source": tsrc,
+                "avg_launch_ms": round(r["avg_launch_us"] / 1e3, 4), "work_per_launch": r["work_per_launch"],
+                "timing": f"hipEvents per launch on the launch stream, {profile_steps} instrumented steps "
+                          "(weight-gradient products in order on the main stream: each launch timed alone)",
+                "pmc": _pmc_lookup(dom), "all": roof_all}
+    return roof_all, roofline
+
+
+def _train_flops_per_clip(bb, neurons):
+    """Algorithmic train FLOPs per clip (BASELINE.md convention: train = 3 x forward)."""
+    N, Lyr, D, F, K = bb.num_tokens, bb.num_hidden_layers, bb.hidden_size, bb.intermediate_size, bb.patch_dim
+    fwd_clip = Lyr * (2 * N * D * 3 * D + 2 * N * D * D + 4 * N * D * F + 4 * N * N * D) + 2 * N * K * D \
+        + 2 * N * D * 64 + 2 * 64 * 100 * neurons
+    return 3.0 * fwd_clip
+
+
+def _oracle_cfg(bb):
+    from oracle import cpu_ref
+    return cpu_ref.ViTCfg(**{k: getattr(bb, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
+                                                         "tubelet_size", "hidden_size", "num_hidden_layers",
+                                                         "num_attention_heads", "intermediate_size",
+                                                         "layer_norm_eps")})
+
+
+# bars of the C3 sub-record's micro-batch check (the bf16 log-rate bar of the full-batch check; the
+# loss of two clips is a mean over 102,400 terms)
+C3_CHECK_TOL = {"log_rates": 7e-3, "loss": 1e-3}
+
+
+def c3_subrecord(args, world, rank, dev):
+    """BASELINE C3 in the same run: ViT-Base/16 (the reference plugin's own width,
+    /root/reference/src/model/videomae.py:7,13) at the reference's 128 clips per process
+    (config/train/vmae_video.yaml:20), n = 512, encoder trainable, bf16: timed steps at the benched
+    dispatch plus a CPU-oracle check of one micro-batch (2 clips) of the benched forward's log-rates
+    and Poisson loss.  lr 5e-8: the synthetic C3 setup diverges at the config's 5e-5 (DESIGN.md section
+    1), which the throughput does not depend on."""
+    spec = {"model": "vmae_video", "neurons": 512, "dtype": "bf16", "frames": None, "freeze": False,
+            "lr": 5e-8, "loss": "poisson", "batch": args.c3_batch}
+    config, criterion, model, B, pixels, target = _setup(spec, dev, rank)
+    bb = model.backbone
+    check = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_ref
+        init = {k: v.detach().cpu().numpy() for k, v in model.reference_state_dict(modern_names=True).items()}
+        with torch.no_grad():
+            out0 = model(pixels)
+            gl = out0[:2].float().cpu()
+            gloss = float(criterion(out0[:2], target[:2]))
+        del out0
+        t0 = time.perf_counter()
+        P = cpu_ref.to_torch(init, requires_grad=False)
+        with torch.no_grad():
+            ref = cpu_ref.videomae_plugin_forward(pixels[:2].cpu(), P, _oracle_cfg(bb), False)
+            rloss = float(cpu_ref.poisson_nll_mean(ref, target[:2].cpu()))
+        e_out = float((gl - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        e_loss = abs(gloss - rloss) / abs(rloss)
+        check = {"what": f"clips 0..1 of the benched {B}-clip forward (log-rates are per clip) and their Poisson "
+                         "loss vs the CPU fp32 oracle (oracle/cpu_ref.py) at the initial weights",
+                 "log_rates_maxrel": round(e_out, 7), "loss_rel": round(e_loss, 8), "tolerance": C3_CHECK_TOL,
+                 "ok": bool(e_out < C3_CHECK_TOL["log_rates"] and e_loss < C3_CHECK_TOL["loss"]),
+                 "cpu_seconds": round(time.perf_counter() - t0, 1)}
+        del P
+        _progress(f"C3 micro-batch check: {check}")
+    run = _train_and_time(model, config, criterion, pixels, target, world, rank, dev, args.c3_steps, args.c3_warmup,
+                          args.c3_profile_steps, tag="C3: ")
+    roof_all, roofline = _roofline(run["kern"], args.c3_profile_steps, bb, B, "bf16")
+    clips = world * B * args.c3_steps
+    out = {"metric": "clips/sec (16-frame 224x224) train step", "value": round(clips / run["elapsed"], 3),
+           "unit": "clips/sec", "n_gpus": world, "steps": args.c3_steps, "warmup": args.c3_warmup,
+           "ms_per_step": round(1e3 * run["elapsed"] / args.c3_steps, 3), "dtype": "bf16",
+           "config": {"workload": f"C3 ViT-Base/16 {bb.num_frames}x{bb.image_size}x{bb.image_size} -> 512 neurons, "
+                                  "encoder+head fwd+bwd+AdamW", "model": "vmae_video", "global_batch": B * world,
+                      "clips_per_gpu": B, "seq_len": bb.num_tokens, "parallelism": f"dp{world}", "lr": 5e-8},
+           "model_tflops": round(_train_flops_per_clip(bb, 512) * clips / run["elapsed"] / 1e12, 2),
+           "check": check, "final_loss": round(run["final_loss"], 6), "replicas_equal": run["replicas_equal"],
+           "dispatch_per_step": run["dispatch"],
+           "products": {k: {f: v[f] for f in ("ms_per_step", "avg_launch_us", "mfma_frac") if f in v}
+                        for k, v in roof_all.items()},
+           "roofline": {k: roofline[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac",
+                                                 "avg_launch_ms")} if roofline else None}
+    out["mfma_util_pct"] = round(100.0 * out["model_tflops"] / PEAK_BF16_TFLOPS, 2)
+    del run, model
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -342,33 +616,12 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from vspike import VideoMAE, load_run_config, make_criterion, ops
     from vspike import _lib as L
-    from vspike.dp import GradExchange
-    from vspike.trainer import build_optimizer, Trainer
 
-    cfg_dir = os.path.join(ROOT, "video-spike_amd", "config")
-    config = load_run_config(os.path.join(cfg_dir, "model", args.model + ".yaml"),
-                             os.path.join(cfg_dir, "train", "vmae_video.yaml"))
-    config["model"]["decoder"]["output_dim"] = 100 * args.neurons       # src/train.py:41
-    config["model"]["compute_dtype"] = args.dtype
-    if args.frames:
-        bbk = dict(config["model"].get("backbone") or {})
-        bbk["num_frames"] = args.frames
-        config["model"]["backbone"] = bbk
-    config["model"]["freeze_encoder"] = bool(args.freeze)
-    if args.lr is not None:
-        config["optimizer"]["lr"] = args.lr
-    config["training"]["loss"] = args.loss
-    criterion = make_criterion(config)
-    torch.manual_seed(1234)                      # identical replicas (GradExchange also broadcasts)
-    model = VideoMAE(config["model"]).to(dev)
+    spec = {"model": args.model, "neurons": args.neurons, "dtype": args.dtype, "frames": args.frames,
+            "freeze": args.freeze, "lr": args.lr, "loss": args.loss, "batch": args.batch}
+    config, criterion, model, B, pixels, target = _setup(spec, dev, rank)
     bb = model.backbone
-    B = args.batch if args.batch else int(config["training"]["train_batch_size"])
-    g = torch.Generator(device=dev).manual_seed(100 + rank)             # each rank its own clips
-    pixels = torch.randn(B, bb.num_frames, bb.num_channels, bb.image_size, bb.image_size, device=dev, generator=g)
-    lam = torch.exp(torch.randn(B, 100, args.neurons, device=dev, generator=g) - 2.0).clamp(0.01, 5.0)
-    target = torch.poisson(lam, generator=g)
     do_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     parity = None
     L.dispatch_reset()
@@ -383,140 +636,37 @@ def main():
                    "grads": _reference_grads(model)}
         model.zero_grad(set_to_none=True)
         del out0, loss0
-    total = args.warmup + args.steps + args.profile_steps + (1 if args.profile_steps > 0 else 0)  # + the pass's re-warm step
-    opt, sched = build_optimizer(model, config, total_steps=total, world=world)
-    exchange = GradExchange(model) if world > 1 else None
-    trainer = Trainer(model, opt, sched, criterion=criterion, exchange=exchange)
 
-    def barrier_sync():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        trainer.step(pixels, target)
-    barrier_sync()
-    if rank == 0:
-        _progress(f"warm-up done ({args.warmup} steps); timing {args.steps} steps")
-    L.dispatch_reset()
-    step_fn = trainer.step
-    if args.graph:
-        if world > 1:
-            raise SystemExit("bench.py --graph: the data-parallel exchange is not captured (N=1 only)")
-        from vspike.graph import GraphedStep
-        graphed = GraphedStep(trainer, pixels, target)     # the capture counts one step's dispatch
-        step_fn = graphed.step
-        barrier_sync()
-    t0 = time.perf_counter()
-    losses = []
-    for _ in range(args.steps):
-        losses.append(step_fn(pixels, target))
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    final_loss = float(losses[-1].item())
-    dispatch = {k: round(v / (1 if args.graph else args.steps), 2) for k, v in L.dispatch_counts().items() if v}
-    replicas_equal = None
-    if world > 1:   # every rank ends with the same weights (the exchange kept the replicas in sync)
-        hi = _param_digest(model, dev)
-        lo = -hi
-        dist.all_reduce(hi, op=dist.ReduceOp.MAX)       # max and min over ranks agree iff all equal
-        dist.all_reduce(lo, op=dist.ReduceOp.MAX)
-        replicas_equal = bool(torch.equal(hi, -lo))
-
-    # ---- instrumented pass (not part of `value`): every kernel class timed on its own stream
-    kern = {}
-    if args.profile_steps > 0:
-        # side stream off for this pass: a weight-gradient product overlapped with the main stream's
-        # kernels is timed from its launch to its end, including the time it waits for CUs that an
-        # attention launch holds (2-3x its own duration); in order, every launch is timed alone
-        serial = hasattr(model, "set_side_stream")
-        if serial:
-            model.set_side_stream(False)
-        trainer.step(pixels, target)
-        barrier_sync()
-        ops.timing_enable((1 << len(L.TIMER_NAMES)) - 1)
-        for _ in range(args.profile_steps):
-            trainer.step(pixels, target)
-        barrier_sync()
-        for tid, name in enumerate(L.TIMER_NAMES):
-            kern[name] = ops.timing_collect(tid, with_bytes=True)
-        ops.timing_enable(0)
-        if serial:
-            model.set_side_stream(True)
-
+    run = _train_and_time(model, config, criterion, pixels, target, world, rank, dev, args.steps, args.warmup,
+                          args.profile_steps, graph=args.graph)
+    elapsed, final_loss, replicas_equal, dispatch = run["elapsed"], run["final_loss"], run["replicas_equal"], \
+        run["dispatch"]
     clips = world * B * args.steps
     value = clips / elapsed
-    N, H, Lyr = bb.num_tokens, bb.num_attention_heads, bb.num_hidden_layers
-    D0, F0 = bb.hidden_size, bb.intermediate_size
-    fwd_flop = 4.0 * B * H * N * N * 64                 # QK^T + PV per launch (one layer)
-    peak_mfma = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS   # fp8: attention + backward are bf16
-    roof_all = {}
-    for name, (n, ms, nbytes) in kern.items():
-        if not n:
-            continue
-        per_step = n / args.profile_steps
-        avg_s = ms / n / 1e3
-        if name in ("attn_fwd", "attn_bwd"):
-            work = fwd_flop if name == "attn_fwd" else 2.5 * fwd_flop      # BASELINE.md convention
-            ach = work / avg_s / 1e12
-            ent = {"bound": "mfma", "unit": "TFLOP/s", "achieved": round(ach, 2), "peak": peak_mfma,
-                   "frac": round(ach / peak_mfma, 4), "work_per_launch": work}
-        else:
-            ach = nbytes / (ms / 1e3) / 1e9                                 # bytes-weighted over launches
-            ent = {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-                   "frac": round(ach / PEAK_HBM_GBS, 4), "work_per_launch": round(nbytes / n, 0)}
-            prod = {"fwd_qkv": 3 * D0 * D0, "fwd_proj": D0 * D0, "fwd_fc1": F0 * D0, "fwd_fc2": D0 * F0,
-                    "dx_qkv": 3 * D0 * D0, "dx_proj": D0 * D0, "dx_fc1": F0 * D0, "dx_fc2": D0 * F0,
-                    "dw_qkv": 3 * D0 * D0, "dw_proj": D0 * D0, "dw_fc1": F0 * D0, "dw_fc2": D0 * F0}.get(name)
-            if prod is not None:
-                # the product's MFMA side (2 M N K flop per launch) against the peak of its dtype (the fp8
-                # forward products: the 5 PF MX-FP8 peak)
-                fl = 2.0 * B * N * prod
-                pk = PEAK_FP8_TFLOPS if (args.dtype == "fp8" and name.startswith("fwd_")) else peak_mfma
-                tf = fl * Lyr / (ms / args.profile_steps / 1e3) / 1e12   # one product per layer per step
-                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2), "mfma_peak": pk,
-                            "mfma_frac": round(tf / pk, 4)})
-            if name in ("fwd_mlp", "dx_mlp"):
-                # the fused MLP kernels sit near the ridge (~300 flop/B): their MFMA side as well
-                # (fwd: h2 W1^T and a W2^T; dx: h2 W1^T recomputed and dy W2 = 4 M D F flop per launch)
-                fl = 4.0 * B * N * bb.hidden_size * bb.intermediate_size
-                tf = fl * Lyr / (ms / args.profile_steps / 1e3) / 1e12
-                ent.update({"mfma_flop_per_launch": fl, "mfma_tflops": round(tf, 2),
-                            "mfma_frac": round(tf / peak_mfma, 4)})
-        ent.update({"ms_per_step": round(ms / args.profile_steps, 4), "launches_per_step": round(per_step, 2),
-                    "avg_launch_us": round(1e3 * ms / n, 2)})
-        roof_all[name] = ent
-    roofline = None
-    if roof_all:
-        dom = max(roof_all, key=lambda k: roof_all[k]["ms_per_step"])
-        r = roof_all[dom]
-        traffic, tsrc = _traffic_lookup(dom, r["launches_per_step"]) if dom in TRAFFIC_CLASSES else (None, None)
-        roofline = {"bound": r["bound"], "kernel": dom, "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"],
-                    "frac": r["frac"], "traffic": traffic, "traffic_source": tsrc,
-                    "avg_launch_ms": round(r["avg_launch_us"] / 1e3, 4), "work_per_launch": r["work_per_launch"],
-                    "timing": f"hipEvents per launch on the launch stream, {args.profile_steps} instrumented steps "
-                              "(weight-gradient products in order on the main stream: each launch timed alone)",
-                    "pmc": _pmc_lookup(dom), "all": roof_all}
-    # algorithmic train FLOPs per clip (BASELINE.md convention: train = 3 x forward)
-    D, F, K = bb.hidden_size, bb.intermediate_size, bb.patch_dim
-    fwd_clip = Lyr * (2 * N * D * 3 * D + 2 * N * D * D + 4 * N * D * F + 4 * N * N * D) + 2 * N * K * D \
-        + 2 * N * D * 64 + 2 * 64 * 100 * args.neurons
-    step_tflops = 3 * fwd_clip * B * world * args.steps / elapsed / 1e12
+    N = bb.num_tokens
+    peak_mfma = PEAK_F32_TFLOPS if args.dtype == "fp32" else PEAK_BF16_TFLOPS
+    _, roofline = _roofline(run["kern"], args.profile_steps, bb, B, args.dtype)
+    step_tflops = _train_flops_per_clip(bb, args.neurons) * B * world * args.steps / elapsed / 1e12
 
     cpu = None
     if do_cpu:
-        from oracle import cpu_ref
-        ccfg = cpu_ref.ViTCfg(**{k: getattr(bb, k) for k in ("image_size", "patch_size", "num_channels", "num_frames",
-                                                             "tubelet_size", "hidden_size", "num_hidden_layers",
-                                                             "num_attention_heads", "intermediate_size",
-                                                             "layer_norm_eps")})
+        ccfg = _oracle_cfg(bb)
         cpu, _ = cpu_baseline(ccfg, init_params, pixels[:4].cpu(), target[:4].cpu(), args.cpu_seconds)
         parity = full_batch_parity(ccfg, init_params, pixels.cpu(), target.cpu(), gpu_par, args)
+
+    c3 = None
+    want_c3 = (not args.no_c3 and args.model == "vmae_tiny" and args.dtype == "bf16" and not args.graph and
+               not args.freeze and args.loss == "poisson")
+    if want_c3:
+        del run, model, pixels, target
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        try:
+            c3 = c3_subrecord(args, world, rank, dev)
+        except Exception as exc:       # recorded in the line; the C2 measurement stands on its own
+            c3 = {"error": f"{type(exc).__name__}: {exc}"}
+            _progress(f"C3 sub-record failed: {c3['error']}")
 
     if rank == 0:
         workload = ("C5 ViT-Base/16 encoder (no temporal transformer: no reference code)"
@@ -538,7 +688,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
             "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
             "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
-            "knobs_nondefault": L.knobs_nondefault(),
+            "knobs_nondefault": L.knobs_nondefault(), "c3": c3,
         }
         if args.graph:
             line["step_mode"] = "hipGraph replay (vspike.graph.GraphedStep)"

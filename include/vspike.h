@@ -154,7 +154,10 @@ int vs_gemm_ln_bwd(const vs_gemm_desc* d, const float* x, int64_t ldx, const flo
  * vs_mlp_bwd_da: its backward's GELU' product with the pre-activation RECOMPUTED from h2 (the same
  *   MFMA chain as the forward):  da = (dy W2) * gelu'(h2 W1^T + b1)  and  a = gelu(h2 W1^T + b1),
  *   dy [M, D] bf16 (dx' of the block), da / a [M, F] bf16 (the operands of dh2 = da W1, dW1 = da^T h2,
- *   dW2 = dy^T a).  GELU: Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7, below bf16's 2^-9).
+ *   dW2 = dy^T a).  GELU: x * sigmoid(x (k1 + k3 x^2 + k5 x^4)), a minimax fit of x Phi(x) with
+ *   |error| <= 2.5e-5 (derivative <= 1.1e-4), below the bf16 rounding (2^-9 relative) every stored
+ *   value gets; the unfused bf16 path (VSPIKE_MLP_FUSE=0) uses the A&S 7.1.26 erf (<= 1.5e-7), so the
+ *   A/B switch changes the GELU's last bits as well as the kernels.
  * Both need vs_mlp_fused_ok(M, D, F): D = 192 (ViT-Tiny), F % 64 == 0, F <= 3072. */
 /* ------------------------------------------------------------------------------------------
  * MX-FP8 (BASELINE C5 "fp8 MFMA"): OCP e4m3 elements with one E8M0 power-of-two scale per 32

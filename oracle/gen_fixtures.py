@@ -322,6 +322,29 @@ def gen_vit_base32f():
     print("vit_base32f", fx["loss"])
 
 
+def gen_vit_base2l_b16():
+    """C3 at its benched dispatch: the reference plugin's width (videomae-base:
+    d768, 12 heads, videomae.py:7-8; C3's n = 512) with two layers at B = 16 -> M = 25,088 token rows,
+    trainable: forward and every gradient (summarised).  The HIP test forces the 128-clip choices
+    (f32 dh + LayerNorm' launches, the big-tile products, the dW split plan of 256 slots) at this
+    batch; two layers exercise the block-to-block gradient hand-off."""
+    cfg = cpu_ref.ViTCfg(num_hidden_layers=2)
+    B, enc_out, n = 16, 64, 512
+    torch.manual_seed(0)
+    m = _RefVideoMAEHead(cfg, enc_out, n)
+    _load_vit(m, cfg, enc_out, n)
+    m.freeze = False
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B, seed=768))
+    y = torch.from_numpy(prng.spike_targets(768, (B, 100, n)))
+    out = m(px)
+    loss = torch.nn.PoissonNLLLoss(reduction="none", log_input=True)(out, y).mean()
+    loss.backward()
+    fx = {"log_rates": out.detach().numpy(), "loss": np.array([loss.item()])}
+    fx.update(_grads_summary_small({k: p.grad for k, p in m.named_parameters() if ".key.bias" not in k}))
+    np.savez_compressed(os.path.join(OUT, "vit_base2l_b16.npz"), **fx)
+    print("vit_base2l_b16", fx["loss"])
+
+
 def gen_vit_base1l():
     """The reference plugin's real width (videomae-base: d768, 12 heads, videomae.py:7-8; C3's
     n=512) with one layer, full 1568 tokens, B=1: trainable forward+backward, and a 3-step curve in

@@ -239,6 +239,22 @@ def test_cached_buffers_two_forwards_before_backward():
     assert torch.equal(o1.detach(), o1c)
 
 
+def test_pixels_modified_before_backward_are_refused():
+    """bf16 training gathers the pixels again in the patch-embedding weight gradient (no cols saved):
+    an in-place write to the caller's input between forward and backward must raise (as autograd
+    does for a modified saved tensor) instead of giving the next batch's gradient."""
+    from vspike import poisson_nll_mean
+    cfg, B, n = cpu_ref.VIT_SMALL_FIXTURE, 2, 16
+    m = _vit_model(cfg, 64, n, dtype="bf16")
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, B)).to(DEV)
+    y = torch.from_numpy(prng.spike_targets(1, (B, 100, n))).to(DEV)
+    poisson_nll_mean(m(px), y).backward()              # unchanged input: fine
+    loss = poisson_nll_mean(m(px), y)
+    px.mul_(0.5)                                       # a loader refilling its buffer in place
+    with pytest.raises(RuntimeError, match="modified in place"):
+        loss.backward()
+
+
 def test_eval_epoch_matches_reference_eval_flow():
     """Trainer.eval_epoch (src/trainer/base.py:161-206) on two sessions: eval_loss and the
     per-session bps / rsquared means against the CPU restatement of the same flow."""

@@ -333,6 +333,82 @@ def test_gemm_big_tile_path(bkc, shape, epi):
     assert rel(out.float(), ref) < tol
 
 
+# the C3 block's products at the bench's 128 clips (M = 200,704 token rows, D = 768, F = 3072), with the
+# operand layouts and epilogues vit_exec.hip launches: forward (W [N, K], K-contiguous) and dX (W read
+# transposed: [K, N] storage)
+C3_PRODUCTS = {
+    "fwd_qkv": ((2304, 768), True, "bias"), "fwd_proj": ((768, 768), True, "bias_res"),
+    "fwd_fc1": ((3072, 768), True, "gelu_grad"), "fwd_fc2": ((768, 3072), True, "bias_res"),
+    "dx_fc2": ((3072, 768), False, "mul_aux"), "dx_fc1": ((768, 3072), False, "none_f32"),
+    "dx_proj": ((768, 768), False, "none_bf16"), "dx_qkv": ((768, 2304), False, "none_f32"),
+    "patch": ((768, 1536), True, "bias_pos"),
+}
+
+
+@pytest.mark.parametrize("prod", sorted(C3_PRODUCTS))
+def test_gemm_big_tile_c3_bench128(prod):
+    """Every C3 block product at its benched size (200,704 rows: VERDICT r4 item 1) on the big-tile
+    path, against fp64 on the device from the same bf16 operands; the dispatch counter shows the
+    big-tile kernel ran.  f32 outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (one bf16 rounding)."""
+    from vspike import ops, _lib as L
+    (N, K), bkc, epi = C3_PRODUCTS[prod]
+    M = 200704
+    g = torch.Generator(device=DEV).manual_seed(N + 7 * K)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV, generator=g)
+    b_dev, ldb = (w, K) if bkc else (w.t().contiguous(), N)
+    kw = dict(M=M, N=N, K=K, a_kcontig=True, b_kcontig=bkc, lda=K, ldb=ldb, ldc=N)
+    ref = x.double() @ w.double().t()
+    L.dispatch_reset()
+    if epi == "bias_res":
+        res = torch.randn(M, N, device=DEV, generator=g)
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_RESIDUAL, bias=bias, residual=res, ld_residual=N, **kw)
+        ref, tol = ref.add_(bias.double()).add_(res.double()), 1e-5
+        del res
+    elif epi == "bias":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS, bias=bias, **kw)
+        ref, tol = ref.add_(bias.double()), 8e-3
+    elif epi == "bias_pos":   # the patch embedding: + bias + sinusoid[token % 1568]
+        pos = ops.sinusoid_table(1568, N, DEV)
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_POS, bias=bias, pos=pos, pos_rows=1568, **kw)
+        ref = ref.add_(bias.double()).view(-1, 1568, N).add_(pos.double()).view(M, N)
+        tol = 1e-5
+    elif epi == "none_f32":
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm(x, b_dev, out, **kw)
+        tol = 1e-5
+    elif epi == "none_bf16":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, **kw)
+        tol = 8e-3
+    elif epi == "gelu_grad":   # bf16 forward: gelu(pre) out, gelu'(pre) into aux
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        gp = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_GRAD, bias=bias, aux_out=gp,
+                 ld_aux_out=N, **kw)
+        pre = ref.add_(bias.double())
+        torch.cuda.synchronize()
+        xp = pre.to(torch.bfloat16).double().requires_grad_()
+        gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        assert rel(gp.float(), gg) < 1.5e-2
+        del xp, gg, gp
+        ref, tol = torch.nn.functional.gelu(pre), 8e-3
+    else:                      # mul_aux: da = (dx' W2) * gelu'(pre), the stored factor
+        aux = (torch.rand(M, N, device=DEV, generator=g) * 1.2 - 0.1).to(torch.bfloat16)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_MUL_AUX, aux_in=aux, ld_aux_in=N, **kw)
+        ref, tol = ref.mul_(aux.double()), 8e-3
+    torch.cuda.synchronize()
+    assert L.dispatch_counts()["gemm_big"] == 1, L.dispatch_counts()
+    err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"\n[{prod}] M={M} N={N} K={K} max err / max|ref| = {err:.3e}")
+    assert err < tol
+
+
 @pytest.mark.parametrize("M", [25088, 9000])
 def test_patch_embed_gemm_pos_on_row_slab(M):
     """The patch embedding x0 = cols W^T + b + sinusoid[token] (K = 1536, N = 192, pos rows = 1568)
@@ -474,7 +550,10 @@ def test_gemm_ln_bwd_fused_bench_rows(knobs, K, wv):
 
 
 @pytest.mark.parametrize("shape", [(192, 768, 200704), (768, 192, 200704), (192, 192, 200704), (576, 192, 200704),
-                                   (192, 1536, 200704)])
+                                   (192, 1536, 200704),
+                                   # C3 (videomae-base): dW2, dW1, dWqkv, dWproj and the patch dW from cols
+                                   (768, 3072, 200704), (3072, 768, 200704), (2304, 768, 200704),
+                                   (768, 768, 200704), (768, 1536, 200704)])
 def test_dw_bench128_split_plan(shape):
     """The weight gradients at the benched 128 clips (K = 200,704 tokens): the dW-tile kernel with the
     split plan the timed step uses and its fixed-order reduce, against fp64 on the device; bitwise
@@ -875,7 +954,7 @@ def test_patch_embed_fused_matches_im2col_gemm(knobs, D, geo):
         assert rel(out, ref.double()) < 1e-5
 
 
-@pytest.mark.parametrize("D", [64, 128, 192])
+@pytest.mark.parametrize("D", [64, 128, 192, 768])
 @pytest.mark.parametrize("geo", [(2, 16, 3, 224, 224), (3, 8, 3, 112, 112), (1, 4, 1, 32, 48), (128, 16, 3, 224, 224)])
 def test_patch_embed_dw_matches_im2col_dw(D, geo):
     """vs_patch_embed_dw (the tubelet gather in the dW kernel's B-operand load, no cols) against
@@ -883,11 +962,11 @@ def test_patch_embed_dw_matches_im2col_dw(D, geo):
     split plan, MFMA order and fixed-order split reduce, so dW and db agree to the last bit (both
     accumulate into non-zero gradients); and against fp64.  Geometries: 2 bench clips, a ragged token
     count (3 x 4 x 7 x 7 = 1,176: a partial last 64-token step), 12 tokens (one partial step), and the
-    bench's 128 clips (200,704 tokens) with D = 192."""
+    bench's 128 clips (200,704 tokens) at D = 192 (C2) and D = 768 (C3's width)."""
     from vspike import ops, _lib as L
     B, F, C, H, W = geo
-    if B == 128 and D != 192:
-        pytest.skip("bench batch at the ViT-Tiny width only")
+    if B == 128 and D not in (192, 768):
+        pytest.skip("bench batch at the ViT-Tiny / ViT-Base widths only")
     t, p = 2, 16
     n_tok = (F // t) * (H // p) * (W // p)
     M, K = B * n_tok, C * t * p * p

@@ -248,6 +248,44 @@ def test_vit_tiny12_b16_encoder_only_curve(golden, dtype, dispatch):
     assert rel.max() < (1e-5 if dtype == "fp32" else BF16_ENC_CURVE)
 
 
+# kernel paths of the C3 (videomae-base width) bf16 step at the bench's 128 clips: every block product
+# on the big-tile kernel (D = 768 / F = 3072), the dW split plan, flash attention, the skinny head, and the
+# patch embedding as im2col + the big-tile GEMM (its dW from cols on the dW kernel)
+BENCH_PATHS_C3 = ("gemm_big", "gemm_dw", "gemm_skinny", "attn_fwd", "attn_bwd")
+
+
+@pytest.mark.parametrize("dtype,dispatch", [("fp32", "b16"), ("bf16", "b16"), ("bf16", "b128")])
+def test_vit_base2l_b16_benched_dispatch_forward_backward(golden, dtype, dispatch):
+    """C3 at its benched dispatch: the reference plugin's width (d768, 12 heads,
+    n = 512), 2 layers, B = 16 -> M = 25,088 token rows, against the reference's own forward/backward
+    (fixture vit_base2l_b16 from HF VideoMAEModel): log-rates, loss and every gradient.  "b128" forces
+    the 128-clip choices (bench128_dispatch: f32 dh + the LayerNorm' launch at D = 768, the 3-wave
+    attention backward); the dW split plan of the C3 products is the same at 25,088 and 200,704 tokens
+    (tests/test_gpu_ops.py::test_dw_bench128_split_plan checks it at 200,704)."""
+    from vspike import _lib as L
+    fx = golden("vit_base2l_b16.npz")
+    cfg, B, n = cpu_ref.ViTCfg(num_hidden_layers=2), 16, 512
+    L.dispatch_reset()
+    with (bench128_dispatch() if dispatch == "b128" else contextlib.nullcontext()):
+        m, g, out_err, loss_err, errs = _fwd_bwd_case(fx, cfg, B, n, dtype, px_seed=768, y_seed=768)
+    counts = {k: v for k, v in L.dispatch_counts().items() if v}
+    print(f"[{dtype} {dispatch}] dispatch {counts}")
+    if dtype == "fp32":
+        assert out_err < 1e-4 and loss_err < 1e-5
+        shapes = cpu_ref.vit_param_shapes(cfg, 64, n)
+        for k, v in g.items():
+            ok, msg = cpu_ref.compare_summary(k, v.reshape(shapes[k]), fx, rtol=1e-3, atol=1e-8)
+            assert ok, msg
+    else:
+        missing = [p for p in BENCH_PATHS_C3 if not counts.get(p)]
+        assert not missing, (missing, counts)
+        # 2 layers x (4 forward + 4 dX products) + the patch GEMM on the big-tile kernel
+        assert counts["gemm_big"] >= 2 * 8 + 1, counts
+        assert out_err < BF16_OUT and loss_err < BF16_LOSS
+        bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
+        assert not bad, bad
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_vit_base_32_frames_c5_encoder_geometry(golden, dtype):
     """BASELINE C5's encoder geometry: videomae-base width at 32 frames -> 3,136 tokens (24 * 128 + 64:

@@ -201,6 +201,21 @@ def test_vit_base_one_layer_matches_reference(golden):
     np.testing.assert_allclose(curve, fx["curve_frozen"], rtol=1e-4)
 
 
+def test_vit_base_two_layers_b16_forward_matches_reference(golden):
+    """C3's benched-dispatch fixture (videomae-base, 2 layers, B=16, n=512; vit_base2l_b16): log-rates
+    are per clip, so the oracle's forward of the first two clips pins it against the reference's
+    (the full-batch backward is the GPU test's job: ~90 s of CPU here)."""
+    fx = golden("vit_base2l_b16.npz")
+    cfg, n = cpu_ref.ViTCfg(num_hidden_layers=2), 512
+    P = cpu_ref.to_torch(cpu_ref.make_vit_params(cfg, 64, n), requires_grad=False)
+    px = torch.from_numpy(cpu_ref.make_pixels(cfg, 16, seed=768))[:2]
+    with torch.no_grad():
+        out = cpu_ref.videomae_plugin_forward(px, P, cfg, freeze_encoder=False)
+    ref = fx["log_rates"][:2]
+    # the head input is 1,204,224 wide: summation-order noise ~1e-5 absolute on values near zero
+    assert np.abs(out.numpy() - ref).max() <= 1e-5 * np.abs(ref).max() + 2e-5
+
+
 def test_k0_preprocess_oracle_matches_reference_processor(golden):
     """K0 (videomae.py:18-25): the restated PIL bilinear resize + HF rescale/normalise reproduce the
     HF image processor's output bit for bit (fixture made by oracle/gen_fixtures.py gen_k0)."""

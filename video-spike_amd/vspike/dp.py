@@ -133,6 +133,12 @@ class GradExchange:
         self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     # ---- end of backward ------------------------------------------------------------------------
+    def end_backward(self) -> None:
+        """Called by the model when its backward has handed over every gradient: the forward's
+        recorded DDP sync decision has been consumed (a stale flag could steer a later
+        backward whose forward bypassed the DDP wrapper)."""
+        self._fwd_sync = None
+
     def finish(self) -> None:
         """Flush partial buckets, reduce the non-sink gradients, and make the current stream wait."""
         if self.world > 1:

@@ -423,7 +423,8 @@ class VideoMAE(nn.Module):
                  bias=lh.view(head32, "enc_b"), workspace=ent["head_ws"])
         ops.linear(z, lh.view(head32, "dec_w"), r, bias=lh.view(head32, "dec_b"))
         state = _FwdState(act=act, structs=ent["structs"], enc_lp=enc_lp, head_lp=head_lp, x_flat_lp=x_flat_lp,
-                          x_final=ent["x_final"], B=B, pixels=pixels if "cols" not in act else None)
+                          x_final=ent["x_final"], B=B, pixels=pixels if "cols" not in act else None,
+                          pixels_version=pixels._version)
         ent["owner"] = weakref.ref(state)
         return r.view(B, 100, -1), state
 
@@ -583,9 +584,19 @@ class _VideoMAEFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, grad):
         mod = ctx.mod
-        g_enc, g_head = mod._run_backward(ctx.st, grad, *ctx.want)
+        st = ctx.st
+        if st is not None and st.get("pixels") is not None and st["pixels"]._version != st["pixels_version"]:
+            # the cols-free patch dW gathers the caller's pixels again here: an in-place
+            # write between forward and backward (a loader refilling its buffer) would silently give
+            # the next batch's gradient — refuse it the way autograd refuses a modified saved tensor
+            raise RuntimeError("VideoMAE backward: the input pixels were modified in place after the forward "
+                               "(the patch-embedding weight gradient reads them again); pass a tensor that "
+                               "stays unchanged until backward, or a copy")
+        g_enc, g_head = mod._run_backward(st, grad, *ctx.want)
         ctx.st = None
         sink = mod.grad_sink
+        if sink is not None and hasattr(sink, "end_backward"):
+            sink.end_backward()
         if sink is not None and not getattr(sink, "return_grads", False):
             return None, None, None, None      # the sink owns .grad (all-reduced in place)
         return None, g_enc, g_head, None
