@@ -173,6 +173,12 @@ def cpu_baseline(cfg, params, pixels, target, seconds, reps=10):
                     p.grad = None
                 return loss.detach()
             return run
+        if threads != share and threads > 4 * share:
+            # the GPU box: os.cpu_count() counts the 256-CPU host, the job's quota is 16 CPUs; a probe
+            # forward at 256 threads took 42 s there (r05) — recorded as skipped without running it
+            skipped[str(threads)] = (f"os.cpu_count() = {threads} threads on a {share}-CPU share: oversubscribed "
+                                     "(the process's CPU quota is smaller than the host's count), not run")
+            continue
         if threads != share:   # probe: one B=1 forward against the share's median
             t0 = time.perf_counter()
             cell(1, "fwd")()

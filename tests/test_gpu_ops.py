@@ -968,6 +968,8 @@ def test_patch_embed_dw_matches_im2col_dw(D, geo):
     if B == 128 and D not in (192, 768):
         pytest.skip("bench batch at the ViT-Tiny / ViT-Base widths only")
     t, p = 2, 16
+    if D > C * t * p * p:
+        pytest.skip("the gather dW keeps D on the tile's narrow side: D <= C * 512 (ops.patch_dw_ok)")
     n_tok = (F // t) * (H // p) * (W // p)
     M, K = B * n_tok, C * t * p * p
     g = torch.Generator(device=DEV).manual_seed(93)

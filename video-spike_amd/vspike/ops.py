@@ -269,7 +269,8 @@ def patch_embed_dw_workspace_bytes(tokens, D, K):
 def patch_dw_ok(cfg, dtype) -> bool:
     """Shapes the gather weight gradient covers (else im2col + the dW product of vs_gemm)."""
     return (dtype == torch.bfloat16 and cfg.tubelet_size == 2 and cfg.patch_size == 16 and cfg.hidden_size % 64 == 0
-            and cfg.num_channels <= 8 and L.knob_get("no_patch_fused") == 0)
+            and cfg.num_channels <= 8 and cfg.hidden_size <= cfg.num_channels * 512
+            and L.knob_get("no_patch_fused") == 0)
 
 
 def patch_embed_dw(pixels, dx, dweight, dbias, tubelet, patch, workspace=None):
