@@ -43,7 +43,7 @@ const char* vs_build_id(void);
 const char* vs_last_error(void);      /* static string, last VS_EINVAL reason */
 int vs_device_arch(char* buf, int n); /* writes gcnArchName of the current device */
 /* sizeof() of the ABI structs, so bindings can verify their mirrors: 0 = vs_gemm_desc,
- * 1 = vs_vit_layer, 2 = vs_vit_layer_grad; -1 for an unknown id */
+ * 1 = vs_vit_layer, 2 = vs_vit_layer_grad, 3 = vs_conv3d_desc; -1 for an unknown id */
 int vs_struct_size(int which);
 
 /* ------------------------------------------------------------------------------------------
@@ -420,6 +420,70 @@ int vs_comm_allreduce_bucket(void* comm, void* buf, int64_t count, int32_t dtype
 int vs_comm_finalize(void* comm);
 
 /* ------------------------------------------------------------------------------------------
+ * R3D-18 video encoder (BASELINE C4: "ResNet-18 3D-conv encoder, 32x112x112 clips, fp32").  The
+ * reference has NO CNN encoder (its registry is src/utils/utils.py:28-34): these
+ * entry points replace what torch would run for a torchvision-style r3d_18 behind the plugin surface
+ * (nn.Conv3d forward / its autograd dX and dW, nn.BatchNorm3d in training mode, nn.ReLU, the residual
+ * add, nn.AdaptiveAvgPool3d(1)), feeding the reference head (src/model/videomae.py:13-14,28-31).
+ * Layout: activations channels-last f32 [N][D][H][W][C] with C a power of two >= 4 (the 3-channel
+ * input is padded to 4 with zeros); weights [Co][kd][kh][kw][Ci] (torch's [Co][Ci][kd][kh][kw]
+ * permuted).  All three conv entry points are implicit GEMMs on v_mfma_f32_16x16x4_f32 (exact f32:
+ * a k-ordered fmaf chain per output), no im2col tensor: rows = output voxels, k = (tap, channel) in
+ * the [kd][kh][kw][Ci] order, the A operand gathered from the input in the operand load (zero
+ * outside the padded volume).  Deterministic: no atomics anywhere (fixed-order partial sums).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct vs_conv3d_desc {
+  int64_t N;                        /* batch */
+  int64_t Di, Hi, Wi, Ci;           /* input volume and channels */
+  int64_t Do, Ho, Wo, Co;           /* output volume and channels (Do = (Di + 2 pd - kd) / sd + 1, ...) */
+  int32_t kd, kh, kw;               /* kernel */
+  int32_t sd, sh, sw;               /* stride (1 or 2) */
+  int32_t pd, ph, pw;               /* zero padding */
+  int32_t reserved;
+} vs_conv3d_desc;
+/* y = conv(x, w); optional stats [ceil(N Do Ho Wo / 128)][2][Co]: per 128-row tile the column sums of
+   y and y^2 (the BatchNorm3d batch statistics, finished by vs_bn3d_stats).  Co % 64 == 0. */
+int vs_conv3d_fwd(const vs_conv3d_desc* d, const float* x, const float* w, float* y, float* stats, void* stream);
+size_t vs_conv3d_stats_rows(const vs_conv3d_desc* d);
+/* dx (=|+=) the input gradient of dy: stride 1 as the flipped-kernel conv of dy, stride 2 as one
+   implicit GEMM per parity class of the input positions (only the taps that reach that class), so
+   no MFMA runs on a zero.  Weights are regrouped per class into the workspace
+   (vs_conv3d_dx_workspace_bytes).  accumulate: 1 adds into dx (a residual branch's gradient),
+   0 overwrites every element. Ci % 64 == 0, Co a power of two >= 4. */
+size_t vs_conv3d_dx_workspace_bytes(const vs_conv3d_desc* d);
+int vs_conv3d_dx(const vs_conv3d_desc* d, const float* dy, const float* w, float* dx, int32_t accumulate,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+/* dw (=|+=) sum over output voxels of dy^T gather(x): split over the rows into workspace partials,
+   summed in split order.  Co % 64 == 0. */
+size_t vs_conv3d_dw_workspace_bytes(const vs_conv3d_desc* d);
+int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+/* BatchNorm3d (training): from the conv's stats partials (rows of [2][C]) -> mean, rstd over count
+   values per channel (biased variance, eps), scale = gamma rstd, shift = beta - mean scale; the
+   running buffers (nullable) move by momentum with the unbiased variance (torch semantics). */
+size_t vs_bn3d_stats_workspace_bytes(int64_t rows, int64_t C);
+int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t count, const float* gamma,
+                  const float* beta, float eps, float momentum, float* mean, float* rstd, float* scale,
+                  float* shift, float* running_mean, float* running_var, void* workspace, void* stream);
+/* out = [relu](y scale + shift [+ residual]) over M rows x C channels (channels-last). */
+int vs_bn3d_apply(int64_t M, int64_t C, const float* y, const float* scale, const float* shift,
+                  const float* residual, int32_t relu, float* out, void* stream);
+/* Backward of out = [relu](bn(y) [+ residual]): g = dout [* (out > 0)];  dgamma (+)= sum g xhat,
+   dbeta (+)= sum g;  dy = gamma rstd (g - mean(g) - xhat mean(g xhat));  dres = g (nullable: the
+   shortcut's gradient).  Workspace: vs_bn3d_bwd_workspace_bytes. */
+size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C);
+int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
+                const float* mean, const float* rstd, const float* gamma, float* dy, float* dres, float* dgamma,
+                float* dbeta, void* workspace, void* stream);
+/* pixels (B, T, C, H, W) f32 -> channels-last (B, T, H, W, Cp) with channels C..Cp-1 zero (Cp = 4 or 8). */
+int vs_to_channels_last(int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int64_t Cp, const float* x,
+                        float* out, void* stream);
+/* pooled[n][c] = mean over S voxels of x[n][s][c] (nn.AdaptiveAvgPool3d(1)); its backward
+   dx[n][s][c] = dpool[n][c] / S. */
+int vs_avgpool3d(int64_t N, int64_t S, int64_t C, const float* x, float* pooled, void* stream);
+int vs_avgpool3d_bwd(int64_t N, int64_t S, int64_t C, const float* dpool, float* dx, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Trial shards (host side of the input path; replaces the per-trial webdataset tars of
  * src/prepare_data.py:210-235 read by src/loader/base.py:21-41).  Fixed-size records: raw uint8
  * frames (T, C, H, W) + f32 spike counts (ap_rows, ap_cols) + a 64-byte "<eid>_<trial>" key.
@@ -470,7 +534,13 @@ const char* vs_shard_last_error(void);
 #define VS_TIMER_FWD_MLP  20   /* the fused MLP forward (vs_mlp_fwd, a_pre == NULL)   (mv:370-399) */
 #define VS_TIMER_DX_MLP   21   /* the fused MLP backward's GELU' product (vs_mlp_bwd_da) */
 #define VS_TIMER_FP8_QUANT 22  /* the MX-FP8 forward's operand quantisation (vs_quant_mxfp8 of A and W) */
-#define VS_TIMER_COUNT    23
+/* the R3D-18 encoder (BASELINE C4): flops are charged for the conv timers (2 M N K of the implicit GEMM,
+   valid taps only), bytes for the BatchNorm / elementwise timer */
+#define VS_TIMER_CONV_FWD 23   /* vs_conv3d_fwd (+ the fused BatchNorm batch statistics) */
+#define VS_TIMER_CONV_DX  24   /* vs_conv3d_dx (every parity class of a strided conv) */
+#define VS_TIMER_CONV_DW  25   /* vs_conv3d_dw (+ its split reduce) */
+#define VS_TIMER_BN       26   /* vs_bn3d_* and the layout / pooling helpers */
+#define VS_TIMER_COUNT    27
 int vs_timing_enable(int mask);   /* bit (1 << timer) enables that timer; 0 disables all */
 int vs_timing_collect(int timer, int64_t* launches, double* total_ms);
 int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_timing_collect */
@@ -502,6 +572,8 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 #define VS_PATH_MLP_BWD      19   /* vs_mlp_bwd_da: fused recompute + GELU' product */
 #define VS_PATH_GEMM_FP8     20   /* vs_gemm_mxfp8: block-scaled fp8 MFMA GEMM */
 #define VS_PATH_PATCH_DW     21   /* vs_patch_embed_dw: patch dW with the tubelet gather in its B-load */
+#define VS_PATH_CONV_IGEMM   22   /* conv_igemm_kernel: Conv3d forward / dX as an implicit GEMM (f32 MFMA) */
+#define VS_PATH_CONV_DW      23   /* conv_dw_kernel: Conv3d weight gradient (implicit-GEMM gather, split over rows) */
 #define VS_PATH_COUNT        24
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);

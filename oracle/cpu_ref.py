@@ -424,3 +424,100 @@ def video_preprocess(video: np.ndarray, idx: np.ndarray, size: int = 224, mean=I
             for ch in range(3):
                 out[bi, fi, ch] = (x - m[ch]) / sd[ch]
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# R3D-18 (BASELINE C4).  NOT in the reference (no CNN encoder, registry
+# src/utils/utils.py:28-34): this restates torchvision's published video ResNet r3d_18
+# (VideoResNet(BasicBlock, [Conv3DSimple] * 4, [2, 2, 2, 2], BasicStem); torchvision is not installed
+# here) with torch CPU ops, under the reference head (src/model/videomae.py:13-14,28-31).  The HIP
+# path is checked against it; parity is UNPINNED by any reference output.
+# ----------------------------------------------------------------------------------------------
+@dataclasses.dataclass(frozen=True)
+class R3DCfg:
+    num_frames: int = 32
+    image_size: int = 112
+    num_channels: int = 3
+    layers: Tuple[int, ...] = (2, 2, 2, 2)
+    widths: Tuple[int, ...] = (64, 128, 256, 512)
+    bn_eps: float = 1e-5
+    bn_momentum: float = 0.1
+
+
+def r3d_conv_specs(cfg: R3DCfg):
+    """(name, ci, co, kernel, stride, padding) in forward order; names as torchvision's r3d_18."""
+    specs = [("stem.0", cfg.num_channels, 64, (3, 7, 7), (1, 2, 2), (1, 3, 3))]
+    cin = 64
+    for li, (nb, w) in enumerate(zip(cfg.layers, cfg.widths)):
+        for b in range(nb):
+            s = 2 if (b == 0 and li > 0) else 1
+            pre = f"layer{li + 1}.{b}."
+            specs.append((pre + "conv1.0", cin, w, (3, 3, 3), (s, s, s), (1, 1, 1)))
+            specs.append((pre + "conv2.0", w, w, (3, 3, 3), (1, 1, 1), (1, 1, 1)))
+            if s != 1 or cin != w:
+                specs.append((pre + "downsample.0", cin, w, (1, 1, 1), (s, s, s), (0, 0, 0)))
+            cin = w
+    return specs
+
+
+def make_r3d_params(cfg: R3DCfg, enc_out: int, n_out: int, seed: int = 3) -> Dict[str, np.ndarray]:
+    """Seeded weights in torch layouts: convs ~ N(0, sqrt(2 / fan_out)) (torchvision's kaiming fan_out
+    init), BN affine perturbed around (1, 0) so every term is exercised, the reference head ~ its
+    nn.Linear scale."""
+    out = {}
+    for name, ci, co, k, _, _ in r3d_conv_specs(cfg):
+        fan_out = co * k[0] * k[1] * k[2]
+        out[name + ".weight"] = prng.normal(seed, (co, ci) + tuple(k), name, std=math.sqrt(2.0 / fan_out))
+        bn = name[:-2] + ".1"
+        out[bn + ".weight"] = prng.normal(seed, (co,), bn + ".weight", std=0.1, mean=1.0)
+        out[bn + ".bias"] = prng.normal(seed, (co,), bn + ".bias", std=0.1)
+    feat = cfg.widths[-1]
+    out["encoder.weight"] = prng.normal(seed, (enc_out, feat), "encoder.weight", std=1.0 / math.sqrt(feat))
+    out["encoder.bias"] = prng.normal(seed, (enc_out,), "encoder.bias", std=0.02)
+    out["decoder.weight"] = prng.normal(seed, (100 * n_out, enc_out), "decoder.weight", std=0.5 / math.sqrt(enc_out))
+    out["decoder.bias"] = prng.normal(seed, (100 * n_out,), "decoder.bias", std=0.02)
+    return out
+
+
+def make_r3d_pixels(cfg: R3DCfg, batch: int, seed: int = 0) -> np.ndarray:
+    """Clips in the plugin's pixel layout (B, T, C, H, W) (the VideoMAE pixel_values order)."""
+    return prng.normal(seed, (batch, cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size), "r3d_pixels")
+
+
+def r3d18_forward(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: R3DCfg, running=None,
+                  training: bool = True) -> torch.Tensor:
+    """log-rates (B, 100, N): the R3D-18 encoder (training-mode BatchNorm: batch statistics; `running`
+    = dict of running_mean / running_var tensors updated in place when given) -> AdaptiveAvgPool3d(1)
+    -> the reference head."""
+    import torch.nn.functional as F
+    B = pixels.shape[0]
+    x = pixels.permute(0, 2, 1, 3, 4)                       # (B, C, T, H, W): torch's NCDHW
+
+    def unit(name, x, stride, pad, relu, residual=None):
+        y = F.conv3d(x, P[name + ".weight"], None, stride, pad)
+        bn = name[:-2] + ".1"
+        rm = running.get(bn + ".running_mean") if running is not None else None
+        rv = running.get(bn + ".running_var") if running is not None else None
+        y = F.batch_norm(y, rm, rv, P[bn + ".weight"], P[bn + ".bias"], training=training,
+                         momentum=cfg.bn_momentum, eps=cfg.bn_eps)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+
+    specs = {s[0]: s for s in r3d_conv_specs(cfg)}
+    x = unit("stem.0", x, (1, 2, 2), (1, 3, 3), True)
+    for li, nb in enumerate(cfg.layers):
+        for b in range(nb):
+            pre = f"layer{li + 1}.{b}."
+            s1 = specs[pre + "conv1.0"]
+            h = unit(pre + "conv1.0", x, s1[4], s1[5], True)
+            if pre + "downsample.0" in specs:
+                sd = specs[pre + "downsample.0"]
+                sc = unit(pre + "downsample.0", x, sd[4], sd[5], False)
+            else:
+                sc = x
+            x = unit(pre + "conv2.0", h, (1, 1, 1), (1, 1, 1), True, residual=sc)
+    feat = x.mean(dim=(2, 3, 4))                             # AdaptiveAvgPool3d(1) + flatten
+    z = F.linear(feat, P["encoder.weight"], P["encoder.bias"])    # videomae.py:29
+    r = F.linear(z, P["decoder.weight"], P["decoder.bias"])        # videomae.py:30
+    return r.reshape(B, 100, -1)                                   # videomae.py:31

@@ -1,0 +1,901 @@
+// conv3d.hip — the R3D-18 encoder's kernels (BASELINE C4: ResNet-18 3D-conv, 32x112x112 clips, fp32).
+//
+// The reference has no CNN encoder: these replace what torch runs for a
+// torchvision-style r3d_18 behind the plugin surface (nn.Conv3d forward and its autograd dX / dW,
+// nn.BatchNorm3d in training mode, the residual add + ReLU, nn.AdaptiveAvgPool3d(1)).
+//
+// MI355X design (include/vspike.h "R3D-18 video encoder"):
+//   * Activations channels-last f32 [N][D][H][W][C]: every (voxel, tap) reads C contiguous floats, so
+//     the implicit GEMM's operand gather is 16-B vector loads of whole channel runs.
+//   * Conv3d = implicit GEMM, no im2col tensor (an explicit im2col of layer1 at 16 clips would be
+//     11 GB written and read back per conv: 2x the conv's f32-MFMA time in HBM traffic).  Rows = output
+//     voxels, k = (tap, channel), the A operand gathered per k-tile into LDS (zero outside the padded
+//     volume), the weights K-contiguous [Co][taps][Ci] as the B operand; v_mfma_f32_16x16x4_f32 (exact
+//     f32: a k-ordered fmaf chain).  128 x 64 output tile, 4 waves of 64 x 32, BK = 32, register-staged
+//     prefetch into a 2-stage LDS ring (the loads of k-tile t+1 in flight under the MFMAs of t).
+//   * dX of a stride-1 conv is the same kernel on dy with the flipped offsets; of a stride-2 conv one
+//     launch per parity class of the input positions with only the taps that reach it (1..8 of 27),
+//     so no MFMA multiplies a structural zero; weights regrouped per class ([Ci][class taps][Co]).
+//   * dW: tiles of (64 out channels x 64 k) summed over the output voxels (the gather as the B
+//     operand), split over the voxel rows; partial tiles summed in split order (no atomics).
+//   * BatchNorm3d statistics ride in the forward conv's epilogue (per 128-row tile column sums of y and
+//     y^2), finished in f64 in a fixed order; apply (+ residual + ReLU) and the backward are
+//     channel-vectorised elementwise passes with fixed-order reductions.
+#include <cstdlib>
+
+#include "common.h"
+
+namespace vs {
+
+// ------------------------------------------------------------------------------------------------
+// geometry of one implicit-GEMM launch
+// ------------------------------------------------------------------------------------------------
+struct Igemm {
+  const float* x;             // gathered operand, channels-last [N][Di][Hi][Wi][C]
+  int N, Di, Hi, Wi, C, cshift;
+  int Gd, Gh, Gw;             // GEMM row grid: rows = N * Gd * Gh * Gw
+  int sd, sh, sw;             // input step per grid step
+  // taps: per dim j in [0, cnt): input offset o0 + ostep * j (added to g * s)
+  int cd, ch, cw;
+  int od0, oh0, ow0, ods, ohs, ows;
+  const float* w;             // [Ng][K] K-contiguous, K = cd*ch*cw * C
+  int Ng, K;
+  float* y;                   // output, channels-last with Ng channels, storage grid Od x Oh x Ow
+  int Od, Oh, Ow;
+  int ysd, ysh, ysw, yod, yoh, yow;   // output voxel = g * ys + yo
+  int accumulate;
+  float* stats;               // [tiles_m][2][Ng] column sums of y and y^2 per 128-row tile, or null
+  int64_t M;
+};
+
+__device__ __forceinline__ int divq(int x, int d, float inv) {
+  // x / d for 0 <= x < 2^24 by a float reciprocal and one correction step
+  int q = (int)((float)x * inv);
+  int r = x - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
+}
+
+// f32 MFMA operand images: row-major [rows][k], 34-float rows (conflict-free ds_read_b32 of 16 rows x
+// 2 k per 32-lane half: bank = 2 row + k), filled by two ds_write_b64 per gathered float4
+constexpr int kLdA = 34;
+
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
+  constexpr int BM = 128, BN = 64, BK = 32, LD = kLdA;
+  constexpr int SA = BM * LD, SB = BN * LD, STAGE = SA + SB;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int tiles_n = g.Ng / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / tiles_n, nt = bid % tiles_n;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+  const int chunk = tid & 7;  // float4 index along k of this thread's operand loads
+
+  // the 4 A rows of this thread (rows tid/8 + 32 s): voxel coordinates of the gathered input
+  int rz[4], ry[4], rx[4];
+  int64_t rbase[4];
+  bool rok[4];
+  {
+    const float ihw = 1.0f / (float)g.Gw, ihh = 1.0f / (float)g.Gh, ihd = 1.0f / (float)g.Gd;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t m = m0 + (tid >> 3) + 32 * s;
+      rok[s] = m < g.M;
+      const int mm = rok[s] ? (int)m : 0;
+      const int q1 = divq(mm, g.Gw, ihw), gw = mm - q1 * g.Gw;
+      const int q2 = divq(q1, g.Gh, ihh), gh = q1 - q2 * g.Gh;
+      const int n = divq(q2, g.Gd, ihd), gd = q2 - n * g.Gd;
+      rz[s] = gd * g.sd;
+      ry[s] = gh * g.sh;
+      rx[s] = gw * g.sw;
+      rbase[s] = (int64_t)n * g.Di;
+    }
+  }
+  const int chw = g.ch * g.cw;
+  auto load_a = [&](float4 (&ra)[4], int k0) {
+    const int k = k0 + chunk * 4;
+    const bool kok = k < g.K;
+    const int tap = k >> g.cshift, c = k & (g.C - 1);
+    const int jd = tap / chw, jr = tap - jd * chw, jh = jr / g.cw, jw = jr - jh * g.cw;
+    const int oz = g.od0 + g.ods * jd, oy = g.oh0 + g.ohs * jh, ox = g.ow0 + g.ows * jw;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int z = rz[s] + oz, yy = ry[s] + oy, xx = rx[s] + ox;
+      const bool ok = kok && rok[s] && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
+                      (unsigned)xx < (unsigned)g.Wi;
+      const float* p = g.x + (((rbase[s] + z) * g.Hi + yy) * g.Wi + xx) * g.C + c;
+      ra[s] = ok ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto load_b = [&](float4 (&rb)[2], int k0) {
+    const int k = k0 + chunk * 4;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int n = n0 + (tid >> 3) + 32 * s;
+      rb[s] = k < g.K ? *(const float4*)(g.w + (int64_t)n * g.K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](float* st, const float4 (&ra)[4], const float4 (&rb)[2]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float* d = st + ((tid >> 3) + 32 * s) * LD + chunk * 4;
+      *(float2*)d = make_float2(ra[s].x, ra[s].y);
+      *(float2*)(d + 2) = make_float2(ra[s].z, ra[s].w);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float* d = st + SA + ((tid >> 3) + 32 * s) * LD + chunk * 4;
+      *(float2*)d = make_float2(rb[s].x, rb[s].y);
+      *(float2*)(d + 2) = make_float2(rb[s].z, rb[s].w);
+    }
+  };
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  float4 ra[4], rb[2];
+  load_a(ra, 0);
+  load_b(rb, 0);
+  store(smem, ra, rb);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const float* sa = smem + (t & 1) * STAGE;
+    const float* sb = sa + SA;
+    const bool more = t + 1 < nk;
+    if (more) {
+      load_a(ra, (t + 1) * BK);
+      load_b(rb, (t + 1) * BK);
+    }
+#pragma unroll
+    for (int sub = 0; sub < BK / 4; ++sub) {
+      const int kk = 4 * sub + (lane >> 4);
+      float af[4], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = sa[(wr * 64 + i * 16 + (lane & 15)) * LD + kk];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = sb[(wc * 32 + j * 16 + (lane & 15)) * LD + kk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(smem + ((t + 1) & 1) * STAGE, ra, rb);
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] = C[wr*64 + i*16 + 4*(lane>>4) + r][wc*32 + j*16 + (lane&15)]
+  float csum[2] = {0.f, 0.f}, csq[2] = {0.f, 0.f};
+  {
+    const float ihw = 1.0f / (float)g.Gw, ihh = 1.0f / (float)g.Gh, ihd = 1.0f / (float)g.Gd;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= g.M) continue;
+        const int mm = (int)m;
+        const int q1 = divq(mm, g.Gw, ihw), gw = mm - q1 * g.Gw;
+        const int q2 = divq(q1, g.Gh, ihh), gh = q1 - q2 * g.Gh;
+        const int n = divq(q2, g.Gd, ihd), gd = q2 - n * g.Gd;
+        const int64_t vox = (((int64_t)n * g.Od + gd * g.ysd + g.yod) * g.Oh + gh * g.ysh + g.yoh) * g.Ow +
+                            gw * g.ysw + g.yow;
+        float* dst = g.y + vox * g.Ng + n0 + wc * 32 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float v = acc[i][j][r];
+          if (g.accumulate) v += dst[j * 16];
+          dst[j * 16] = v;
+          csum[j] += v;
+          csq[j] += v * v;
+        }
+      }
+  }
+  if (g.stats) {
+    // column sums over this wave's 64 rows: the 4 lane groups (lane >> 4), then the two row waves
+    __shared__ float red[2][2][64];
+    __syncthreads();  // (smem reads done; red is a separate array written once)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float s = csum[j], q = csq[j];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        red[wr][0][wc * 32 + j * 16 + lane] = s;
+        red[wr][1][wc * 32 + j * 16 + lane] = q;
+      }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int which = tid >> 6, col = tid & 63;
+      g.stats[((int64_t)mt * 2 + which) * g.Ng + n0 + col] = red[0][which][col] + red[1][which][col];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient: dw[o][k] (+)= sum_m dy[m][o] * gather(x)[m][k]
+// ------------------------------------------------------------------------------------------------
+struct ConvDw {
+  const float* x;
+  int N, Di, Hi, Wi, C, cshift;
+  int Do, Ho, Wo;             // output (row) grid
+  int sd, sh, sw, pd, ph, pw;
+  int kd, kh, kw;
+  const float* dy;            // [M][Co]
+  int Co, K;                  // K = kd*kh*kw*C
+  int64_t M;
+  int splits, steps_per_split;  // rows of a split: steps_per_split * 32
+  float* part;                // [splits][Co][Kp], Kp = tiles_k * 64
+  int Kp;
+};
+
+__global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
+  constexpr int BO = 64, BKK = 64, BM = 32, LD = 80;
+  constexpr int SO = BM * LD, STAGE = 2 * SO;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int tiles_o = g.Co / BO, tiles_k = g.Kp / BKK;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / (tiles_o * tiles_k), rem = bid % (tiles_o * tiles_k);
+  const int ot = rem / tiles_k, kt = rem % tiles_k;
+  const int o0 = ot * BO, k0 = kt * BKK;
+  const int64_t mb = (int64_t)split * g.steps_per_split * BM;
+  int64_t me = mb + (int64_t)g.steps_per_split * BM;
+  if (me > g.M) me = g.M;
+  const int nsteps = me > mb ? (int)((me - mb + BM - 1) / BM) : 0;
+  const int chunk = tid & 15;  // float4 index along o (dy) / k (gather)
+  // the gather's k chunk: tap and channel are fixed for the whole launch of this thread
+  const int k = k0 + chunk * 4;
+  const bool kok = k < g.K;
+  const int tap = k >> g.cshift, c = k & (g.C - 1);
+  const int khw = g.kh * g.kw;
+  const int td = tap / khw, tr = tap - td * khw, th = tr / g.kw, tw = tr - th * g.kw;
+  const int oz = td - g.pd, oy = th - g.ph, ox = tw - g.pw;
+  const float ihw = 1.0f / (float)g.Wo, ihh = 1.0f / (float)g.Ho, ihd = 1.0f / (float)g.Do;
+
+  auto load = [&](float4 (&rd)[2], float4 (&rx)[2], int step) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int64_t m = mb + (int64_t)step * BM + (tid >> 4) + 16 * s;
+      const bool ok = m < me;
+      const int mm = ok ? (int)m : 0;
+      rd[s] = ok ? *(const float4*)(g.dy + (int64_t)mm * g.Co + o0 + chunk * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int q1 = divq(mm, g.Wo, ihw), gw = mm - q1 * g.Wo;
+      const int q2 = divq(q1, g.Ho, ihh), gh = q1 - q2 * g.Ho;
+      const int n = divq(q2, g.Do, ihd), gd = q2 - n * g.Do;
+      const int z = gd * g.sd + oz, yy = gh * g.sh + oy, xx = gw * g.sw + ox;
+      const bool in = ok && kok && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
+                      (unsigned)xx < (unsigned)g.Wi;
+      const float* p = g.x + ((((int64_t)n * g.Di + z) * g.Hi + yy) * g.Wi + xx) * g.C + c;
+      rx[s] = in ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](float* st, const float4 (&rd)[2], const float4 (&rx)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int row = (tid >> 4) + 16 * s;
+      *(float4*)(st + row * LD + chunk * 4) = rd[s];
+      *(float4*)(st + SO + row * LD + chunk * 4) = rx[s];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 rd[2], rx[2];
+  if (nsteps > 0) {
+    load(rd, rx, 0);
+    store(smem, rd, rx);
+  }
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    const float* sd_ = smem + (t & 1) * STAGE;
+    const float* sx = sd_ + SO;
+    const bool more = t + 1 < nsteps;
+    if (more) load(rd, rx, t + 1);
+#pragma unroll
+    for (int sub = 0; sub < BM / 4; ++sub) {
+      const int mrow = 4 * sub + (lane >> 4);
+      float af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = sd_[mrow * LD + wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = sx[mrow * LD + wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(smem + ((t + 1) & 1) * STAGE, rd, rx);
+    __syncthreads();
+  }
+  // partial tile (plain stores; the reduce adds the splits in order)
+  float* pt = g.part + (int64_t)split * g.Co * g.Kp;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wr * 32 + i * 16 + 4 * (lane >> 4) + r;
+        const int kk = k0 + wc * 32 + j * 16 + (lane & 15);
+        pt[(int64_t)o * g.Kp + kk] = acc[i][j][r];
+      }
+}
+
+// dw[o][k] (=|+=) sum_s part[s][o][k] for k < K (float4 over k when K % 4 == 0)
+__global__ __launch_bounds__(256) void conv_dw_reduce(const float* __restrict__ part, int splits, int Co, int K,
+                                                      int Kp, float* __restrict__ dw, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = (int64_t)Co * K;
+  if (i >= n) return;
+  const int o = (int)(i / K), k = (int)(i % K);
+  const int64_t src = (int64_t)o * Kp + k, plane = (int64_t)Co * Kp;
+  float s = 0.f;
+  for (int sp = 0; sp < splits; ++sp) s += part[sp * plane + src];
+  dw[i] = accumulate ? dw[i] + s : s;
+}
+
+// dX weights of one parity class: wd[ci][(jd, jh, jw)][co] = w[co][td][th][tw][ci], t = t0 + tstep j
+__global__ __launch_bounds__(256) void conv_dx_weights(const float* __restrict__ w, int Co, int Ci, int kd, int kh,
+                                                       int kw, int cd, int ch, int cw, int t0d, int t0h, int t0w,
+                                                       int tsd, int tsh, int tsw, float* __restrict__ wd) {
+  const int T = cd * ch * cw;
+  const int64_t n = (int64_t)Ci * T * Co;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int co = (int)(i % Co);
+  const int64_t q = i / Co;
+  const int j = (int)(q % T), ci = (int)(q / T);
+  const int jd = j / (ch * cw), jr = j % (ch * cw), jh = jr / cw, jw = jr % cw;
+  const int td = t0d + tsd * jd, th = t0h + tsh * jh, tw = t0w + tsw * jw;
+  wd[i] = w[((((int64_t)co * kd + td) * kh + th) * kw + tw) * Ci + ci];
+}
+
+// ------------------------------------------------------------------------------------------------
+// BatchNorm3d
+// ------------------------------------------------------------------------------------------------
+// level 1: rows [r0, r0 + 256) of the [rows][2][C] partials, 64 channels per block: f64 sums
+__global__ __launch_bounds__(256) void bn_stats_l1(const float* __restrict__ part, int64_t rows, int C,
+                                                   double* __restrict__ out) {
+  __shared__ double red[2][4][64];
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int64_t r = r0 + grp; r < r0 + 256 && r < rows; r += 4) {
+      s += (double)part[(r * 2) * C + c];
+      q += (double)part[(r * 2 + 1) * C + c];
+    }
+  red[0][grp][threadIdx.x & 63] = s;
+  red[1][grp][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    out[((int64_t)blockIdx.x * 2) * C + c] = ((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l];
+    out[((int64_t)blockIdx.x * 2 + 1) * C + c] = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_l2(const double* __restrict__ l1, int nblk, int C, int64_t count,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float eps, float momentum, float* mean, float* rstd, float* scale,
+                                                   float* shift, float* rmean, float* rvar) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s += l1[((int64_t)b * 2) * C + c];
+    q += l1[((int64_t)b * 2 + 1) * C + c];
+  }
+  const double mu = s / (double)count;
+  double var = q / (double)count - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  rstd[c] = rs;
+  const float sc = gamma[c] * rs;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mu * sc;
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+  if (rvar) {
+    const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n4, int C, const float4* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float4* __restrict__ res, int relu,
+                                                       float4* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)((i * 4) % C);
+    float4 v = y[i];
+    const float4 a = *(const float4*)(scale + c), b = *(const float4*)(shift + c);
+    v.x = fmaf(v.x, a.x, b.x); v.y = fmaf(v.y, a.y, b.y); v.z = fmaf(v.z, a.z, b.z); v.w = fmaf(v.w, a.w, b.w);
+    if (res) {
+      const float4 r = res[i];
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    if (relu) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    out[i] = v;
+  }
+}
+
+// backward, pass 1: per block over a contiguous row range, per channel sum g and sum g xhat
+// (g = dout masked by out > 0 under ReLU); partial rows [blocks][2][C]
+__global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const float* __restrict__ dout,
+                                                     const float* __restrict__ out, int relu,
+                                                     const float* __restrict__ y, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, int64_t rows_per_blk,
+                                                     float* __restrict__ part) {
+  __shared__ float4 red[2][256];
+  const int groups = C / 4;                  // float4 channel groups per row
+  const int rpi = 256 / groups;              // rows per iteration (C <= 1024)
+  const int t = threadIdx.x, cg = t % groups, ro = t / groups;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
+  int64_t r1 = r0 + rows_per_blk;
+  if (r1 > M) r1 = M;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  const float4 mu = *(const float4*)(mean + cg * 4), rs = *(const float4*)(rstd + cg * 4);
+  if (ro < rpi)
+    for (int64_t r = r0 + ro; r < r1; r += rpi) {
+      const int64_t i = r * C + cg * 4;
+      float4 gv = *(const float4*)(dout + i);
+      if (relu) {
+        const float4 o = *(const float4*)(out + i);
+        gv.x = o.x > 0.f ? gv.x : 0.f; gv.y = o.y > 0.f ? gv.y : 0.f;
+        gv.z = o.z > 0.f ? gv.z : 0.f; gv.w = o.w > 0.f ? gv.w : 0.f;
+      }
+      const float4 yv = *(const float4*)(y + i);
+      s.x += gv.x; s.y += gv.y; s.z += gv.z; s.w += gv.w;
+      q.x = fmaf(gv.x, (yv.x - mu.x) * rs.x, q.x);
+      q.y = fmaf(gv.y, (yv.y - mu.y) * rs.y, q.y);
+      q.z = fmaf(gv.z, (yv.z - mu.z) * rs.z, q.z);
+      q.w = fmaf(gv.w, (yv.w - mu.w) * rs.w, q.w);
+    }
+  red[0][t] = s;
+  red[1][t] = q;
+  __syncthreads();
+  if (t < groups) {       // fixed order over the row offsets
+    float4 a = red[0][t], b = red[1][t];
+    for (int k = 1; k < rpi; ++k) {
+      const float4 u = red[0][k * groups + t], v = red[1][k * groups + t];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    }
+    *(float4*)(part + ((int64_t)blockIdx.x * 2) * C + t * 4) = a;
+    *(float4*)(part + ((int64_t)blockIdx.x * 2 + 1) * C + t * 4) = b;
+  }
+}
+
+// pass 2: per channel the totals (f64, block order), dgamma / dbeta (+=), and the apply coefficients
+// coef[0][c] = gamma rstd, coef[1][c] = gamma rstd mean(g), coef[2][c] = gamma rstd mean(g xhat)
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__ part, int nblk, int C, int64_t M,
+                                                       const float* __restrict__ gamma, const float* __restrict__ rstd,
+                                                       float* dgamma, float* dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s += (double)part[((int64_t)b * 2) * C + c];
+    q += (double)part[((int64_t)b * 2 + 1) * C + c];
+  }
+  if (dgamma) dgamma[c] += (float)q;
+  if (dbeta) dbeta[c] += (float)s;
+  const float a = gamma[c] * rstd[c];
+  coef[c] = a;
+  coef[C + c] = a * (float)(s / (double)M);
+  coef[2 * C + c] = a * (float)(q / (double)M);
+}
+
+// pass 3: dy = a g - b - c xhat;  dres = g
+__global__ __launch_bounds__(256) void bn_bwd_apply(int64_t n4, int C, const float4* __restrict__ dout,
+                                                    const float4* __restrict__ out, int relu,
+                                                    const float4* __restrict__ y, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, const float* __restrict__ coef,
+                                                    float4* __restrict__ dy, float4* __restrict__ dres) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)((i * 4) % C);
+    float4 gv = dout[i];
+    if (relu) {
+      const float4 o = out[i];
+      gv.x = o.x > 0.f ? gv.x : 0.f; gv.y = o.y > 0.f ? gv.y : 0.f;
+      gv.z = o.z > 0.f ? gv.z : 0.f; gv.w = o.w > 0.f ? gv.w : 0.f;
+    }
+    if (dres) dres[i] = gv;
+    const float4 yv = y[i];
+    const float4 mu = *(const float4*)(mean + c), rs = *(const float4*)(rstd + c);
+    const float4 a = *(const float4*)(coef + c), b = *(const float4*)(coef + C + c),
+                 cc = *(const float4*)(coef + 2 * C + c);
+    float4 o;
+    o.x = fmaf(a.x, gv.x, -b.x) - cc.x * ((yv.x - mu.x) * rs.x);
+    o.y = fmaf(a.y, gv.y, -b.y) - cc.y * ((yv.y - mu.y) * rs.y);
+    o.z = fmaf(a.z, gv.z, -b.z) - cc.z * ((yv.z - mu.z) * rs.z);
+    o.w = fmaf(a.w, gv.w, -b.w) - cc.w * ((yv.w - mu.w) * rs.w);
+    dy[i] = o;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// layout and pooling helpers
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void to_channels_last_kernel(int64_t vox, int64_t HW, int C, int Cp,
+                                                               const float* __restrict__ x,
+                                                               float* __restrict__ out) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;  // voxel index over (B, T, H, W)
+  if (v >= vox) return;
+  const int64_t bt = v / HW, hw = v % HW;
+  float o[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) o[c] = c < C ? x[(bt * C + c) * HW + hw] : 0.f;
+  float* dst = out + v * Cp;
+  *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
+  if (Cp == 8) *(float4*)(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+__global__ __launch_bounds__(256) void avgpool_kernel(int64_t S, int C, const float* __restrict__ x,
+                                                      float* __restrict__ pooled) {
+  const int n = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = x + (int64_t)n * S * C + c;
+  float s = 0.f;
+  for (int64_t i = 0; i < S; ++i) s += p[i * C];
+  pooled[(int64_t)n * C + c] = s / (float)S;
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(int64_t total, int64_t S, int C,
+                                                          const float* __restrict__ dpool, float* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  const int64_t n = i / ((int64_t)S * C);
+  dx[i] = dpool[n * C + c] / (float)S;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+static int ilog2(int64_t v) {
+  int s = 0;
+  while ((1ll << s) < v) ++s;
+  return (1ll << s) == v ? s : -1;
+}
+
+static bool desc_ok(const vs_conv3d_desc* d) {
+  if (!d || d->N <= 0 || d->Ci <= 0 || d->Co <= 0) return false;
+  if (d->kd < 1 || d->kh < 1 || d->kw < 1 || d->sd < 1 || d->sh < 1 || d->sw < 1) return false;
+  if (d->pd < 0 || d->ph < 0 || d->pw < 0) return false;
+  return d->Do == (d->Di + 2 * d->pd - d->kd) / d->sd + 1 && d->Ho == (d->Hi + 2 * d->ph - d->kh) / d->sh + 1 &&
+         d->Wo == (d->Wi + 2 * d->pw - d->kw) / d->sw + 1 && d->Do > 0 && d->Ho > 0 && d->Wo > 0;
+}
+
+static double conv_flops(const vs_conv3d_desc* d) {
+  return 2.0 * (double)(d->N * d->Do * d->Ho * d->Wo) * (double)d->Co * (double)(d->kd * d->kh * d->kw * d->Ci);
+}
+
+static int launch_igemm(const Igemm& g, hipStream_t s) {
+  const int64_t tiles_m = (g.M + 127) / 128;
+  const int64_t nwg = tiles_m * (g.Ng / 64);
+  VS_REQUIRE(nwg < (1ll << 31), "conv3d: grid too large");
+  count_path(VS_PATH_CONV_IGEMM);
+  hipLaunchKernelGGL(conv_igemm_kernel, dim3((unsigned)nwg), dim3(256), 0, s, g);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+}  // namespace vs
+
+using namespace vs;
+
+extern "C" size_t vs_conv3d_stats_rows(const vs_conv3d_desc* d) {
+  if (!desc_ok(d)) return 0;
+  return (size_t)((d->N * d->Do * d->Ho * d->Wo + 127) / 128);
+}
+
+extern "C" int vs_conv3d_fwd(const vs_conv3d_desc* d, const float* x, const float* w, float* y, float* stats,
+                             void* stream) {
+  VS_REQUIRE(desc_ok(d), "vs_conv3d_fwd: inconsistent geometry (Do = (Di + 2 pd - kd) / sd + 1, ...)");
+  VS_REQUIRE(x && w && y, "vs_conv3d_fwd: null pointer");
+  const int cs = ilog2(d->Ci);
+  VS_REQUIRE(cs >= 2 && d->Co % 64 == 0, "vs_conv3d_fwd: Ci must be a power of two >= 4, Co a multiple of 64");
+  VS_REQUIRE(aligned16(x) && aligned16(w) && aligned16(y), "vs_conv3d_fwd: pointers must be 16-byte aligned");
+  const int64_t M = d->N * d->Do * d->Ho * d->Wo;
+  VS_REQUIRE(M < (1ll << 24) && d->N * d->Di * d->Hi * d->Wi < (1ll << 31), "vs_conv3d_fwd: volume too large");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_CONV_FWD, s, conv_flops(d));
+  Igemm g = {};
+  g.x = x; g.N = (int)d->N; g.Di = (int)d->Di; g.Hi = (int)d->Hi; g.Wi = (int)d->Wi; g.C = (int)d->Ci; g.cshift = cs;
+  g.Gd = (int)d->Do; g.Gh = (int)d->Ho; g.Gw = (int)d->Wo;
+  g.sd = d->sd; g.sh = d->sh; g.sw = d->sw;
+  g.cd = d->kd; g.ch = d->kh; g.cw = d->kw;
+  g.od0 = -d->pd; g.oh0 = -d->ph; g.ow0 = -d->pw; g.ods = 1; g.ohs = 1; g.ows = 1;
+  g.w = w; g.Ng = (int)d->Co; g.K = d->kd * d->kh * d->kw * (int)d->Ci;
+  g.y = y; g.Od = (int)d->Do; g.Oh = (int)d->Ho; g.Ow = (int)d->Wo;
+  g.ysd = g.ysh = g.ysw = 1;
+  g.accumulate = 0;
+  g.stats = stats;
+  g.M = M;
+  return launch_igemm(g, s);
+}
+
+// the parity classes of a dX launch: per dim the first tap, tap step, class count and the offsets
+struct DxDim {
+  int ncls;            // 1 (stride 1) or 2 (stride 2)
+  int cnt[2], t0[2], ts[2], o0[2], os[2], start[2], step;
+};
+static DxDim dx_dim(int k, int s, int p) {
+  DxDim r = {};
+  if (s == 1) {    // dX[i] = sum_t dy[i + p - t] w[t]
+    r.ncls = 1;
+    r.cnt[0] = k; r.t0[0] = 0; r.ts[0] = 1; r.o0[0] = p; r.os[0] = -1; r.start[0] = 0;
+    r.step = 1;
+    return r;
+  }
+  // stride 2: i = 2 j + par; taps t with (par + p - t) even; dy index j + (par + p - t) / 2
+  r.ncls = 2;
+  r.step = 2;
+  for (int par = 0; par < 2; ++par) {
+    const int t0 = (par + p) & 1;
+    r.t0[par] = t0;
+    r.ts[par] = 2;
+    r.cnt[par] = t0 < k ? (k - 1 - t0) / 2 + 1 : 0;
+    r.o0[par] = (par + p - t0) / 2;
+    r.os[par] = -1;
+    r.start[par] = par;
+  }
+  return r;
+}
+
+extern "C" size_t vs_conv3d_dx_workspace_bytes(const vs_conv3d_desc* d) {
+  if (!desc_ok(d)) return 0;
+  return (size_t)d->Ci * d->kd * d->kh * d->kw * d->Co * 4 + 256;
+}
+
+extern "C" int vs_conv3d_dx(const vs_conv3d_desc* d, const float* dy, const float* w, float* dx, int32_t accumulate,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
+  VS_REQUIRE(desc_ok(d), "vs_conv3d_dx: inconsistent geometry");
+  VS_REQUIRE(dy && w && dx && workspace, "vs_conv3d_dx: null pointer");
+  const int cs = ilog2(d->Co);
+  VS_REQUIRE(cs >= 2 && d->Ci % 64 == 0, "vs_conv3d_dx: Co must be a power of two >= 4, Ci a multiple of 64");
+  VS_REQUIRE(d->sd <= 2 && d->sh <= 2 && d->sw <= 2, "vs_conv3d_dx: stride 1 or 2");
+  VS_REQUIRE((size_t)workspace_bytes >= vs_conv3d_dx_workspace_bytes(d), "vs_conv3d_dx: workspace too small");
+  VS_REQUIRE(aligned16(dy) && aligned16(w) && aligned16(dx) && aligned16(workspace),
+             "vs_conv3d_dx: pointers must be 16-byte aligned");
+  VS_REQUIRE(d->N * d->Di * d->Hi * d->Wi < (1ll << 24), "vs_conv3d_dx: volume too large");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_CONV_DX, s, conv_flops(d));
+  const DxDim zd = dx_dim(d->kd, d->sd, d->pd), yd = dx_dim(d->kh, d->sh, d->ph), xd = dx_dim(d->kw, d->sw, d->pw);
+  float* wd = (float*)workspace;
+  for (int a = 0; a < zd.ncls; ++a)
+    for (int b = 0; b < yd.ncls; ++b)
+      for (int c = 0; c < xd.ncls; ++c) {
+        // the positions of this class: i = start + step * j, j < G
+        const int Gd = (int)((d->Di - zd.start[a] + zd.step - 1) / zd.step);
+        const int Gh = (int)((d->Hi - yd.start[b] + yd.step - 1) / yd.step);
+        const int Gw = (int)((d->Wi - xd.start[c] + xd.step - 1) / xd.step);
+        if (Gd <= 0 || Gh <= 0 || Gw <= 0) continue;
+        const int T = zd.cnt[a] * yd.cnt[b] * xd.cnt[c];
+        if (T == 0) {   // no tap reaches these positions: their gradient is zero
+          if (!accumulate) {
+            Igemm g = {};   // a K = 0 GEMM writes zeros through the same epilogue
+            g.x = dy; g.N = (int)d->N; g.Di = (int)d->Do; g.Hi = (int)d->Ho; g.Wi = (int)d->Wo; g.C = (int)d->Co;
+            g.cshift = cs; g.Gd = Gd; g.Gh = Gh; g.Gw = Gw; g.sd = g.sh = g.sw = 1; g.cd = g.ch = g.cw = 1;
+            g.w = wd; g.Ng = (int)d->Ci; g.K = 0;
+            g.y = dx; g.Od = (int)d->Di; g.Oh = (int)d->Hi; g.Ow = (int)d->Wi;
+            g.ysd = zd.step; g.ysh = yd.step; g.ysw = xd.step; g.yod = zd.start[a]; g.yoh = yd.start[b];
+            g.yow = xd.start[c];
+            g.M = d->N * (int64_t)Gd * Gh * Gw;
+            VS_CALL(launch_igemm(g, s));
+          }
+          continue;
+        }
+        const int64_t nw = d->Ci * (int64_t)T * d->Co;
+        hipLaunchKernelGGL(conv_dx_weights, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, (int)d->Co,
+                           (int)d->Ci, d->kd, d->kh, d->kw, zd.cnt[a], yd.cnt[b], xd.cnt[c], zd.t0[a], yd.t0[b],
+                           xd.t0[c], zd.ts[a], yd.ts[b], xd.ts[c], wd);
+        VS_LAUNCH_CHECK();
+        Igemm g = {};
+        g.x = dy; g.N = (int)d->N; g.Di = (int)d->Do; g.Hi = (int)d->Ho; g.Wi = (int)d->Wo; g.C = (int)d->Co;
+        g.cshift = cs;
+        g.Gd = Gd; g.Gh = Gh; g.Gw = Gw;
+        g.sd = g.sh = g.sw = 1;
+        g.cd = zd.cnt[a]; g.ch = yd.cnt[b]; g.cw = xd.cnt[c];
+        g.od0 = zd.o0[a]; g.oh0 = yd.o0[b]; g.ow0 = xd.o0[c];
+        g.ods = zd.os[a]; g.ohs = yd.os[b]; g.ows = xd.os[c];
+        g.w = wd; g.Ng = (int)d->Ci; g.K = T * (int)d->Co;
+        g.y = dx; g.Od = (int)d->Di; g.Oh = (int)d->Hi; g.Ow = (int)d->Wi;
+        g.ysd = zd.step; g.ysh = yd.step; g.ysw = xd.step;
+        g.yod = zd.start[a]; g.yoh = yd.start[b]; g.yow = xd.start[c];
+        g.accumulate = accumulate;
+        g.M = d->N * (int64_t)Gd * Gh * Gw;
+        VS_CALL(launch_igemm(g, s));
+      }
+  return VS_OK;
+}
+
+namespace vs {
+struct DwPlanC {
+  int tiles_o, tiles_k, Kp, splits, sps;
+};
+static DwPlanC plan_conv_dw(const vs_conv3d_desc* d) {
+  DwPlanC p;
+  const int K = d->kd * d->kh * d->kw * (int)d->Ci;
+  p.tiles_o = (int)(d->Co / 64);
+  p.tiles_k = (K + 63) / 64;
+  p.Kp = p.tiles_k * 64;
+  const int64_t M = d->N * d->Do * d->Ho * d->Wo;
+  const int64_t steps = (M + 31) / 32;
+  const int tiles = p.tiles_o * p.tiles_k;
+  int64_t S = (1024 + tiles - 1) / tiles;        // ~4 workgroups per CU
+  const int64_t smax = steps / 16 > 0 ? steps / 16 : 1;   // >= 16 row steps per split
+  if (S > smax) S = smax;
+  if (S < 1) S = 1;
+  p.sps = (int)((steps + S - 1) / S);
+  p.splits = (int)((steps + p.sps - 1) / p.sps);
+  return p;
+}
+}  // namespace vs
+
+extern "C" size_t vs_conv3d_dw_workspace_bytes(const vs_conv3d_desc* d) {
+  if (!desc_ok(d) || d->Co % 64) return 0;
+  const DwPlanC p = plan_conv_dw(d);
+  return (size_t)p.splits * d->Co * p.Kp * 4 + 256;
+}
+
+extern "C" int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
+  VS_REQUIRE(desc_ok(d), "vs_conv3d_dw: inconsistent geometry");
+  VS_REQUIRE(x && dy && dw && workspace, "vs_conv3d_dw: null pointer");
+  const int cs = ilog2(d->Ci);
+  VS_REQUIRE(cs >= 2 && d->Co % 64 == 0, "vs_conv3d_dw: Ci must be a power of two >= 4, Co a multiple of 64");
+  VS_REQUIRE((size_t)workspace_bytes >= vs_conv3d_dw_workspace_bytes(d), "vs_conv3d_dw: workspace too small");
+  VS_REQUIRE(aligned16(x) && aligned16(dy) && aligned16(workspace), "vs_conv3d_dw: pointers must be 16-byte aligned");
+  const int64_t M = d->N * d->Do * d->Ho * d->Wo;
+  VS_REQUIRE(M < (1ll << 24), "vs_conv3d_dw: volume too large");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_CONV_DW, s, conv_flops(d));
+  const DwPlanC p = plan_conv_dw(d);
+  ConvDw g = {};
+  g.x = x; g.N = (int)d->N; g.Di = (int)d->Di; g.Hi = (int)d->Hi; g.Wi = (int)d->Wi; g.C = (int)d->Ci; g.cshift = cs;
+  g.Do = (int)d->Do; g.Ho = (int)d->Ho; g.Wo = (int)d->Wo;
+  g.sd = d->sd; g.sh = d->sh; g.sw = d->sw; g.pd = d->pd; g.ph = d->ph; g.pw = d->pw;
+  g.kd = d->kd; g.kh = d->kh; g.kw = d->kw;
+  g.dy = dy; g.Co = (int)d->Co; g.K = d->kd * d->kh * d->kw * (int)d->Ci;
+  g.M = M; g.splits = p.splits; g.steps_per_split = p.sps; g.part = (float*)workspace; g.Kp = p.Kp;
+  count_path(VS_PATH_CONV_DW);
+  const int64_t nwg = (int64_t)p.splits * p.tiles_o * p.tiles_k;
+  hipLaunchKernelGGL(conv_dw_kernel, dim3((unsigned)nwg), dim3(256), 0, s, g);
+  VS_LAUNCH_CHECK();
+  const int64_t n = d->Co * (int64_t)g.K;
+  hipLaunchKernelGGL(conv_dw_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)workspace,
+                     p.splits, g.Co, g.K, p.Kp, dw, accumulate);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" size_t vs_bn3d_stats_workspace_bytes(int64_t rows, int64_t C) {
+  return (size_t)((rows + 255) / 256) * 2 * C * sizeof(double) + 256;
+}
+
+extern "C" int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t count, const float* gamma,
+                             const float* beta, float eps, float momentum, float* mean, float* rstd, float* scale,
+                             float* shift, float* running_mean, float* running_var, void* workspace, void* stream) {
+  VS_REQUIRE(part && gamma && beta && mean && rstd && scale && shift && workspace, "vs_bn3d_stats: null pointer");
+  VS_REQUIRE(rows > 0 && C > 0 && count > 0 && C % 4 == 0, "vs_bn3d_stats: bad extents");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)rows * 2.0 * (double)C * 4.0);
+  const int64_t nblk = (rows + 255) / 256;
+  double* l1 = (double*)workspace;   // level-1 f64 partial sums [nblk][2][C]
+  hipLaunchKernelGGL(bn_stats_l1, dim3((unsigned)nblk, (unsigned)((C + 63) / 64)), dim3(256), 0, s, part, rows,
+                     (int)C, l1);
+  VS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_stats_l2, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const double*)l1, (int)nblk,
+                     (int)C, count, gamma, beta, eps, momentum, mean, rstd, scale, shift, running_mean, running_var);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_bn3d_apply(int64_t M, int64_t C, const float* y, const float* scale, const float* shift,
+                             const float* residual, int32_t relu, float* out, void* stream) {
+  VS_REQUIRE(y && scale && shift && out, "vs_bn3d_apply: null pointer");
+  VS_REQUIRE(C % 4 == 0 && aligned16(y) && aligned16(out) && (!residual || aligned16(residual)) && aligned16(scale) &&
+                 aligned16(shift),
+             "vs_bn3d_apply: C % 4 == 0 and 16-byte aligned pointers");
+  if (M <= 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)M * C * (residual ? 12.0 : 8.0));
+  const int64_t n4 = M * C / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n4, (int)C, (const float4*)y, scale,
+                     shift, (const float4*)residual, relu, (float4*)out);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+namespace vs {
+static int64_t bn_bwd_blocks(int64_t M) {
+  const int64_t b = (M + 1023) / 1024;
+  return b < 2048 ? (b > 0 ? b : 1) : 2048;
+}
+}  // namespace vs
+
+extern "C" size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C) {
+  return (size_t)(bn_bwd_blocks(M) * 2 * C + 3 * C) * 4 + 256;
+}
+
+extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
+                           const float* mean, const float* rstd, const float* gamma, float* dy, float* dres,
+                           float* dgamma, float* dbeta, void* workspace, void* stream) {
+  VS_REQUIRE(dout && y && mean && rstd && gamma && dy && workspace && (!relu || out), "vs_bn3d_bwd: null pointer");
+  VS_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(dout) && aligned16(y) && aligned16(dy) &&
+                 (!out || aligned16(out)) && (!dres || aligned16(dres)) && aligned16(workspace),
+             "vs_bn3d_bwd: C % 4 == 0, C <= 1024, 16-byte aligned pointers");
+  if (M <= 0) return VS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)M * C * (4.0 * (relu ? 3 : 2) + 4.0 + (dres ? 4.0 : 0.0)));
+  const int64_t nblk = bn_bwd_blocks(M);
+  const int64_t rpb = (M + nblk - 1) / nblk;
+  float* part = (float*)workspace;
+  float* coef = part + nblk * 2 * C;
+  hipLaunchKernelGGL(bn_bwd_reduce, dim3((unsigned)nblk), dim3(256), 0, s, M, (int)C, dout, out, relu, y, mean, rstd,
+                     rpb, part);
+  VS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const float*)part,
+                     (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef);
+  VS_LAUNCH_CHECK();
+  const int64_t n4 = M * C / 4;
+  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  hipLaunchKernelGGL(bn_bwd_apply, dim3((unsigned)blocks), dim3(256), 0, s, n4, (int)C, (const float4*)dout,
+                     (const float4*)out, relu, (const float4*)y, mean, rstd, (const float*)coef, (float4*)dy,
+                     (float4*)dres);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_to_channels_last(int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int64_t Cp, const float* x,
+                                   float* out, void* stream) {
+  VS_REQUIRE(x && out && aligned16(out), "vs_to_channels_last: null / misaligned pointer");
+  VS_REQUIRE(C >= 1 && C <= Cp && (Cp == 4 || Cp == 8), "vs_to_channels_last: C <= Cp, Cp = 4 or 8");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)B * T * H * W * (C + Cp) * 4.0);
+  const int64_t vox = B * T * H * W;
+  hipLaunchKernelGGL(to_channels_last_kernel, dim3((unsigned)((vox + 255) / 256)), dim3(256), 0, s, vox, H * W,
+                     (int)C, (int)Cp, x, out);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_avgpool3d(int64_t N, int64_t S, int64_t C, const float* x, float* pooled, void* stream) {
+  VS_REQUIRE(x && pooled && N > 0 && S > 0 && C > 0, "vs_avgpool3d: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)N * S * C * 4.0);
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((C + 255) / 256), (unsigned)N), dim3(256), 0, s, S, (int)C, x,
+                     pooled);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_avgpool3d_bwd(int64_t N, int64_t S, int64_t C, const float* dpool, float* dx, void* stream) {
+  VS_REQUIRE(dpool && dx && N > 0 && S > 0 && C > 0, "vs_avgpool3d_bwd: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  ScopedTimer timer(VS_TIMER_BN, s, (double)N * S * C * 4.0);
+  const int64_t total = N * S * C;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, S, (int)C,
+                     dpool, dx);
+  VS_LAUNCH_CHECK();
+  return VS_OK;
+}

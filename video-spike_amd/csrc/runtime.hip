@@ -133,6 +133,7 @@ extern "C" int vs_struct_size(int which) {
     case 0: return (int)sizeof(vs_gemm_desc);
     case 1: return (int)sizeof(vs_vit_layer);
     case 2: return (int)sizeof(vs_vit_layer_grad);
+    case 3: return (int)sizeof(vs_conv3d_desc);
     default: return -1;
   }
 }

@@ -8,13 +8,16 @@ from .config import DictConfig, config_from_kwargs, load_run_config, update_conf
 from .linear import Linear
 from .loss import MSEMeanLoss, PoissonNLLMeanLoss, make_criterion, mse_mean, poisson_nll_mean
 from .optim import FusedAdamW
+from .r3d import R3D
 from .vit import VideoMAE
 
 NAME2MODEL = {
     "Linear": Linear,
     "VideoMAE": VideoMAE,
+    # BASELINE C4's CNN encoder (no reference counterpart: SURVEY.md section 0), same plugin surface
+    "R3D": R3D,
 }
 
-__all__ = ["NAME2MODEL", "Linear", "VideoMAE", "FusedAdamW", "poisson_nll_mean", "PoissonNLLMeanLoss",
+__all__ = ["NAME2MODEL", "Linear", "VideoMAE", "R3D", "FusedAdamW", "poisson_nll_mean", "PoissonNLLMeanLoss",
            "mse_mean", "MSEMeanLoss", "make_criterion",
            "DictConfig", "update_config", "config_from_kwargs", "load_run_config"]

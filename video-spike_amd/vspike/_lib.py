@@ -28,12 +28,15 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
                # the fused MLP (a_pre == NULL in vs_vit_layer): forward, backward GELU' product
                "fwd_mlp", "dx_mlp",
                # the MX-FP8 forward's operand quantisation (compute_dtype fp8)
-               "fp8_quant")
+               "fp8_quant",
+               # the R3D-18 encoder (BASELINE C4): conv forward / dX / dW (flops), BatchNorm + helpers (bytes)
+               "conv_fwd", "conv_dx", "conv_dw", "bn")
 
 # vspike.h VS_PATH_* (dispatch counters) and VS_KNOB_* (A/B and test knobs), in id order
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
               "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
-              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8", "patch_dw")
+              "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8", "patch_dw",
+              "conv_igemm", "conv_dw")
 PATH_COUNT = 24
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
@@ -57,6 +60,13 @@ class GemmDesc(ctypes.Structure):
                 ("aux_in", c_p), ("ld_aux_in", c_i64), ("aux_out", c_p), ("ld_aux_out", c_i64),
                 ("split_k", c_i32), ("reserved", c_i32), ("a_rowsum", c_p), ("workspace", c_p),
                 ("workspace_bytes", c_i64)]
+
+
+class Conv3dDesc(ctypes.Structure):
+    _fields_ = [("N", c_i64), ("Di", c_i64), ("Hi", c_i64), ("Wi", c_i64), ("Ci", c_i64),
+                ("Do", c_i64), ("Ho", c_i64), ("Wo", c_i64), ("Co", c_i64),
+                ("kd", c_i32), ("kh", c_i32), ("kw", c_i32), ("sd", c_i32), ("sh", c_i32), ("sw", c_i32),
+                ("pd", c_i32), ("ph", c_i32), ("pw", c_i32), ("reserved", c_i32)]
 
 
 class VitLayer(ctypes.Structure):
@@ -155,6 +165,21 @@ PROTOTYPES = {
     "vs_vit_layer_bwd": (ctypes.c_int, [ctypes.POINTER(VitLayer), ctypes.POINTER(VitLayerGrad), c_p]),
     "vs_bwd_chain_create": (ctypes.c_int, [ctypes.POINTER(c_p)]),
     "vs_bwd_chain_destroy": (ctypes.c_int, [c_p]),
+    "vs_conv3d_fwd": (ctypes.c_int, [ctypes.POINTER(Conv3dDesc), c_p, c_p, c_p, c_p, c_p]),
+    "vs_conv3d_stats_rows": (c_sz, [ctypes.POINTER(Conv3dDesc)]),
+    "vs_conv3d_dx_workspace_bytes": (c_sz, [ctypes.POINTER(Conv3dDesc)]),
+    "vs_conv3d_dx": (ctypes.c_int, [ctypes.POINTER(Conv3dDesc), c_p, c_p, c_p, c_i32, c_p, c_i64, c_p]),
+    "vs_conv3d_dw_workspace_bytes": (c_sz, [ctypes.POINTER(Conv3dDesc)]),
+    "vs_conv3d_dw": (ctypes.c_int, [ctypes.POINTER(Conv3dDesc), c_p, c_p, c_p, c_i32, c_p, c_i64, c_p]),
+    "vs_bn3d_stats_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "vs_bn3d_stats": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
+                                     c_p, c_p]),
+    "vs_bn3d_apply": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_p]),
+    "vs_bn3d_bwd_workspace_bytes": (c_sz, [c_i64, c_i64]),
+    "vs_bn3d_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "vs_to_channels_last": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "vs_avgpool3d": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "vs_avgpool3d_bwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "vs_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "vs_timing_collect": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
     "vs_timing_bytes": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
@@ -176,7 +201,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        for which, st in enumerate((GemmDesc, VitLayer, VitLayerGrad)):
+        for which, st in enumerate((GemmDesc, VitLayer, VitLayerGrad, Conv3dDesc)):
             got = handle.vs_struct_size(which)
             if got != ctypes.sizeof(st):
                 raise VsError(f"ABI mismatch: {st.__name__} is {ctypes.sizeof(st)} B in Python, {got} B in C")
