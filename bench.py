@@ -87,6 +87,12 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--c3-warmup", type=int, default=3)
     ap.add_argument("--c3-profile-steps", type=int, default=2)
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the C4 sub-record (R3D-18, 32x112x112 clips, n = 256, fp32) the default C2 run appends")
+    ap.add_argument("--c4-batch", type=int, default=16, help="C4 sub-record clips per GPU")
+    ap.add_argument("--c4-steps", type=int, default=10)
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--c4-profile-steps", type=int, default=2)
     ap.add_argument("--graph", action="store_true",
                     help="time the step as a hipGraph replay (vspike.graph.GraphedStep; N=1 only).  Off by default: "
                          "on MI355X the replay measured 6.20 vs 5.62 ms/step eager (DESIGN.md section 7)")
@@ -366,7 +372,7 @@ def _param_digest(model, dev):
 def _setup(spec, dev, rank):
     """Model, config, criterion and the synthetic batch of one workload (spec: model, neurons, dtype,
     frames, freeze, lr, loss, batch)."""
-    from vspike import VideoMAE, load_run_config, make_criterion
+    from vspike import load_run_config, make_criterion
     cfg_dir = os.path.join(ROOT, "video-spike_amd", "config")
     config = load_run_config(os.path.join(cfg_dir, "model", spec["model"] + ".yaml"),
                              os.path.join(cfg_dir, "train", "vmae_video.yaml"))
@@ -382,7 +388,8 @@ def _setup(spec, dev, rank):
     config["training"]["loss"] = spec["loss"]
     criterion = make_criterion(config)
     torch.manual_seed(1234)                      # identical replicas (GradExchange also broadcasts)
-    model = VideoMAE(config["model"]).to(dev)
+    from vspike import NAME2MODEL
+    model = NAME2MODEL[config["model"]["model_class"]](config["model"]).to(dev)
     bb = model.backbone
     B = spec["batch"] if spec.get("batch") else int(config["training"]["train_batch_size"])
     g = torch.Generator(device=dev).manual_seed(100 + rank)             # each rank its own clips
@@ -602,6 +609,143 @@ def c3_subrecord(args, world, rank, dev):
     return out
 
 
+PEAK_F32 = PEAK_F32_TFLOPS
+
+
+def r3d_flops(cfg, B):
+    """Algorithmic FLOPs of one R3D-18 train step on B clips: per conv 2 Mo Co K (forward), the same
+    for dW, and for dX (every conv but the stem: the pixels need no gradient); the head is negligible.
+    Returns (forward, dX, dW)."""
+    from vspike.r3d import r3d_convs
+
+    def out(shape, c):
+        return tuple((shape[i] + 2 * c.p[i] - c.k[i]) // c.s[i] + 1 for i in range(3))
+
+    def flops(o, c):
+        return 2.0 * B * o[0] * o[1] * o[2] * c.co * c.k[0] * c.k[1] * c.k[2] * c.ci_ref
+    convs = {c.name: c for c in r3d_convs(cfg)}
+    stem = convs["stem.0"]
+    cur = out((cfg.num_frames, cfg.image_size, cfg.image_size), stem)
+    fwd, dx = flops(cur, stem), 0.0
+    for li, nb in enumerate(cfg.layers):
+        for b in range(nb):
+            pre = f"layer{li + 1}.{b}."
+            o = out(cur, convs[pre + "conv1.0"])
+            names = [pre + "conv1.0", pre + "conv2.0"] + ([pre + "downsample.0"] if pre + "downsample.0" in convs else [])
+            for nm in names:
+                f = flops(o, convs[nm])
+                fwd += f
+                dx += f
+            cur = o
+    return fwd, dx, fwd
+
+
+def c4_subrecord(args, world, rank, dev):
+    """BASELINE C4 in the same run: the R3D-18 encoder (32 x 112 x 112 clips, n = 256, fp32; the R3D
+    plugin, vspike/r3d.py — no reference counterpart) under the reference head:
+    timed train steps (fwd + bwd + AdamW, training-mode BatchNorm) and a full-batch fwd + bwd check
+    against the CPU oracle's restatement (parity unpinned: there is no reference code for this
+    encoder).  The conv kernels are implicit GEMMs on the exact-f32 MFMA: reported against the f32
+    MFMA peak (157.3 TF) and with their operand bytes."""
+    spec = {"model": "r3d18", "neurons": 256, "dtype": "fp32", "frames": None, "freeze": False,
+            "lr": None, "loss": "poisson", "batch": args.c4_batch}
+    config, criterion, model, B, pixels, target = _setup(spec, dev, rank)
+    cfg = model.backbone
+    check = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_ref
+        sd = {k: v.detach().cpu() for k, v in model.reference_state_dict().items()}
+        out0 = model(pixels)
+        loss0 = criterion(out0, target)
+        loss0.backward()
+        lay = model.layout
+        g_enc, g_head = model.enc_flat.grad, model.head_flat.grad
+        gpu_grads = {}
+        for c in lay.convs:
+            gpu_grads[c.name + ".weight"] = lay.enc.view(g_enc, c.name + ".weight")[..., :c.ci_ref].permute(
+                0, 4, 1, 2, 3).cpu()
+            bn = c.name[:-2] + ".1"
+            for suf in (".weight", ".bias"):
+                gpu_grads[bn + suf] = lay.enc.view(g_enc, bn + suf).cpu()
+        for ref_name, slot in (("encoder.weight", "enc_w"), ("encoder.bias", "enc_b"), ("decoder.weight", "dec_w"),
+                               ("decoder.bias", "dec_b")):
+            gpu_grads[ref_name] = lay.head.view(g_head, slot).cpu()
+        gl, gloss = out0.detach().cpu(), float(loss0.detach())
+        model.zero_grad(set_to_none=True)
+        model.load_reference_state_dict(sd)          # undo the check's running-statistics update
+        del out0, loss0
+        t0 = time.perf_counter()
+        ccfg = cpu_ref.R3DCfg(num_frames=cfg.num_frames, image_size=cfg.image_size, num_channels=cfg.num_channels)
+        # the oracle in f64: training-mode BatchNorm over 16 x 100,352 voxels makes torch's f32 CPU
+        # backward itself drift by ~5e-3 of the conv gradients' norms (measured r05), so f32-vs-f32
+        # would not say which side is off
+        P = {k: v.double().clone().requires_grad_() for k, v in sd.items()
+             if not k.endswith(("running_mean", "running_var"))}
+        ref = cpu_ref.r3d18_forward(pixels.cpu().double(), P, ccfg)
+        rloss = cpu_ref.poisson_nll_mean(ref, target.cpu().double())
+        rloss.backward()
+        e_out = float((gl - ref.detach()).abs().max() / ref.detach().abs().max())
+        e_loss = abs(gloss - float(rloss)) / abs(float(rloss))
+        errs = {k: float((gpu_grads[k].double() - P[k].grad.double()).norm() / P[k].grad.double().norm())
+                for k in gpu_grads}
+        # torch's own f32 CPU kernels against the same f64 result: the scale of f32 rounding on these
+        # strongly cancelling BatchNorm-path gradients (the bars below are relative to it)
+        P32 = {k: v.clone().requires_grad_() for k, v in sd.items() if not k.endswith(("running_mean", "running_var"))}
+        cpu_ref.poisson_nll_mean(cpu_ref.r3d18_forward(pixels.cpu(), P32, ccfg), target.cpu()).backward()
+        e32 = {k: float((P32[k].grad.double() - P[k].grad.double()).norm() / P[k].grad.double().norm())
+               for k in gpu_grads}
+        del P32
+        worst_conv = max((k for k in errs if not k.endswith((".1.weight", ".1.bias"))), key=errs.get)
+        worst_bn = max((k for k in errs if k.endswith((".1.weight", ".1.bias"))), key=errs.get)
+        tol = {"log_rates": 1e-4, "loss": 1e-5, "grad_conv_head": 1e-3, "grad_bn_affine": 3e-3,
+               "grad_rule": "a gradient passes at its bar or at 3x torch-f32's distance from f64, the larger"}
+        check = {"what": f"one fwd+bwd of the whole benched batch ({B} clips, training-mode BatchNorm) at the initial "
+                         "weights vs the CPU oracle's R3D-18 restatement run in f64 (oracle/cpu_ref.py r3d18_forward); "
+                         "parity UNPINNED: the reference has no CNN encoder",
+                 "log_rates_maxrel": round(e_out, 8), "loss_rel": round(e_loss, 9),
+                 "worst_conv_head_grad": worst_conv, "worst_conv_head_grad_rel": round(errs[worst_conv], 6),
+                 "worst_conv_head_grad_torch_f32_rel": round(e32[worst_conv], 6),
+                 "worst_bn_grad": worst_bn, "worst_bn_grad_rel": round(errs[worst_bn], 6),
+                 "worst_bn_grad_torch_f32_rel": round(e32[worst_bn], 6), "tolerance": tol,
+                 "ok": bool(e_out < tol["log_rates"] and e_loss < tol["loss"] and all(
+                     errs[k] <= max(tol["grad_bn_affine"] if k.endswith((".1.weight", ".1.bias"))
+                                    else tol["grad_conv_head"], 3.0 * e32[k]) for k in errs)),
+                 "cpu_seconds": round(time.perf_counter() - t0, 1)}
+        del P, ref, rloss
+        _progress(f"C4 check: {check}")
+    run = _train_and_time(model, config, criterion, pixels, target, world, rank, dev, args.c4_steps, args.c4_warmup,
+                          args.c4_profile_steps, tag="C4: ")
+    fwd, dxf, dwf = r3d_flops(cfg, B)
+    clips = world * B * args.c4_steps
+    step_s = run["elapsed"] / args.c4_steps
+    kern = {}
+    for name in ("conv_fwd", "conv_dx", "conv_dw", "bn", "adamw", "gemm"):
+        n, ms, work = run["kern"].get(name, (0, 0.0, 0.0))
+        if not n:
+            continue
+        per_step_ms = ms / args.c4_profile_steps
+        ent = {"ms_per_step": round(per_step_ms, 3), "launches_per_step": round(n / args.c4_profile_steps, 1)}
+        if name.startswith("conv_"):
+            tf = work / (ms / 1e3) / 1e12          # the conv timers carry flops
+            ent.update({"bound": "mfma_f32", "tflops": round(tf, 2), "peak": PEAK_F32, "frac": round(tf / PEAK_F32, 4)})
+        else:
+            gbs = work / (ms / 1e3) / 1e9
+            ent.update({"bound": "hbm", "gbs": round(gbs, 1), "peak": PEAK_HBM_GBS, "frac": round(gbs / PEAK_HBM_GBS, 4)})
+        kern[name] = ent
+    total_tf = (fwd + dxf + dwf) / step_s / 1e12
+    out = {"metric": f"clips/sec ({cfg.num_frames}-frame {cfg.image_size}x{cfg.image_size}) train step",
+           "value": round(clips / run["elapsed"], 3), "unit": "clips/sec", "n_gpus": world, "steps": args.c4_steps,
+           "warmup": args.c4_warmup, "ms_per_step": round(1e3 * step_s, 3), "dtype": "fp32",
+           "config": {"workload": f"C4 R3D-18 {cfg.num_frames}x{cfg.image_size}x{cfg.image_size} -> 256 neurons, "
+                                  "encoder+head fwd+bwd+AdamW (training-mode BatchNorm)", "model": "r3d18",
+                      "global_batch": B * world, "clips_per_gpu": B, "parallelism": f"dp{world}"},
+           "model_tflops": round(total_tf, 2), "f32_mfma_util_pct": round(100 * total_tf / PEAK_F32, 2),
+           "check": check, "final_loss": round(run["final_loss"], 6), "replicas_equal": run["replicas_equal"],
+           "dispatch_per_step": run["dispatch"], "kernels": kern}
+    del run, model
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -674,6 +818,18 @@ def main():
             c3 = {"error": f"{type(exc).__name__}: {exc}"}
             _progress(f"C3 sub-record failed: {c3['error']}")
 
+    c4 = None
+    if not args.no_c4 and args.model == "vmae_tiny" and args.dtype == "bf16" and not args.graph and not args.freeze \
+            and args.loss == "poisson":
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        try:
+            c4 = c4_subrecord(args, world, rank, dev)
+        except Exception as exc:
+            c4 = {"error": f"{type(exc).__name__}: {exc}"}
+            _progress(f"C4 sub-record failed: {c4['error']}")
+
     if rank == 0:
         workload = ("C5 ViT-Base/16 encoder (no temporal transformer: no reference code)"
                     if bb.hidden_size == 768 and bb.num_frames == 32 else
@@ -694,7 +850,7 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
             "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
             "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
-            "knobs_nondefault": L.knobs_nondefault(), "c3": c3,
+            "knobs_nondefault": L.knobs_nondefault(), "c3": c3, "c4": c4,
         }
         if args.graph:
             line["step_mode"] = "hipGraph replay (vspike.graph.GraphedStep)"

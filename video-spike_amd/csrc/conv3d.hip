@@ -287,11 +287,14 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     }
   };
 
-  f32x4 acc[2][2];
+  // blocked accumulation: the MFMA chain runs over 16 steps (512 voxels), then folds into tot —
+  // one f32 chain over a whole split (up to ~40k voxels at 16 clips) lets rounding grow with its
+  // length, and these sums cancel strongly (the gradient of a conv feeding a BatchNorm)
+  f32x4 acc[2][2], tot[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 rd[2], rx[2];
   if (nsteps > 0) {
     load(rd, rx, 0);
@@ -317,8 +320,21 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) store(smem + ((t + 1) & 1) * STAGE, rd, rx);
+    if ((t & 15) == 15) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          tot[i][j] += acc[i][j];
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
     __syncthreads();
   }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] += tot[i][j];
   // partial tile (plain stores; the reduce adds the splits in order)
   float* pt = g.part + (int64_t)split * g.Co * g.Kp;
 #pragma unroll
@@ -436,20 +452,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n4, int C, const 
 }
 
 // backward, pass 1: per block over a contiguous row range, per channel sum g and sum g xhat
-// (g = dout masked by out > 0 under ReLU); partial rows [blocks][2][C]
+// (g = dout masked by out > 0 under ReLU); partial rows [blocks][2][C] in f64.  The sums are kept in
+// f64 from the first add: mean(g) and mean(g xhat) are subtracted from EVERY element's gradient, so
+// their rounding is a coherent error that the next conv's weight-gradient sum over ~10^6 voxels
+// accumulates instead of averaging out (f32 running sums here put 6e-3 of the norm on layer1's dW
+// at 16 clips, against 1e-3 at 2 clips: r05)
 __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const float* __restrict__ dout,
                                                      const float* __restrict__ out, int relu,
                                                      const float* __restrict__ y, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, int64_t rows_per_blk,
-                                                     float* __restrict__ part) {
-  __shared__ float4 red[2][256];
+                                                     double* __restrict__ part) {
+  __shared__ double red[2][4][256];
   const int groups = C / 4;                  // float4 channel groups per row
   const int rpi = 256 / groups;              // rows per iteration (C <= 1024)
   const int t = threadIdx.x, cg = t % groups, ro = t / groups;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk;
   int64_t r1 = r0 + rows_per_blk;
   if (r1 > M) r1 = M;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
   const float4 mu = *(const float4*)(mean + cg * 4), rs = *(const float4*)(rstd + cg * 4);
   if (ro < rpi)
     for (int64_t r = r0 + ro; r < r1; r += rpi) {
@@ -461,45 +481,57 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const flo
         gv.z = o.z > 0.f ? gv.z : 0.f; gv.w = o.w > 0.f ? gv.w : 0.f;
       }
       const float4 yv = *(const float4*)(y + i);
-      s.x += gv.x; s.y += gv.y; s.z += gv.z; s.w += gv.w;
-      q.x = fmaf(gv.x, (yv.x - mu.x) * rs.x, q.x);
-      q.y = fmaf(gv.y, (yv.y - mu.y) * rs.y, q.y);
-      q.z = fmaf(gv.z, (yv.z - mu.z) * rs.z, q.z);
-      q.w = fmaf(gv.w, (yv.w - mu.w) * rs.w, q.w);
+      s[0] += gv.x; s[1] += gv.y; s[2] += gv.z; s[3] += gv.w;
+      q[0] += (double)gv.x * ((yv.x - mu.x) * rs.x);
+      q[1] += (double)gv.y * ((yv.y - mu.y) * rs.y);
+      q[2] += (double)gv.z * ((yv.z - mu.z) * rs.z);
+      q[3] += (double)gv.w * ((yv.w - mu.w) * rs.w);
     }
-  red[0][t] = s;
-  red[1][t] = q;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[0][k][t] = s[k];
+    red[1][k][t] = q[k];
+  }
   __syncthreads();
   if (t < groups) {       // fixed order over the row offsets
-    float4 a = red[0][t], b = red[1][t];
-    for (int k = 1; k < rpi; ++k) {
-      const float4 u = red[0][k * groups + t], v = red[1][k * groups + t];
-      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    double a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = red[0][k][t];
+      b[k] = red[1][k][t];
     }
-    *(float4*)(part + ((int64_t)blockIdx.x * 2) * C + t * 4) = a;
-    *(float4*)(part + ((int64_t)blockIdx.x * 2 + 1) * C + t * 4) = b;
+    for (int o = 1; o < rpi; ++o)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] += red[0][k][o * groups + t];
+        b[k] += red[1][k][o * groups + t];
+      }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      part[((int64_t)blockIdx.x * 2) * C + t * 4 + k] = a[k];
+      part[((int64_t)blockIdx.x * 2 + 1) * C + t * 4 + k] = b[k];
+    }
   }
 }
 
 // pass 2: per channel the totals (f64, block order), dgamma / dbeta (+=), and the apply coefficients
 // coef[0][c] = gamma rstd, coef[1][c] = gamma rstd mean(g), coef[2][c] = gamma rstd mean(g xhat)
-__global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__ part, int nblk, int C, int64_t M,
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict__ part, int nblk, int C, int64_t M,
                                                        const float* __restrict__ gamma, const float* __restrict__ rstd,
                                                        float* dgamma, float* dbeta, float* __restrict__ coef) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
   for (int b = 0; b < nblk; ++b) {
-    s += (double)part[((int64_t)b * 2) * C + c];
-    q += (double)part[((int64_t)b * 2 + 1) * C + c];
+    s += part[((int64_t)b * 2) * C + c];
+    q += part[((int64_t)b * 2 + 1) * C + c];
   }
   if (dgamma) dgamma[c] += (float)q;
   if (dbeta) dbeta[c] += (float)s;
-  const float a = gamma[c] * rstd[c];
-  coef[c] = a;
-  coef[C + c] = a * (float)(s / (double)M);
-  coef[2 * C + c] = a * (float)(q / (double)M);
+  const double a = (double)gamma[c] * (double)rstd[c];
+  coef[c] = (float)a;
+  coef[C + c] = (float)(a * (s / (double)M));
+  coef[2 * C + c] = (float)(a * (q / (double)M));
 }
 
 // pass 3: dy = a g - b - c xhat;  dres = g
@@ -834,7 +866,7 @@ static int64_t bn_bwd_blocks(int64_t M) {
 }  // namespace vs
 
 extern "C" size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C) {
-  return (size_t)(bn_bwd_blocks(M) * 2 * C + 3 * C) * 4 + 256;
+  return (size_t)bn_bwd_blocks(M) * 2 * C * 8 + (size_t)3 * C * 4 + 256;
 }
 
 extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
@@ -849,12 +881,12 @@ extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float*
   ScopedTimer timer(VS_TIMER_BN, s, (double)M * C * (4.0 * (relu ? 3 : 2) + 4.0 + (dres ? 4.0 : 0.0)));
   const int64_t nblk = bn_bwd_blocks(M);
   const int64_t rpb = (M + nblk - 1) / nblk;
-  float* part = (float*)workspace;
-  float* coef = part + nblk * 2 * C;
+  double* part = (double*)workspace;
+  float* coef = (float*)(part + nblk * 2 * C);
   hipLaunchKernelGGL(bn_bwd_reduce, dim3((unsigned)nblk), dim3(256), 0, s, M, (int)C, dout, out, relu, y, mean, rstd,
                      rpb, part);
   VS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const float*)part,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const double*)part,
                      (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef);
   VS_LAUNCH_CHECK();
   const int64_t n4 = M * C / 4;
