@@ -450,6 +450,7 @@ def test_kernel_timers_per_product():
     fused = m._mlp_fused(2)          # D = 192 bf16: the fused MLP kernels replace fc1 / fc2 fwd and dx_fc2
     unused = {"fwd_fc1", "fwd_fc2", "dx_fc2"} if fused else {"fwd_mlp", "dx_mlp"}
     unused |= {"fp8_quant"}          # compute_dtype fp8 only
+    unused |= {"conv_fwd", "conv_dx", "conv_dw", "bn"}   # the R3D encoder's (tests/test_gpu_r3d.py)
     for name in L.TIMER_NAMES[8:] + ("attn_fwd", "attn_bwd", "ln_bwd"):
         n, ms, nbytes = got[name]
         want = 0 if name in unused else (2 * Lh if name.startswith("ln_") else Lh)
