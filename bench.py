@@ -432,12 +432,14 @@ def _train_and_time(model, config, criterion, pixels, target, world, rank, dev, 
         graphed = GraphedStep(trainer, pixels, target)     # the capture counts one step's dispatch
         step_fn = graphed.step
         _barrier_sync(world)
+    L.attn_redo_count(reset=True)            # (synchronising: before the clock starts)
     t0 = time.perf_counter()
     losses = []
     for _ in range(steps):
         losses.append(step_fn(pixels, target))
     _barrier_sync(world)
     elapsed = time.perf_counter() - t0
+    redo = L.attn_redo_count(reset=True) / (1 if graph else steps)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -473,7 +475,7 @@ def _train_and_time(model, config, criterion, pixels, target, world, rank, dev, 
         if serial:
             model.set_side_stream(True)
     return {"elapsed": elapsed, "final_loss": final_loss, "dispatch": dispatch, "replicas_equal": replicas_equal,
-            "kern": kern, "trainer": trainer}
+            "kern": kern, "trainer": trainer, "attn_redo_per_step": redo}
 
 
 def _roofline(kern, profile_steps, bb, B, dtype):
@@ -791,6 +793,7 @@ def main():
                           args.profile_steps, graph=args.graph)
     elapsed, final_loss, replicas_equal, dispatch = run["elapsed"], run["final_loss"], run["replicas_equal"], \
         run["dispatch"]
+    redo = run["attn_redo_per_step"]
     clips = world * B * args.steps
     value = clips / elapsed
     N = bb.num_tokens
@@ -850,7 +853,13 @@ def main():
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "final_loss": round(final_loss, 6),
             "lr": float(config["optimizer"]["lr"]), "loss": args.loss, "backend": args.backend if world > 1 else None,
             "replicas_equal": replicas_equal, "build_id": L.build_id(), "dispatch_per_step": dispatch,
-            "knobs_nondefault": L.knobs_nondefault(), "c3": c3, "c4": c4,
+            "knobs_nondefault": L.knobs_nondefault(),
+            # the attention forward's fast pass (no running max) re-runs a workgroup under the safe
+            # softmax when a query's scores leave its band: how often that happened in the timed steps
+            "attn_redo": {"workgroups_per_step": redo,
+                          "of": bb.num_hidden_layers * B * bb.num_attention_heads * ((N + 127) // 128),
+                          "logit_scale_sweep": "profiles/r05_attn_logit_scale.txt"},
+            "c3": c3, "c4": c4,
         }
         if args.graph:
             line["step_mode"] = "hipGraph replay (vspike.graph.GraphedStep)"

@@ -197,6 +197,11 @@ int vs_mlp_bwd_da(int64_t M, int64_t D, int64_t F, const void* h2, int64_t ldh, 
  * ------------------------------------------------------------------------------------------ */
 int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv,
                 int64_t ld_qkv, void* o, int64_t ld_o, float* lse, float scale, void* stream);
+/* The bf16 forward's fast pass uses no running row maximum: exact while every query's row sum of
+ * exp2(scores) stays within [2^-100, 2^96]; a workgroup with a query outside re-runs its tile under the
+ * safe online softmax.  vs_attn_redo_count: workgroups that re-ran since the last reset (device-wide,
+ * synchronising; reset != 0 zeroes the counter). */
+int vs_attn_redo_count(int64_t* out, int32_t reset);
 size_t vs_attn_bwd_workspace_bytes(int64_t B, int64_t N, int64_t H, int64_t Dh);
 int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64_t Dh, const void* qkv,
                 int64_t ld_qkv, const void* o, int64_t ld_o, const void* dout, int64_t ld_do,

@@ -376,6 +376,10 @@ __device__ __forceinline__ bf16x8 rowsum_selector(int lane) {
   return __builtin_convertvector(v, bf16x8);
 }
 
+// workgroups of the bf16 forward that re-ran their tile under the safe softmax (a query's scores
+// left the fast pass's band): read / reset by vs_attn_redo_count
+__device__ unsigned long long g_attn_redo = 0;
+
 // SW: QK(b) is issued before PV(a), so softmax(b) waits on a chain that ran under PV(a)'s MFMAs
 template <bool SW = false>
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
@@ -500,7 +504,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   // starts from 0).
   //  FAST pass (SAFE = 0): p = exp2(s) against a fixed reference 0 — no row maximum, no rescale,
   //    no per-score subtraction; row sums on the matrix pipe (lacc).  Exact whenever every query's
-  //    scores stay within about [-60, 60] (log2 units); the epilogue checks the row sums and, if
+  //    scores stay within about [-100, 85] (log2 units); the epilogue checks the row sums and, if
   //    any query of the workgroup is outside that band (or overflowed), the workgroup re-runs
   //  SAFE pass (SAFE = 1): online softmax against a running reference that is raised lazily (a
   //    wave-uniform rare branch when a score exceeds it by 2^kRefBand, guide T13) and is set from
@@ -653,12 +657,23 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
         : "memory");
     l = q < 16 ? l0 : l1;
   }
-  // Fast-pass validity: the row sum of every real query within [2^-60, 2^60] (false for NaN/inf).
-  const bool bad = active && qi < N && !(l >= 0x1p-60f && l <= 0x1p60f);
+  // Fast-pass validity: the row sum of every real query within [2^-100, 2^96] (false for NaN/inf) and
+  // its O accumulators finite.  p = exp2(s) is a normal bf16 / f32 number from 2^-126 to 2^127, so
+  // the band only guards the sums: l <= 2^96 keeps every p and the O sums (<= l * max|v|) finite for
+  // |v| < 2^31, and l >= 2^-100 keeps the largest p normal.  (Round 4's [2^-60, 2^60] re-ran every
+  // workgroup with a score above ~41 natural-log units: 1.9-2.2x the forward's time, which
+  // pretrained attention sinks reach; profiles/r05_attn_logit_scale.txt.)
+  bool ofin = true;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ofin = ofin && __builtin_isfinite(oacc[dt][r]);
+  const bool bad = active && qi < N && !(l >= 0x1p-100f && l <= 0x1p96f && ofin);
   __syncthreads();  // every wave is done with the last K/V tile; redo_flag = 0 is visible
   if (__any(bad) && lane == 0) redo_flag = 1;
   __syncthreads();
   if (redo_flag) {  // workgroup-uniform: the whole workgroup streams K/V again, safe softmax
+    if (tid == 0) atomicAdd(&g_attn_redo, 1ull);
     pass(IC<1>{});
     l = pair_sum(l_half);
     __syncthreads();
@@ -1532,6 +1547,20 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     VS_REQUIRE(false, "vs_attn_fwd: bad dtype");
   }
   VS_LAUNCH_CHECK();
+  return VS_OK;
+}
+
+extern "C" int vs_attn_redo_count(int64_t* out, int32_t reset) {
+  VS_REQUIRE(out, "vs_attn_redo_count: null pointer");
+  unsigned long long v = 0;
+  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(vs::g_attn_redo), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return (int)e;
+  *out = (int64_t)v;
+  if (reset) {
+    const unsigned long long z = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(vs::g_attn_redo), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return (int)e;
+  }
   return VS_OK;
 }
 

@@ -135,6 +135,7 @@ PROTOTYPES = {
                                      c_i64, c_p]),
     "vs_attn_fwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_f32, c_p]),
     "vs_attn_bwd_workspace_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "vs_attn_redo_count": (ctypes.c_int, [ctypes.POINTER(c_i64), c_i32]),
     "vs_attn_bwd": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,
                                    c_p, c_i64, c_p, c_f32, c_p]),
     "vs_patch_im2col": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
@@ -272,6 +273,13 @@ def dispatch_counts() -> dict:
 
 def dispatch_reset() -> None:
     lib().vs_dispatch_reset()
+
+
+def attn_redo_count(reset: bool = False) -> int:
+    """Workgroups of the bf16 attention forward that re-ran under the safe softmax (vs_attn_redo_count)."""
+    v = c_i64()
+    check(lib().vs_attn_redo_count(ctypes.byref(v), int(reset)), "vs_attn_redo_count")
+    return int(v.value)
 
 
 def knob_get(name: str) -> int:
