@@ -579,7 +579,9 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 #define VS_PATH_PATCH_DW     21   /* vs_patch_embed_dw: patch dW with the tubelet gather in its B-load */
 #define VS_PATH_CONV_IGEMM   22   /* conv_igemm_kernel: Conv3d forward / dX as an implicit GEMM (f32 MFMA) */
 #define VS_PATH_CONV_DW      23   /* conv_dw_kernel: Conv3d weight gradient (implicit-GEMM gather, split over rows) */
-#define VS_PATH_COUNT        24
+#define VS_PATH_GEMM_G256    24   /* gemm_bf16_g256_kernel: 256 x 256 persistent tiles, 64-deep LDS-DMA stages (long-M ViT-Base products) */
+#define VS_PATH_GEMM_DW256   25   /* gemm_dw256_kernel: long-K weight gradients on 256 x 256 persistent tiles + fixed-order reduce */
+#define VS_PATH_COUNT        26
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);
 int vs_dispatch_reset(void);
@@ -617,7 +619,11 @@ int vs_dispatch_reset(void);
 #define VS_KNOB_SLAB_WV     25   /* row-slab GEMM waves per workgroup: 4 or 8 (0 = by slab length) */
 #define VS_KNOB_WRES_WV     26   /* W-resident GEMM waves per workgroup: 8, else 4 */
 #define VS_KNOB_WRES_DBG    27   /* VS_DEBUG_KNOBS builds only (ignored otherwise): W-resident GEMM 1 = L2-resident stores, 2 = L2-resident reads (WRONG results) */
-#define VS_KNOB_COUNT       32
+#define VS_KNOB_G256        28   /* long-M products on the 256 x 256 persistent kernel: 0 = where measured faster (N or K >= 2304, not the GELU' product), 1 = every eligible product, 2 = never (256 x 128 big tile) */
+#define VS_KNOB_G256_GRID   29   /* 256 x 256 persistent GEMM grid cap (0 = 256: one workgroup per CU) */
+#define VS_KNOB_G256_DBG    30   /* VS_DEBUG_KNOBS builds only: 256 x 256 GEMM bit 0 = no operand DMA, bit 1 = no epilogue stores (WRONG results) */
+#define VS_KNOB_NO_DW256    31   /* 1: the long-K dW products on the split-K dW kernel instead of the 256 x 256 persistent one */
+#define VS_KNOB_COUNT       40
 int vs_knob_get(int knob);               /* VS_EINVAL for an unknown id */
 int vs_knob_set(int knob, int value);    /* returns the previous value; VS_EINVAL for an unknown id */
 int vs_knob_default(int knob);           /* the built-in default of a knob (before the environment) */

@@ -176,28 +176,73 @@ def layer_norm(x, g, b, eps):
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), g, b, eps)
 
 
-def vit_layer(x: torch.Tensor, P: Dict[str, torch.Tensor], prefix: str, cfg: ViTCfg) -> torch.Tensor:
-    """One pre-LN block, `modeling_videomae.py:419-445` with `VideoMAESelfAttention` :230-266."""
+def _plain_mm(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return a @ w.T
+
+
+def vit_layer(x: torch.Tensor, P: Dict[str, torch.Tensor], prefix: str, cfg: ViTCfg, mm=None) -> torch.Tensor:
+    """One pre-LN block, `modeling_videomae.py:419-445` with `VideoMAESelfAttention` :230-266.
+    `mm(a, W)` is the block's four Linear products (qkv, proj, fc1, fc2: a @ W^T by default;
+    `mx_matmul` for the MX-FP8 products of BASELINE C5)."""
+    mm = mm or _plain_mm
     B, N, D = x.shape
     H = cfg.num_attention_heads
     dh = D // H
     h = layer_norm(x, P[prefix + "layernorm_before.weight"], P[prefix + "layernorm_before.bias"],
                    cfg.layer_norm_eps)
-    q = h @ P[prefix + "attention.attention.query.weight"].T + P[prefix + "attention.attention.query.bias"]
-    k = h @ P[prefix + "attention.attention.key.weight"].T            # k bias is identically zero
-    v = h @ P[prefix + "attention.attention.value.weight"].T + P[prefix + "attention.attention.value.bias"]
+    q = mm(h, P[prefix + "attention.attention.query.weight"]) + P[prefix + "attention.attention.query.bias"]
+    k = mm(h, P[prefix + "attention.attention.key.weight"])           # k bias is identically zero
+    v = mm(h, P[prefix + "attention.attention.value.weight"]) + P[prefix + "attention.attention.value.bias"]
     q, k, v = (t.reshape(B, N, H, dh).permute(0, 2, 1, 3) for t in (q, k, v))
     s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
     pr = torch.softmax(s, dim=-1)
     o = (pr @ v).permute(0, 2, 1, 3).reshape(B, N, D)
-    y = x + o @ P[prefix + "attention.output.dense.weight"].T + P[prefix + "attention.output.dense.bias"]
+    y = x + mm(o, P[prefix + "attention.output.dense.weight"]) + P[prefix + "attention.output.dense.bias"]
     h2 = layer_norm(y, P[prefix + "layernorm_after.weight"], P[prefix + "layernorm_after.bias"],
                     cfg.layer_norm_eps)
-    a = torch.nn.functional.gelu(h2 @ P[prefix + "intermediate.dense.weight"].T + P[prefix + "intermediate.dense.bias"])
-    return y + a @ P[prefix + "output.dense.weight"].T + P[prefix + "output.dense.bias"]
+    a = torch.nn.functional.gelu(mm(h2, P[prefix + "intermediate.dense.weight"]) + P[prefix + "intermediate.dense.bias"])
+    return y + mm(a, P[prefix + "output.dense.weight"]) + P[prefix + "output.dense.bias"]
 
 
-def videomae_encoder(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTCfg) -> torch.Tensor:
+def mx_dequant(x: torch.Tensor) -> torch.Tensor:
+    """MX-FP8 round trip of an operand as BASELINE C5's products see it (csrc/fp8.hip:7-10 recipe, the
+    OCP MX format): the value rounded to bf16 (the activations / weights the kernels quantise are
+    bf16), then per 32 consecutive elements of the last axis an E8M0 scale 2^e with e = ceil(log2(
+    amax / 448)) (amax * f32(1/448), clamped to [-126, 127], 0 for an all-zero block) and elements
+    rounded to nearest-even e4m3 (torch.float8_e4m3fn); returned dequantised in f32."""
+    shp = x.shape
+    xb = x.detach().to(torch.bfloat16).float().reshape(*shp[:-1], shp[-1] // 32, 32)
+    amax = xb.abs().amax(-1)
+    bits = (amax * torch.tensor(1.0 / 448.0, dtype=torch.float32)).view(torch.int32)
+    e = ((bits >> 23) & 0xFF) - 127 + ((bits & 0x7FFFFF) != 0).int()
+    e = torch.where(((bits >> 23) & 0xFF) == 0, torch.full_like(e, -126), e).clamp(-126, 127)
+    e = torch.where(amax > 0, e, torch.zeros_like(e))
+    inv = ((127 - e) << 23).view(torch.float32)[..., None]       # 2^-e exactly
+    scale = ((127 + e) << 23).view(torch.float32)[..., None]     # 2^e exactly
+    return ((xb * inv).to(torch.float8_e4m3fn).float() * scale).reshape(shp)
+
+
+class _MXLinear(torch.autograd.Function):
+    """a @ W^T on the MX-FP8 round trips of both operands; the backward is the straight-through one the
+    HIP path runs (bf16 products on the unquantised activations and weights: dA = g W, dW = g^T a)."""
+
+    @staticmethod
+    def forward(ctx, a, w):
+        ctx.save_for_backward(a, w)
+        return mx_dequant(a) @ mx_dequant(w).T
+
+    @staticmethod
+    def backward(ctx, g):
+        a, w = ctx.saved_tensors
+        return g @ w, g.reshape(-1, g.shape[-1]).T @ a.reshape(-1, a.shape[-1])
+
+
+def mx_matmul(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """`mm` for vit_layer: the block products of BASELINE C5's fp8 encoder (compute_dtype "fp8")."""
+    return _MXLinear.apply(a, w)
+
+
+def videomae_encoder(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTCfg, mm=None) -> torch.Tensor:
     """`VideoMAEModel.forward` (modeling_videomae.py:592-715): patch-embed + sinusoid, 12 blocks,
     no final LayerNorm because `use_mean_pooling=True` (:571-574)."""
     B = pixels.shape[0]
@@ -207,19 +252,19 @@ def videomae_encoder(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTC
     x = cols @ w.T + P["video_mae.embeddings.patch_embeddings.projection.bias"]
     x = x.reshape(B, N, D) + sinusoid_table(N, D)
     for i in range(cfg.num_hidden_layers):
-        x = vit_layer(x, P, f"video_mae.encoder.layer.{i}.", cfg)
+        x = vit_layer(x, P, f"video_mae.encoder.layer.{i}.", cfg, mm)
     return x
 
 
 def videomae_plugin_forward(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: ViTCfg,
-                            freeze_encoder: bool = True) -> torch.Tensor:
+                            freeze_encoder: bool = True, mm=None) -> torch.Tensor:
     """`src/model/videomae.py:16-32` from `pixel_values` on (the CPU preprocessing K0 is outside)."""
     B = pixels.shape[0]
     if freeze_encoder:
         with torch.no_grad():
-            hid = videomae_encoder(pixels, P, cfg)
+            hid = videomae_encoder(pixels, P, cfg, mm)
     else:
-        hid = videomae_encoder(pixels, P, cfg)
+        hid = videomae_encoder(pixels, P, cfg, mm)
     z = hid.flatten(1) @ P["encoder.weight"].T + P["encoder.bias"]
     r = z @ P["decoder.weight"].T + P["decoder.bias"]
     return r.reshape(B, 100, -1)

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--rows", type=int, default=200704)
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--dw-nobias", action="store_true", help="dW products without the fused bias gradient")
     a = ap.parse_args()
     M, D, F = a.rows, 768, 3072
     dev = "cuda"
@@ -87,7 +88,8 @@ def main():
         db = torch.zeros(Mo, device=dev)
         ws = torch.empty(ops.splitk_workspace_bytes(bf, Mo, No, M) // 4 + 64, device=dev)
         L.dispatch_reset()
-        t_ours = timeit(lambda: ops.linear_dw(dy, xx, c, db=db, workspace=ws), a.reps)
+        dbb = None if a.dw_nobias else db
+        t_ours = timeit(lambda: ops.linear_dw(dy, xx, c, db=dbb, workspace=ws), a.reps)
         path = [k for k, v in L.dispatch_counts().items() if v]
         fl = 2.0 * M * Mo * No
         line = f"{name:10s} {Mo}x{No}x{M} ours {t_ours:8.1f} us {fl / t_ours / 1e6:7.1f} TF/s ({fl / t_ours / 1e6 / 2500:.3f}) {path}"

@@ -42,12 +42,19 @@ def main(d, out, filt):
             e["lds_conflict_frac"] = a.get("SQ_LDS_BANK_CONFLICT", 0.0) / a["SQ_LDS_IDX_ACTIVE"]
         if "FETCH_SIZE" in a and "WRITE_SIZE" in a:
             e["hbm_bytes"] = (2 * a["FETCH_SIZE"] + a["WRITE_SIZE"]) * 1024.0
+        if "TCC_HIT_sum" in a and "TCC_MISS_sum" in a and a["TCC_HIT_sum"] + a["TCC_MISS_sum"] > 0:
+            e["l2_hit_frac"] = a["TCC_HIT_sum"] / (a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
+        if "TA_BUSY_avr" in a and "GRBM_GUI_ACTIVE" in a:
+            e["ta_busy_frac"] = a["TA_BUSY_avr"] / (a["GRBM_GUI_ACTIVE"] / 8.0)
+        if a.get("TCP_TCC_READ_REQ_sum"):
+            e["l2_read_latency_cycles"] = a.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / a["TCP_TCC_READ_REQ_sum"]
         res[name] = e
     json.dump({"source": d, "kernels": res}, open(out, "w"), indent=1, sort_keys=True)
     for n, e in res.items():
         print(f"{n[:60]:60s} mfma_busy {e.get('mfma_busy_frac', float('nan')):.3f} "
               f"active {e.get('active_frac', float('nan')):.2f} wait {e.get('wait_any_frac', float('nan')):.2f} "
-              f"stall {e.get('wait_inst_frac', float('nan')):.2f}")
+              f"stall {e.get('wait_inst_frac', float('nan')):.2f} l2hit {e.get('l2_hit_frac', float('nan')):.2f} "
+              f"ta {e.get('ta_busy_frac', float('nan')):.2f} l2lat {e.get('l2_read_latency_cycles', float('nan')):.0f}")
 
 
 if __name__ == "__main__":

@@ -345,13 +345,18 @@ C3_PRODUCTS = {
 }
 
 
+@pytest.mark.parametrize("kernel", ["big", "g256"])
 @pytest.mark.parametrize("prod", sorted(C3_PRODUCTS))
-def test_gemm_big_tile_c3_bench128(prod):
+def test_gemm_big_tile_c3_bench128(prod, kernel, knobs):
     """Every C3 block product at its benched size (200,704 rows: VERDICT r4 item 1) on the big-tile
-    path, against fp64 on the device from the same bf16 operands; the dispatch counter shows the
-    big-tile kernel ran.  f32 outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (one bf16 rounding)."""
+    path (the 256 x 128 kernel and the 256 x 256 persistent one, each forced by knob g256), against fp64 on
+    the device from the same bf16 operands; the dispatch counter shows the big-tile kernel ran.  f32
+    outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (one bf16 rounding)."""
     from vspike import ops, _lib as L
     (N, K), bkc, epi = C3_PRODUCTS[prod]
+    if kernel == "g256" and epi == "bias_pos":
+        pytest.skip("the 256 x 256 kernel has no position-table epilogue (the patch embedding stays on the big tile)")
+    knobs("g256", 1 if kernel == "g256" else 2)
     M = 200704
     g = torch.Generator(device=DEV).manual_seed(N + 7 * K)
     x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
@@ -403,7 +408,7 @@ def test_gemm_big_tile_c3_bench128(prod):
         ops.gemm(x, b_dev, out, epilogue=L.EPI_MUL_AUX, aux_in=aux, ld_aux_in=N, **kw)
         ref, tol = ref.mul_(aux.double()), 8e-3
     torch.cuda.synchronize()
-    assert L.dispatch_counts()["gemm_big"] == 1, L.dispatch_counts()
+    assert L.dispatch_counts()["gemm_" + kernel] == 1, L.dispatch_counts()
     err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
     print(f"\n[{prod}] M={M} N={N} K={K} max err / max|ref| = {err:.3e}")
     assert err < tol
@@ -553,13 +558,22 @@ def test_gemm_ln_bwd_fused_bench_rows(knobs, K, wv):
                                    (192, 1536, 200704),
                                    # C3 (videomae-base): dW2, dW1, dWqkv, dWproj and the patch dW from cols
                                    (768, 3072, 200704), (3072, 768, 200704), (2304, 768, 200704),
-                                   (768, 768, 200704), (768, 1536, 200704)])
-def test_dw_bench128_split_plan(shape):
+                                   (768, 768, 200704), (768, 1536, 200704),
+                                   # the 256 x 256 kernel at other token counts (C3 at 16 clips, C5, odd splits)
+                                   (768, 1536, 25088), (2304, 768, 50176), (3072, 768, 64 * 1001)])
+@pytest.mark.parametrize("kernel", ["dw", "dw256"])
+def test_dw_bench128_split_plan(shape, kernel, knobs):
     """The weight gradients at the benched 128 clips (K = 200,704 tokens): the dW-tile kernel with the
-    split plan the timed step uses and its fixed-order reduce, against fp64 on the device; bitwise
-    reproducible; the dispatch counter shows the dW kernel ran."""
+    split plan the timed step uses and its fixed-order reduce, and (256-multiple widths) the 256 x 256
+    persistent dW kernel with its split-ordered reduce, against fp64 on the device; bitwise
+    reproducible; the dispatch counter shows which kernel ran."""
     from vspike import ops, _lib as L
     M, N, K = shape
+    if kernel == "dw256" and (M % 256 or N % 256 or M * N <= 768 * 768):
+        pytest.skip("the 256 x 256 dW kernel takes 256-multiple widths above 768 x 768")
+    if kernel == "dw" and K != 200704:
+        pytest.skip("split-K dW kernel: the benched token count only")
+    knobs("no_dw256", int(kernel == "dw"))
     g = torch.Generator(device=DEV).manual_seed(M + N)
     dy = torch.randn(K, M, device=DEV, generator=g).to(torch.bfloat16)
     x = torch.randn(K, N, device=DEV, generator=g).to(torch.bfloat16)
@@ -573,7 +587,7 @@ def test_dw_bench128_split_plan(shape):
         ops.linear_dw(dy, x, c, db=db, workspace=ws)
         outs.append((c, db))
     torch.cuda.synchronize()
-    assert L.dispatch_counts()["gemm_dw"] == 2
+    assert L.dispatch_counts()["gemm_" + kernel] == 2, L.dispatch_counts()
     ref = dy.double().t() @ x.double() + 0.25
     assert rel(outs[0][0], ref) < 2e-5
     assert rel(outs[0][1], dy.double().sum(0) + 1.5) < 2e-5
@@ -956,7 +970,7 @@ def test_patch_embed_fused_matches_im2col_gemm(knobs, D, geo):
 
 @pytest.mark.parametrize("D", [64, 128, 192, 768])
 @pytest.mark.parametrize("geo", [(2, 16, 3, 224, 224), (3, 8, 3, 112, 112), (1, 4, 1, 32, 48), (128, 16, 3, 224, 224)])
-def test_patch_embed_dw_matches_im2col_dw(D, geo):
+def test_patch_embed_dw_matches_im2col_dw(D, geo, knobs):
     """vs_patch_embed_dw (the tubelet gather in the dW kernel's B-operand load, no cols) against
     vs_patch_im2col + the dW product of vs_gemm on the same inputs: the same bf16 operand rounding,
     split plan, MFMA order and fixed-order split reduce, so dW and db agree to the last bit (both
@@ -984,6 +998,7 @@ def test_patch_embed_dw_matches_im2col_dw(D, geo):
     cols = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
     ops.patch_im2col(px, cols, t, p)
     dw2, db2 = dw0.clone(), db0.clone()
+    knobs("no_dw256", 1)          # the same split-K dW kernel as the gather path (bitwise comparison)
     ops.linear_dw(dx, cols, dw2, db=db2)
     torch.cuda.synchronize()
     assert torch.equal(dw, dw2) and torch.equal(db, db2)

@@ -249,9 +249,11 @@ def test_vit_tiny12_b16_encoder_only_curve(golden, dtype, dispatch):
 
 
 # kernel paths of the C3 (videomae-base width) bf16 step at the bench's 128 clips: every block product
-# on the big-tile kernel (D = 768 / F = 3072), the dW split plan, flash attention, the skinny head, and the
-# patch embedding as im2col + the big-tile GEMM (its dW from cols on the dW kernel)
-BENCH_PATHS_C3 = ("gemm_big", "gemm_dw", "gemm_skinny", "attn_fwd", "attn_bwd")
+# on the big-tile kernels (D = 768 / F = 3072: 256 x 256 persistent tiles where N or K >= 2304, 256 x 128
+# tiles for the rest), the qkv / fc1 / fc2 weight gradients on the 256 x 256 persistent dW kernel (the
+# projection's on the split-K dW tiles), flash attention,
+# the skinny head, and the patch embedding as im2col + the big-tile GEMM
+BENCH_PATHS_C3 = ("gemm_big", "gemm_g256", "gemm_dw256", "gemm_dw", "gemm_skinny", "attn_fwd", "attn_bwd")
 
 
 @pytest.mark.parametrize("dtype,dispatch", [("fp32", "b16"), ("bf16", "b16"), ("bf16", "b128")])
@@ -279,8 +281,11 @@ def test_vit_base2l_b16_benched_dispatch_forward_backward(golden, dtype, dispatc
     else:
         missing = [p for p in BENCH_PATHS_C3 if not counts.get(p)]
         assert not missing, (missing, counts)
-        # 2 layers x (4 forward + 4 dX products) + the patch GEMM on the big-tile kernel
-        assert counts["gemm_big"] >= 2 * 8 + 1, counts
+        # 2 layers x (4 forward + 4 dX products) + the patch GEMM on the big-tile kernels; per layer qkv,
+        # fc1, fc2, dX of fc1 and of qkv on the 256 x 256 one
+        assert counts["gemm_big"] + counts["gemm_g256"] >= 2 * 8 + 1, counts
+        assert counts["gemm_g256"] >= 2 * 5, counts
+        assert counts["gemm_dw256"] >= 2 * 3, counts        # dW of qkv, fc1, fc2 per layer
         assert out_err < BF16_OUT and loss_err < BF16_LOSS
         bad = {k: v for k, v in errs.items() if v > BF16_GRAD}
         assert not bad, bad

@@ -1592,6 +1592,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
                 acc[i][j][r] * e.alpha;
     }
     __syncthreads();
+    // the 4 passes' operands are fetched before the first store (epi_eight_fetch: one store round
+    // trip per half-tile instead of one per pass)
+    EpiOps8 ops[EF == kEpiRuntime ? 1 : 4];
+    if constexpr (EF != kEpiRuntime) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int64_t m = m0 + part * 128 + p * 32 + tid / CPR, n = n0 + (tid % CPR) * 8;
+        epi_eight_fetch<EF>(e, m < e.M ? m : e.M - 1, n, ops[p], false);
+      }
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int rr = p * 32 + tid / CPR, cg = tid % CPR;
@@ -1602,10 +1612,576 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
         const float4 a = *(const float4*)src;
         const float4 b = *(const float4*)(src + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        epi_eight<EF>(e, m, n, v, false);
+        if constexpr (EF != kEpiRuntime) epi_eight_finish<EF>(e, m, n, v, ops[p], false);
+        else epi_eight<EF>(e, m, n, v, false);
       }
     }
   }
+}
+
+// ----------------------------------------------------------------------------------------------
+// 256 x 256 persistent bf16 GEMM for the long-M block products of ViT-Base (C3: M = 200,704 token
+// rows, N in {768, 2304, 3072}, K in {768, 2304, 3072}) where it beats the 256 x 128 big tile (VS_KNOB_G256).
+//   * one persistent workgroup per CU (8 waves, 2 x 4, 128 x 64 outputs per wave: 4 x 4 16x16x32
+//     MFMAs per 8 fragment reads), tiles dealt XCD-contiguously (a tile's A row-panel and the
+//     weights stay in that XCD's L2);
+//   * 64-deep k stages (2 x 32 KB: A and B images with 128-B rows), two LDS slots: the stage after
+//     the current one is issued at its start and waited for at its last phase; the ring runs ACROSS
+//     tiles, so the next tile's first stage loads under this tile's last stage and epilogue.  Full
+//     128-B row segments per DMA piece (8 rows x 128 B): round 5's first version used 32-deep stages
+//     whose pieces were 16 rows x 64 B, half-line requests that doubled the address path's work
+//     (cdna_hip_programming.md: fragment-shaped 64-B loads +18-45 %);
+//   * four phases per stage (k half x row half), the next phase's fragments read before the current
+//     phase's MFMAs; one vmcnt(0) + raw barrier per stage;
+//   * the product is computed transposed (C^T = B^T A^T on the MFMA), so a lane's accumulator quad is
+//     4 consecutive output columns of one row: the epilogue works straight from registers with 8-B
+//     (bf16) / 16-B (f32) vector loads and stores, no LDS staging, ring untouched.
+// Operand images (per stage): A K-contiguous [256 rows][64 k] (128-B rows, 16-B chunk ^= (r >> 1) & 7:
+// conflict-free ds_read_b128 over each 16-lane group); B K-contiguous likewise, or N-contiguous
+// [64 k][256 n] (512-B rows, chunk ^= swz_mc(k): conflict-free ds_read_tr16_b64 pairs).
+// ----------------------------------------------------------------------------------------------
+// a wave-uniform pointer pinned to SGPRs (the saddr operand of the asm DMA)
+__device__ __forceinline__ const char* sgpr_ptr(const char* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const char*)(((uint64_t)hi << 32) | lo);
+}
+
+struct G256Map {
+  int tiles_n, tiles, per_xcd, nk;  // nk = K / 64 stages per tile
+  int dbg;  // VS_DEBUG_KNOBS builds: VS_KNOB_G256_DBG
+};
+
+template <bool BKC, uint32_t EF>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                                const bf16_t* __restrict__ B, int64_t ldb,
+                                                                G256Map g, EpiParams e) {
+  constexpr int AB = 256 * 64 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
+  // this workgroup's tiles: XCD x = blockIdx % 8 owns logical tiles [x * per_xcd, (x+1) * per_xcd)
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, slots = gridDim.x >> 3;
+  const int t_lo = xcd * g.per_xcd;
+  const int t_hi = t_lo + g.per_xcd < g.tiles ? t_lo + g.per_xcd : g.tiles;
+  const int my_tiles = t_lo + slot < t_hi ? (t_hi - t_lo - slot + slots - 1) / slots : 0;
+  const int total = my_tiles * g.nk;  // stages of this workgroup
+  if (total == 0) return;
+#ifdef VS_DEBUG_KNOBS
+  // diagnostic builds only (VS_KNOB_G256_DBG): bit 0 skips the operand DMA (MFMAs on stale LDS), bit
+  // 1 the epilogue's stores -- the k-loop, the memory stream and the epilogue timed apart
+  const int dbg = g.dbg;
+#else
+  constexpr int dbg = 0;
+#endif
+  auto tile_of = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
+    const int L = t_lo + slot + k * slots;
+    m0 = (L / g.tiles_n) * 256;
+    n0 = (L % g.tiles_n) * 256;
+  };
+
+  // ---- DMA: stage s -> slot s & 1; wave w fills rows 32w .. 32w+31 of the A image (4 pieces of
+  // 8 rows x 128 B) and the same of B (or k rows 8w .. 8w+7 of an N-contiguous B: 4 pieces of
+  // 2 k-rows x 512 B).  Per-lane byte offsets are stage-invariant (the tile / k base is an SGPR).
+  uint32_t a_off[4], b_off[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = wid * 32 + p * 8 + (lane >> 3);
+    a_off[p] = (uint32_t)(r * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4));
+    if constexpr (BKC) {
+      b_off[p] = (uint32_t)(r * ldb * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4));
+    } else {
+      const int k = wid * 8 + 2 * p + (lane >> 5);
+      b_off[p] = (uint32_t)(k * ldb * 2 + ((((lane & 31) ^ swz_mc<128>(k))) << 4));
+    }
+  }
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    if (dbg & 1) return;
+    const int k = s / g.nk, t = s - k * g.nk;
+    int m0, n0;
+    tile_of(k, m0, n0);
+    char* st = smem + (s & 1) * STAGE + wid * 4096;
+    const int64_t mrows = e.M - m0;  // rows past M re-read row M-1 (never stored)
+    const char* abase = sgpr_ptr((const char*)(A + (int64_t)m0 * lda + (int64_t)t * 64));
+    if (mrows >= 256) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int r = wid * 32 + p * 8 + (lane >> 3), rc = r < mrows ? r : (int)mrows - 1;
+        glds16_asm_so(abase, (uint32_t)(rc * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4)), st + p * 1024);
+      }
+    }
+    const char* bbase = sgpr_ptr(BKC ? (const char*)(B + (int64_t)n0 * ldb + (int64_t)t * 64)
+                                     : (const char*)(B + (int64_t)t * 64 * ldb + n0));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) glds16_asm_so(bbase, b_off[p], st + AB + p * 1024);
+  };
+
+  // ---- fragments (per lane, stage-invariant byte offsets; kk = 32-deep half of the stage)
+  const int fr = lane & 15, fc = lane >> 4;
+  int a_rd[2], b_rd[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) a_rd[kk] = (wr * 128 + fr) * 128 + (((kk * 4 + fc) ^ ((fr >> 1) & 7)) << 4);
+  if constexpr (BKC) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) b_rd[kk][0] = AB + (wc * 64 + fr) * 128 + (((kk * 4 + fc) ^ ((fr >> 1) & 7)) << 4);
+  } else {  // k rows kr0 / kr1 of a 32-deep half (swz_mc has period 16 in k: the second half is + 16 KB)
+    const int q = fr >> 2, p4 = (lane & 3) * 4, kr0 = 8 * fc + q, kr1 = kr0 + 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc * 64 + j * 16 + p4;
+      b_rd[j][0] = AB + kr0 * 512 + (((col >> 3) ^ swz_mc<128>(kr0)) << 4) + (col & 7) * 2;
+      b_rd[j][1] = AB + kr1 * 512 + (((col >> 3) ^ swz_mc<128>(kr1)) << 4) + (col & 7) * 2;
+    }
+  }
+  auto read_a = [&](const char* st, int kk, int rh, bf16x8 (&af)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) af[f] = *(const bf16x8*)(st + a_rd[kk] + (rh * 64 + f * 16) * 128);
+  };
+  auto read_b = [&](const char* st, int kk, bf16x8 (&bf)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (BKC) {
+        bf[j] = *(const bf16x8*)(st + b_rd[kk][0] + j * 16 * 128);
+      } else {
+        short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st + b_rd[j][0] + kk * 16384));
+        short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st + b_rd[j][1] + kk * 16384));
+        typedef __attribute__((ext_vector_type(8))) short short8v;
+        short8v v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+        bf[j] = __builtin_bit_cast(bf16x8, v);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Epilogue straight from the accumulators (C^T layout: lane (fr, fc) holds row m0+...+fr, the 4
+  // columns n0+...+4fc..+3 of each 16 x 16 block).  CDNA4's vmcnt counts stores as well as loads
+  // and retires them in order, so a "load operand -> use -> store" sequence per block would wait
+  // for every earlier store; every operand a group of rows needs is loaded before its first store:
+  // the bias once per tile, the residual / GELU' factor per 32 rows of the wave.
+  auto epilogue = [&](int k) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_of(k, m0, n0);
+    constexpr uint32_t F = EF;
+    constexpr bool BIAS = (F & VS_EPI_BIAS) != 0, RES = (F & VS_EPI_RESIDUAL) != 0;
+    constexpr bool AUXIN = (F & (VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) != 0, GELU = (F & VS_EPI_GELU) != 0;
+    const int ncol = n0 + wc * 64 + 4 * fc;
+    float bias[4][4];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) ld4(e.bias, ncol + jj * 16, 0, bias[jj]);
+    }
+    constexpr int GR = 2;  // row fragments per operand group (32 VGPRs of f32 operands)
+#pragma unroll
+    for (int h = 0; h < 8 / GR; ++h) {
+      float opnd[GR][4][4];
+      if constexpr (RES || AUXIN) {
+#pragma unroll
+        for (int ii = 0; ii < GR; ++ii) {
+          const int64_t m = m0 + wr * 128 + (GR * h + ii) * 16 + fr;
+          const int64_t mc = m < e.M ? m : e.M - 1;     // rows past M: any valid row (not stored)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            if constexpr (RES) ld4(e.residual, mc * e.ldr + ncol + jj * 16, 0, opnd[ii][jj]);
+            else ld4(e.aux_in, mc * e.ld_aux_in + ncol + jj * 16, e.op_bf16, opnd[ii][jj]);
+          }
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < GR; ++ii) {
+        const int i = GR * h + ii;
+        const int64_t m = m0 + wr * 128 + i * 16 + fr;
+        const bool live = m < e.M;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          float v[4], t[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = acc[i][jj][r] * e.alpha;
+            if constexpr (BIAS) v[r] += bias[jj][r];
+          }
+          if constexpr ((F & VS_EPI_GELU_BWD) != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] *= gelu_fast_grad(opnd[ii][jj][r]);
+          }
+          if constexpr ((F & VS_EPI_MUL_AUX) != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] *= opnd[ii][jj][r];
+          }
+          const int64_t n = ncol + jj * 16;
+          if constexpr (GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = bf2f(f2bf(v[r]));
+              if constexpr ((F & VS_EPI_GELU_GRAD) != 0) v[r] = gelu_fast_both(x, t[r]);
+              else {
+                t[r] = v[r];
+                v[r] = gelu_fast(x);
+              }
+            }
+            if (live && !(dbg & 2)) st4(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, t);
+          }
+          if constexpr (RES) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += opnd[ii][jj][r];
+          }
+          if (live && !(dbg & 2)) st4(e.c, m * e.ldc + n, e.out_bf16, v);
+          acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  };
+
+  auto mfma16 = [&](const bf16x8 (&bc)[4], const bf16x8 (&af)[4], int rh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[rh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], af[i], acc[rh * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: stage 0 landed, its first fragments in registers
+  bf16x8 a0[4], a1[4], b0[4], b1[4];
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_b(smem, 0, b0);
+  read_a(smem, 0, 0, a0);
+
+  // Stage s (slot s & 1), four phases; fragments of the next phase are read before this phase's MFMAs:
+  //   P0: DMA stage s+1 into the other slot (every wave's reads of stage s-1 retired before the
+  //       barrier of s-1's P3) | A(kk0, rh1) | MFMA B0 x A(kk0, rh0)
+  //   P1: B(kk1), A(kk1, rh0) | MFMA B0 x A(kk0, rh1)
+  //   P2: A(kk1, rh1) | MFMA B1 x A(kk1, rh0)
+  //   P3: vmcnt(0) + lgkmcnt(0) + barrier (stage s+1 landed everywhere; stage s's reads retired) |
+  //       B(kk0), A(kk0, rh0) of stage s+1 | MFMA B1 x A(kk1, rh1) | epilogue at a tile's last stage
+  for (int s = 0; s < total; ++s) {
+    const char* cur = smem + (s & 1) * STAGE;
+    if (s + 1 < total) issue(s + 1);
+    read_a(cur, 0, 1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b0, a0, 0);
+    read_b(cur, 1, b1);
+    read_a(cur, 1, 0, a0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b0, a1, 1);
+    read_a(cur, 1, 1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b1, a0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < total) {
+      const char* nxt = smem + ((s + 1) & 1) * STAGE;
+      read_b(nxt, 0, b0);
+      read_a(nxt, 0, 0, a0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b1, a1, 1);
+    if ((s + 1) % g.nk == 0) epilogue(s / g.nk);
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// 256 x 256 persistent weight-gradient GEMM: dW[M][N] += dY^T X over the token axis for the long-K
+// products of ViT-Base (C3: K = 200,704 tokens; M, N in {768, 2304, 3072}), VERDICT r4 item 3 ("a
+// true long-K GEMM with few splits and large tiles").  Same engine as gemm_bf16_g256_kernel (8 waves,
+// 128 x 64 per wave, C^T on the MFMA, 64-deep stages of 2 x 32 KB, two slots, one barrier per
+// stage), with both operands token-major: A = dY [K][M] and B = X [K][N] are staged as [64 k][256]
+// images (512-B rows, chunk ^= swz_mc(k)) and BOTH are read by ds_read_tr16_b64.  The token axis is
+// cut into `splits` equal slabs; an item = (split, tile) is processed by one workgroup and its f32
+// 256 x 256 partial goes to the workspace, which gemm_dw256_reduce sums IN SPLIT ORDER into C (C +=
+// sum: bitwise reproducible, no atomics).  Items are dealt XCD-contiguously, split-major: the
+// workgroups of one XCD share one token slab's A and B rows in its L2.  The bias gradient (row sums
+// of dY) is summed from the staged A image by VALU, spread over the tile's N-column items (item
+// (mt, nt) takes the k rows r % tiles_n == nt), into per-item partial rows reduced the same way.
+// A tile's A fragment offsets differ per 16-row fragment only in chunk bits 1-3, which the k-row
+// swizzle also uses: the read address is a lane constant XOR an immediate (one v_xor per read).
+// ----------------------------------------------------------------------------------------------
+struct Dw256Map {
+  int tiles_n, tiles, items, per_xcd, kps, nk;
+};
+
+template <bool SUMS>
+__global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                            const bf16_t* __restrict__ B, int64_t ldb, Dw256Map g,
+                                                            float* __restrict__ part, float* __restrict__ sums) {
+  constexpr int AB = 64 * 256 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB (+ 16 KB of bias partials)
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (SUMS ? 16 * 256 * 4 : 0)];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, slots = gridDim.x >> 3;
+  const int i_lo = xcd * g.per_xcd;
+  const int i_hi = i_lo + g.per_xcd < g.items ? i_lo + g.per_xcd : g.items;
+  const int my_items = i_lo + slot < i_hi ? (i_hi - i_lo - slot + slots - 1) / slots : 0;
+  if (my_items == 0) return;
+  auto item_of = [&](int k) __attribute__((always_inline)) { return i_lo + slot + k * slots; };
+  auto steps_of = [&](int item) __attribute__((always_inline)) {
+    const int k0 = (item / g.tiles) * g.kps;
+    return g.nk - k0 < g.kps ? g.nk - k0 : g.kps;
+  };
+
+  // ---- DMA: wave w fills k rows 8w .. 8w+7 of both images (4 pieces of 2 k-rows x 512 B each)
+  uint32_t a_off[4], b_off[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int k = wid * 8 + 2 * p + (lane >> 5), c = ((lane & 31) ^ swz_mc<128>(k)) << 4;
+    a_off[p] = (uint32_t)(k * lda * 2 + c);
+    b_off[p] = (uint32_t)(k * ldb * 2 + c);
+  }
+  auto issue = [&](int item, int t, int slot_s) __attribute__((always_inline)) {
+    const int sp = item / g.tiles, tile = item - sp * g.tiles, mt = tile / g.tiles_n, nt = tile - mt * g.tiles_n;
+    const int64_t k0 = (int64_t)(sp * g.kps + t) * 64;
+    char* st = smem + slot_s * STAGE + wid * 4096;
+    const char* abase = sgpr_ptr((const char*)(A + k0 * lda + (int64_t)mt * 256));
+    const char* bbase = sgpr_ptr((const char*)(B + k0 * ldb + (int64_t)nt * 256));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) glds16_asm_so(bbase, b_off[p], st + AB + p * 1024);
+  };
+
+  // ---- fragments: lane (fr, fc) reads k rows kr0 = 8 fc + (fr >> 2) and kr0 + 4, columns p4 .. p4+3
+  // of each 16-column block (ds_read_tr16_b64 pairs: the MFMA operand layout row = lane & 15,
+  // k = 8 (lane >> 4) + 0..7).  A: block base wr*128 + rh*64 + f*16 -> address = xa ^ ((rh*8 + f*2) << 4).
+  const int fr = lane & 15, fc = lane >> 4;
+  const int q = fr >> 2, p4 = (lane & 3) * 4, kr0 = 8 * fc + q, kr1 = kr0 + 4;
+  const int lc = wr * 16 + (p4 >> 3);
+  const int xa0 = kr0 * 512 + ((lc ^ swz_mc<128>(kr0)) << 4) + (p4 & 7) * 2;
+  const int xa1 = kr1 * 512 + ((lc ^ swz_mc<128>(kr1)) << 4) + (p4 & 7) * 2;
+  int b_rd[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wc * 64 + j * 16 + p4;
+    b_rd[j][0] = AB + kr0 * 512 + (((col >> 3) ^ swz_mc<128>(kr0)) << 4) + (col & 7) * 2;
+    b_rd[j][1] = AB + kr1 * 512 + (((col >> 3) ^ swz_mc<128>(kr1)) << 4) + (col & 7) * 2;
+  }
+  typedef __attribute__((ext_vector_type(8))) short short8v;
+  auto tr_frag = [&](const char* p0, const char* p1) __attribute__((always_inline)) {
+    short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)p0);
+    short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)p1);
+    short8v v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto read_a = [&](const char* st, int kk, int rh, bf16x8 (&af)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int x = (rh * 8 + f * 2) << 4;
+      af[f] = tr_frag(st + kk * 16384 + (xa0 ^ x), st + kk * 16384 + (xa1 ^ x));
+    }
+  };
+  auto read_b = [&](const char* st, int kk, bf16x8 (&bf)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = tr_frag(st + b_rd[j][0] + kk * 16384, st + b_rd[j][1] + kk * 16384);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias-gradient partials: thread -> 8-column group sg = tid & 31 of the A image, k rows
+  // (tid >> 5) + 16 i whose index is = nt (mod tiles_n); the running sums live in a thread-private
+  // LDS slot (8 floats), not in registers (the k-loop holds 232 VGPRs)
+  const int sg = tid & 31, sr = tid >> 5;
+  float* bslot = (float*)(smem + 2 * STAGE) + sr * 256 + sg * 8;
+  if constexpr (SUMS) {
+    *(float4*)bslot = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(bslot + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int bmask = 0;  // bit ii: k row sr + 16 ii belongs to this item's share (recomputed per item)
+  auto set_bmask = [&](int it) __attribute__((always_inline)) {
+    const int nt = (it % g.tiles) % g.tiles_n;
+    bmask = 0;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) bmask |= ((sr + 16 * ii) % g.tiles_n == nt) << ii;
+  };
+  auto bias_rows = [&](const char* st) __attribute__((always_inline)) {
+    if (!bmask) return;
+    float t[8];
+    const float4 s0 = *(const float4*)bslot, s1 = *(const float4*)(bslot + 4);
+    t[0] = s0.x; t[1] = s0.y; t[2] = s0.z; t[3] = s0.w; t[4] = s1.x; t[5] = s1.y; t[6] = s1.z; t[7] = s1.w;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int r = sr + 16 * ii;
+      if ((bmask >> ii) & 1) {
+        const uint4 u = *(const uint4*)(st + r * 512 + ((sg ^ swz_mc<128>(r)) << 4));
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          t[2 * c] += __uint_as_float(w[c] << 16);
+          t[2 * c + 1] += __uint_as_float(w[c] & 0xffff0000u);
+        }
+      }
+    }
+    *(float4*)bslot = make_float4(t[0], t[1], t[2], t[3]);
+    *(float4*)(bslot + 4) = make_float4(t[4], t[5], t[6], t[7]);
+  };
+  auto epilogue = [&](int item) __attribute__((always_inline)) {
+    float* pt = part + (int64_t)item * 65536;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float v[4] = {acc[i][jj][0], acc[i][jj][1], acc[i][jj][2], acc[i][jj][3]};
+        st4(pt, (wr * 128 + i * 16 + fr) * 256 + wc * 64 + jj * 16 + 4 * fc, 0, v);
+        acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    if constexpr (SUMS) {  // the thread's own slot: no barrier needed
+      float* ps = sums + ((int64_t)item * 16 + sr) * 256 + sg * 8;
+      *(float4*)ps = *(const float4*)bslot;
+      *(float4*)(ps + 4) = *(const float4*)(bslot + 4);
+      *(float4*)bslot = make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)(bslot + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto mfma16 = [&](const bf16x8 (&bc)[4], const bf16x8 (&af)[4], int rh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[rh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], af[i], acc[rh * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  bf16x8 a0[4], a1[4], b0[4], b1[4];
+  int item = item_of(0), nsteps = steps_of(item), k = 0, t = 0, s = 0;
+  if constexpr (SUMS) set_bmask(item);
+  issue(item, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_b(smem, 0, b0);
+  read_a(smem, 0, 0, a0);
+  // the four phases of gemm_bf16_g256_kernel's stage loop; (k, t) walks this workgroup's items and
+  // their k-steps, the ring continues across items
+  while (true) {
+    const char* cur = smem + (s & 1) * STAGE;
+    int nk_item = k, nt_step = t + 1;
+    if (nt_step == nsteps) {
+      nk_item = k + 1;
+      nt_step = 0;
+    }
+    const bool more = nk_item < my_items;
+    const int nitem = nk_item == k ? item : (more ? item_of(nk_item) : item);
+    if (more) issue(nitem, nt_step, (s + 1) & 1);
+    read_a(cur, 0, 1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b0, a0, 0);
+    read_b(cur, 1, b1);
+    read_a(cur, 1, 0, a0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b0, a1, 1);
+    read_a(cur, 1, 1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b1, a0, 0);
+    if constexpr (SUMS) bias_rows(cur);  // behind the queued MFMAs (a0's registers are dead here)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (more) {
+      const char* nxt = smem + ((s + 1) & 1) * STAGE;
+      read_b(nxt, 0, b0);
+      read_a(nxt, 0, 0, a0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma16(b1, a1, 1);
+    if (nk_item != k) epilogue(item);
+    if (!more) break;
+    if (nk_item != k) {
+      item = nitem;
+      nsteps = steps_of(item);
+      if constexpr (SUMS) set_bmask(item);
+    }
+    k = nk_item;
+    t = nt_step;
+    ++s;
+  }
+}
+
+// C[m][n] += sum over splits (in order) of the items' partial tiles; bias[m] += the bias partials
+// (splits, then the tile row's N-column items, then the 16 partial rows, in order).  One thread per
+// output float4, then one per bias element.
+__global__ __launch_bounds__(256) void gemm_dw256_reduce(const float* __restrict__ part, const float* __restrict__ sums,
+                                                         Dw256Map g, int splits, int64_t M, int64_t N,
+                                                         float* __restrict__ c, int64_t ldc, float* __restrict__ bias) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, nc4 = M * N / 4;
+  if (i < nc4) {
+    const int64_t m = i / (N / 4), n = (i % (N / 4)) * 4;
+    const int tile = (int)(m / 256) * g.tiles_n + (int)(n / 256);
+    const int64_t off = (m % 256) * 256 + (n % 256);
+    float4 acc = *(const float4*)(part + (int64_t)tile * 65536 + off);
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = *(const float4*)(part + ((int64_t)sp * g.tiles + tile) * 65536 + off);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* cp = (float4*)(c + m * ldc + n);
+    float4 o = *cp;
+    o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+    *cp = o;
+  } else if (bias && i < nc4 + M) {
+    const int64_t m = i - nc4;
+    const int mt = (int)(m / 256), ml = (int)(m % 256);
+    float a = 0.f;
+    for (int sp = 0; sp < splits; ++sp)
+      for (int nt = 0; nt < g.tiles_n; ++nt) {
+        const float* p = sums + ((int64_t)(sp * g.tiles + mt * g.tiles_n + nt) * 16) * 256 + ml;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a += p[r * 256];
+      }
+    bias[m] += a;
+  }
+}
+
+// the split count: every workgroup one item per round (256 slots), the busiest one's k-steps
+// (plus ~4 steps' worth per item for its partial-tile store) minimised, partials <= 128 MB
+struct Dw256Plan {
+  bool valid;
+  int splits;
+  Dw256Map g;
+};
+static Dw256Plan plan_dw256(int64_t M, int64_t N, int64_t K) {
+  Dw256Plan p = {};
+  // 768 x 768 (the projection's dW) measured no faster than the split-K dW tiles: 326 vs 308 us
+  if (M % 256 || N % 256 || K % 64 || K < 64 * 64 || M * N <= 768 * 768) return p;
+  const int64_t tiles = (M / 256) * (N / 256), nk = K / 64;
+  double best = 1e30;
+  for (int64_t S0 = 1; S0 <= 256 && S0 * 8 <= nk; ++S0) {
+    const int64_t kps = (nk + S0 - 1) / S0, S = (nk + kps - 1) / kps;  // no empty last split
+    const int64_t items = tiles * S;
+    if (items * 65536 * 4 > (128ll << 20)) break;
+    const int64_t rounds = (items + 255) / 256;
+    const double t = (double)rounds * (double)(kps + 4);
+    if (t < best - 1e-9) {
+      best = t;
+      p.valid = true;
+      p.splits = (int)S;
+      p.g.kps = (int)kps;
+    }
+  }
+  if (!p.valid) return p;
+  p.g.tiles_n = (int)(N / 256);
+  p.g.tiles = (int)tiles;
+  p.g.items = (int)(tiles * p.splits);
+  p.g.per_xcd = (p.g.items + 7) / 8;
+  p.g.nk = (int)nk;
+  return p;
+}
+static size_t dw256_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  const Dw256Plan p = plan_dw256(M, N, K);
+  return p.valid ? (size_t)p.g.items * (65536 + 16 * 256) * 4 : 0;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1885,6 +2461,17 @@ static void launch_bf16_big_ef(const vs_gemm_desc* d, unsigned nblk, const GridM
     hipLaunchKernelGGL((gemm_bf16_big_kernel<false, EF>), dim3(nblk), dim3(512), 0, s, a, d->lda, b, d->ldb, d->K, g, e);
 }
 
+template <uint32_t EF>
+static void launch_bf16_g256_ef(const vs_gemm_desc* d, const G256Map& g, unsigned grid, const EpiParams& e,
+                                hipStream_t s) {
+  const bf16_t* a = (const bf16_t*)d->a;
+  const bf16_t* b = (const bf16_t*)d->b;
+  if (d->b_kcontig)
+    hipLaunchKernelGGL((gemm_bf16_g256_kernel<true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+  else
+    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+}
+
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
 #define VS_EPI_SWITCH(F, CALL)                                                             \
   switch (F) {                                                                             \
@@ -1898,6 +2485,13 @@ static void launch_bf16_big_ef(const vs_gemm_desc* d, unsigned nblk, const GridM
     case VS_EPI_MUL_AUX: CALL((uint32_t)VS_EPI_MUL_AUX); break;                            \
     default: CALL(kEpiRuntime); break;                                                     \
   }
+
+static void launch_bf16_g256(const vs_gemm_desc* d, const G256Map& g, unsigned grid, const EpiParams& e,
+                             hipStream_t s) {
+#define L_(EF) launch_bf16_g256_ef<EF>(d, g, grid, e, s)
+  VS_EPI_SWITCH(e.flags, L_)
+#undef L_
+}
 
 static void launch_bf16_big(const vs_gemm_desc* d, unsigned nblk, const GridMap& g, const EpiParams& e, hipStream_t s) {
 #define L_(EF) launch_bf16_big_ef<EF>(d, nblk, g, e, s)
@@ -2169,8 +2763,31 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
                     gemm_algorithmic_bytes(d));
   const bool atomic_ok = (f & VS_EPI_ATOMIC) != 0;
   const bool use_ws = atomic_ok && d->workspace && d->workspace_bytes > 0 && aligned16(d->workspace);
-  // token-reduction weight gradients (dW = dY^T X, both operands token-major): the dedicated
-  // split-K kernel with a fixed-order reduce (gemm_dw.hip)
+  // token-reduction weight gradients (dW = dY^T X, both operands token-major): the long-K products
+  // with 256-multiple widths on the 256 x 256 persistent kernel, the rest on the split-K dW kernel
+  // (gemm_dw.hip); both reduce their partials in a fixed order
+  if (!knob(VS_KNOB_NO_DW256) && d->dtype == VS_BF16 && d->out_dtype == VS_F32 && f == VS_EPI_ATOMIC &&
+      !d->a_kcontig && !d->b_kcontig && d->split_k <= 0 && use_ws && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
+      d->ldc % 4 == 0 && aligned16(d->c) && 64 * d->lda * 2 < (1ll << 31) && 64 * d->ldb * 2 < (1ll << 31)) {
+    const Dw256Plan p = plan_dw256(d->M, d->N, d->K);
+    if (p.valid && (size_t)d->workspace_bytes >= dw256_workspace_bytes(d->M, d->N, d->K)) {
+      count_path(VS_PATH_GEMM_DW256);
+      float* part = (float*)d->workspace;
+      float* sums = part + (int64_t)p.g.items * 65536;
+      const unsigned grid = p.g.items < 256 ? (unsigned)((p.g.items + 7) / 8 * 8) : 256u;
+      if (d->a_rowsum)
+        hipLaunchKernelGGL((gemm_dw256_kernel<true>), dim3(grid), dim3(512), 0, s, (const bf16_t*)d->a, d->lda,
+                           (const bf16_t*)d->b, d->ldb, p.g, part, sums);
+      else
+        hipLaunchKernelGGL((gemm_dw256_kernel<false>), dim3(grid), dim3(512), 0, s, (const bf16_t*)d->a, d->lda,
+                           (const bf16_t*)d->b, d->ldb, p.g, part, sums);
+      const int64_t n = d->M * d->N / 4 + (d->a_rowsum ? d->M : 0);
+      hipLaunchKernelGGL(gemm_dw256_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, sums, p.g,
+                         p.splits, d->M, d->N, (float*)d->c, d->ldc, d->a_rowsum);
+      VS_LAUNCH_CHECK();
+      return VS_OK;
+    }
+  }
   if (!knob(VS_KNOB_DW_OLD) && d->dtype == VS_BF16 && d->out_dtype == VS_F32 && f == VS_EPI_ATOMIC && !d->a_kcontig &&
       !d->b_kcontig && d->split_k <= 0 && use_ws && d->K >= 1 && d->M % 8 == 0 && d->N % 8 == 0 &&
       d->lda % 8 == 0 && d->ldb % 8 == 0 && (size_t)d->workspace_bytes >= dw_workspace_bytes(d->M, d->N, d->K))
@@ -2200,6 +2817,36 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     if (d->N == 64) launch_bf16_slab<1>(d, (unsigned)G, e, s);
     else if (d->N == 128) launch_bf16_slab<2>(d, (unsigned)G, e, s);
     else launch_bf16_slab<3>(d, (unsigned)G, e, s);
+    VS_LAUNCH_CHECK();
+    return VS_OK;
+  }
+  // 256 x 256 persistent path: long-M ViT-Base block products (N % 256 == 0, K % 64 == 0, rows
+  // and leading dims addressable with 32-bit per-lane DMA offsets)
+  const bool g256_ef = f == 0 || f == VS_EPI_BIAS || f == (VS_EPI_BIAS | VS_EPI_RESIDUAL) ||
+                       f == (VS_EPI_BIAS | VS_EPI_GELU) || f == VS_EPI_GELU_BWD ||
+                       f == (VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD) || f == VS_EPI_MUL_AUX;
+  const int g256k = knob(VS_KNOB_G256);
+  const bool g256_pick = g256k == 1 || (g256k == 0 && (d->N >= 2304 || d->K >= 2304) && f != VS_EPI_MUL_AUX);
+  if (g256_pick && g256_ef && d->dtype == VS_BF16 && e.op_bf16 &&
+      d->a_kcontig && d->M >= 16384 && d->N % 256 == 0 &&
+      d->K >= 256 && d->K % 64 == 0 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->ldc % 4 == 0 &&
+      !(f & (VS_EPI_ATOMIC)) && 256 * d->lda * 2 < (1ll << 31) && (d->b_kcontig ? d->N * d->ldb : d->K * d->ldb) * 2 <
+      (1ll << 31)) {
+    G256Map g;
+    g.tiles_n = (int)(d->N / 256);
+    g.tiles = (int)(cdiv(d->M, 256) * g.tiles_n);
+    g.nk = (int)(d->K / 64);
+    const int gcap = knob(VS_KNOB_G256_GRID) > 0 ? knob(VS_KNOB_G256_GRID) : 256;
+    int grid = g.tiles < gcap ? (g.tiles + 7) / 8 * 8 : gcap;
+    grid = grid < 8 ? 8 : grid / 8 * 8;
+    g.per_xcd = (int)cdiv(g.tiles, 8);
+#ifdef VS_DEBUG_KNOBS
+    g.dbg = knob(VS_KNOB_G256_DBG);
+#else
+    g.dbg = 0;
+#endif
+    count_path(VS_PATH_GEMM_G256);
+    launch_bf16_g256(d, g, (unsigned)grid, e, s);
     VS_LAUNCH_CHECK();
     return VS_OK;
   }
@@ -2516,9 +3163,11 @@ extern "C" size_t vs_gemm_splitk_workspace_bytes(int32_t dtype, int64_t M, int64
   if (M <= 0 || N <= 0 || K <= 0 || (dtype != VS_F32 && dtype != VS_BF16)) return 0;
   const GemmPlan p = plan_gemm(dtype, M, N, K, 0, true, 0);
   size_t b = p.g.splits > 1 ? (size_t)p.g.splits * (size_t)(M * N) * 4 : 0;
-  if (dtype == VS_BF16) {  // the dW kernel's partial tiles + bias sums (if this shape is a dW product)
+  if (dtype == VS_BF16) {  // the dW kernels' partial tiles + bias sums (if this shape is a dW product)
     const size_t dw = dw_workspace_bytes(M, N, K);
     if (dw > b) b = dw;
+    const size_t dw256 = knob(VS_KNOB_NO_DW256) ? 0 : dw256_workspace_bytes(M, N, K);
+    if (dw256 > b) b = dw256;
   }
   const size_t sk = skinny_workspace_bytes(dtype, M, N, K);   // skinny split-K (head / Linear layer 0)
   if (sk > b) b = sk;

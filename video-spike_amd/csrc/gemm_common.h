@@ -133,35 +133,46 @@ __device__ __forceinline__ void epi_one(const EpiParams& e, int64_t m, int64_t n
   st_any(e.c, m * e.ldc + n, v, e.out_bf16);
 }
 
-// the same for 8 consecutive columns with 16-B vector accesses
+// the same for 8 consecutive columns with 16-B vector accesses, in two halves: fetch (every operand
+// load) and finish (arithmetic + stores).  CDNA4's vmcnt counts stores as well as loads and retires
+// them in order, so a load issued after a store waits for that store's round trip too: an epilogue
+// that runs several 8-column groups per thread fetches all of them before the first finish (one
+// store round trip per tile, not one per group).
+struct EpiOps8 {
+  float bias[8], pos[8], aux[8], res[8], acc[8];
+};
 template <uint32_t EF>
-__device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t n, float (&v)[8], bool skip_bias) {
+__device__ __forceinline__ void epi_eight_fetch(const EpiParams& e, int64_t m, int64_t n, EpiOps8& o, bool skip_bias) {
+  const uint32_t f = epi_flags<EF>(e) & (skip_bias ? ~(uint32_t)VS_EPI_BIAS : 0xFFFFFFFFu);
+  if (f & VS_EPI_BIAS) ld8(e.bias, n, 0, o.bias);
+  if (f & VS_EPI_POS) ld8(e.pos, (m % e.pos_rows) * e.N + n, 0, o.pos);
+  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD | VS_EPI_MUL_AUX)) ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, o.aux);
+  if (f & VS_EPI_RESIDUAL) ld8(e.residual, m * e.ldr + n, 0, o.res);
+  if (f & VS_EPI_ACCUM) ld8(e.c, m * e.ldc + n, 0, o.acc);
+}
+template <uint32_t EF>
+__device__ __forceinline__ void epi_eight_finish(const EpiParams& e, int64_t m, int64_t n, float (&v)[8], const EpiOps8& o,
+                                                 bool skip_bias) {
   const uint32_t f = epi_flags<EF>(e) & (skip_bias ? ~(uint32_t)VS_EPI_BIAS : 0xFFFFFFFFu);
   float t[8];
   if (f & VS_EPI_BIAS) {
-    ld8(e.bias, n, 0, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += t[k];
+    for (int k = 0; k < 8; ++k) v[k] += o.bias[k];
   }
   if (f & VS_EPI_POS) {
-    ld8(e.pos, (m % e.pos_rows) * e.N + n, 0, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += t[k];
+    for (int k = 0; k < 8; ++k) v[k] += o.pos[k];
   }
-  if (f & (VS_EPI_GELU_BWD | VS_EPI_RELU_BWD)) {
-    ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, t);
-    if (f & VS_EPI_GELU_BWD) {
+  if (f & VS_EPI_GELU_BWD) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= e.op_bf16 ? gelu_fast_grad(t[k]) : gelu_erf_grad(t[k]);
-    } else {
+    for (int k = 0; k < 8; ++k) v[k] *= e.op_bf16 ? gelu_fast_grad(o.aux[k]) : gelu_erf_grad(o.aux[k]);
+  } else if (f & VS_EPI_RELU_BWD) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = t[k] > 0.f ? v[k] : 0.f;
-    }
+    for (int k = 0; k < 8; ++k) v[k] = o.aux[k] > 0.f ? v[k] : 0.f;
   }
   if (f & VS_EPI_MUL_AUX) {
-    ld8(e.aux_in, m * e.ld_aux_in + n, e.op_bf16, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= t[k];
+    for (int k = 0; k < 8; ++k) v[k] *= o.aux[k];
   }
   if (f & VS_EPI_GELU) {
     if (f & VS_EPI_GELU_GRAD) {  // store gelu'(x) for the backward, x = the value it would have seen
@@ -186,16 +197,43 @@ __device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t
     for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
   }
   if (f & VS_EPI_RESIDUAL) {
-    ld8(e.residual, m * e.ldr + n, 0, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += t[k];
+    for (int k = 0; k < 8; ++k) v[k] += o.res[k];
   }
   if (f & VS_EPI_ACCUM) {
-    ld8(e.c, m * e.ldc + n, 0, t);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += t[k];
+    for (int k = 0; k < 8; ++k) v[k] += o.acc[k];
   }
   st8(e.c, m * e.ldc + n, e.out_bf16, v);
+}
+template <uint32_t EF>
+__device__ __forceinline__ void epi_eight(const EpiParams& e, int64_t m, int64_t n, float (&v)[8], bool skip_bias) {
+  EpiOps8 o;
+  epi_eight_fetch<EF>(e, m, n, o, skip_bias);
+  epi_eight_finish<EF>(e, m, n, v, o, skip_bias);
+}
+
+// 4 consecutive columns (n % 4 == 0) of one row, as a lane of the transposed (C^T) MFMA layout holds
+// them: 8-B bf16 / 16-B f32 vector accesses for every operand
+__device__ __forceinline__ void ld4(const void* p, int64_t i, int bf, float (&v)[4]) {
+  if (bf) {
+    const uint2 u = *(const uint2*)((const bf16_t*)p + i);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    const float4 a = *(const float4*)((const float*)p + i);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+}
+__device__ __forceinline__ void st4(void* p, int64_t i, int bf, const float (&v)[4]) {
+  if (bf) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *(uint2*)((bf16_t*)p + i) = u;
+  } else {
+    *(float4*)((float*)p + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
 }
 
 }  // namespace vs

@@ -36,12 +36,13 @@ TIMER_NAMES = ("attn_fwd", "attn_bwd", "gemm", "gemm_dw", "ln_fwd", "ln_bwd", "a
 PATH_NAMES = ("gemm_dw", "gemm_skinny", "gemm_slab", "gemm_big", "gemm_wres", "gemm_wslab", "gemm_panel",
               "gemm_fullk", "gemm_ring", "gemm_tile", "gemm_f32", "gemm_ln_fwd", "gemm_ln_bwd", "attn_fwd",
               "attn_bwd", "attn_f32", "patch_fused", "dw_grouped", "mlp_fwd", "mlp_bwd", "gemm_fp8", "patch_dw",
-              "conv_igemm", "conv_dw")
-PATH_COUNT = 24
+              "conv_igemm", "conv_dw", "gemm_g256", "gemm_dw256")
+PATH_COUNT = 26
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
-              "dw_splits", "dw_stages", "ln_blocks", "dh_f32", "no_patch_fused", "no_dw_group", "attn_variant", "slab_wv", "wres_wv", "wres_dbg")
-KNOB_COUNT = 32
+              "dw_splits", "dw_stages", "ln_blocks", "dh_f32", "no_patch_fused", "no_dw_group", "attn_variant", "slab_wv", "wres_wv", "wres_dbg",
+              "g256", "g256_grid", "g256_dbg", "no_dw256")
+KNOB_COUNT = 40
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
                                          ctypes.c_void_p, ctypes.c_size_t)
