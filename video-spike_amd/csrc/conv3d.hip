@@ -435,10 +435,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t n4, int C, const 
                                                        const float* __restrict__ shift,
                                                        const float4* __restrict__ res, int relu,
                                                        float4* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)((i * 4) % C);
+  // the grid stride (gridDim * 1024 floats) is a multiple of C (the host checks it), so a thread's
+  // channel offset is loop-invariant: no 64-bit modulo per element
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = (int)((i0 * 4) % C);
+  const float4 a = *(const float4*)(scale + c), b = *(const float4*)(shift + c);
+  for (int64_t i = i0; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 v = y[i];
-    const float4 a = *(const float4*)(scale + c), b = *(const float4*)(shift + c);
     v.x = fmaf(v.x, a.x, b.x); v.y = fmaf(v.y, a.y, b.y); v.z = fmaf(v.z, a.z, b.z); v.w = fmaf(v.w, a.w, b.w);
     if (res) {
       const float4 r = res[i];
@@ -516,16 +519,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const flo
 
 // pass 2: per channel the totals (f64, block order), dgamma / dbeta (+=), and the apply coefficients
 // coef[0][c] = gamma rstd, coef[1][c] = gamma rstd mean(g), coef[2][c] = gamma rstd mean(g xhat)
+// 64 channels per workgroup, the partial rows split over 4 thread groups (rows b = grp mod 4, in
+// order) and the 4 group sums added in a fixed order: one thread per channel walking all the rows was
+// a 116-us latency chain per call (r05 rocprof)
 __global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict__ part, int nblk, int C, int64_t M,
                                                        const float* __restrict__ gamma, const float* __restrict__ rstd,
                                                        float* dgamma, float* dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s += part[((int64_t)b * 2) * C + c];
-    q += part[((int64_t)b * 2 + 1) * C + c];
-  }
+  __shared__ double red[2][4][64];
+  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6, c = blockIdx.x * 64 + l;
+  double s0 = 0.0, q0 = 0.0;
+  if (c < C)
+    for (int b = grp; b < nblk; b += 4) {
+      s0 += part[((int64_t)b * 2) * C + c];
+      q0 += part[((int64_t)b * 2 + 1) * C + c];
+    }
+  red[0][grp][l] = s0;
+  red[1][grp][l] = q0;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  const double s = ((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l];
+  const double q = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
   if (dgamma) dgamma[c] += (float)q;
   if (dbeta) dbeta[c] += (float)s;
   const double a = (double)gamma[c] * (double)rstd[c];
@@ -540,8 +553,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(int64_t n4, int C, const flo
                                                     const float4* __restrict__ y, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ coef,
                                                     float4* __restrict__ dy, float4* __restrict__ dres) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)((i * 4) % C);
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;  // loop-invariant channel (as bn_apply_kernel)
+  const int c = (int)((i0 * 4) % C);
+  const float4 mu = *(const float4*)(mean + c), rs = *(const float4*)(rstd + c);
+  const float4 a = *(const float4*)(coef + c), b = *(const float4*)(coef + C + c),
+               cc = *(const float4*)(coef + 2 * C + c);
+  for (int64_t i = i0; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 gv = dout[i];
     if (relu) {
       const float4 o = out[i];
@@ -550,9 +567,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(int64_t n4, int C, const flo
     }
     if (dres) dres[i] = gv;
     const float4 yv = y[i];
-    const float4 mu = *(const float4*)(mean + c), rs = *(const float4*)(rstd + c);
-    const float4 a = *(const float4*)(coef + c), b = *(const float4*)(coef + C + c),
-                 cc = *(const float4*)(coef + 2 * C + c);
     float4 o;
     o.x = fmaf(a.x, gv.x, -b.x) - cc.x * ((yv.x - mu.x) * rs.x);
     o.y = fmaf(a.y, gv.y, -b.y) - cc.y * ((yv.y - mu.y) * rs.y);
@@ -841,6 +855,22 @@ extern "C" int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t
   return VS_OK;
 }
 
+namespace vs {
+static int64_t bn_bwd_blocks(int64_t M) {
+  const int64_t b = (M + 1023) / 1024;
+  return b < 512 ? (b > 0 ? b : 1) : 512;
+}
+// grid of the elementwise BN passes: <= 4096 workgroups, and a stride (blocks x 1024 floats) that is
+// a multiple of C so each thread's channel offset is fixed (C <= 1024 divides 1024, or 1 round)
+static int64_t bn_ew_blocks(int64_t n4, int64_t C) {
+  const int64_t need = (n4 + 255) / 256;
+  if (need <= 4096) return need;
+  int64_t b = 4096;
+  while (b > 1 && (b * 1024) % C != 0) --b;
+  return b;
+}
+}  // namespace vs
+
 extern "C" int vs_bn3d_apply(int64_t M, int64_t C, const float* y, const float* scale, const float* shift,
                              const float* residual, int32_t relu, float* out, void* stream) {
   VS_REQUIRE(y && scale && shift && out, "vs_bn3d_apply: null pointer");
@@ -851,19 +881,13 @@ extern "C" int vs_bn3d_apply(int64_t M, int64_t C, const float* y, const float* 
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_BN, s, (double)M * C * (residual ? 12.0 : 8.0));
   const int64_t n4 = M * C / 4;
-  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  const int64_t blocks = bn_ew_blocks(n4, C);
   hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, s, n4, (int)C, (const float4*)y, scale,
                      shift, (const float4*)residual, relu, (float4*)out);
   VS_LAUNCH_CHECK();
   return VS_OK;
 }
 
-namespace vs {
-static int64_t bn_bwd_blocks(int64_t M) {
-  const int64_t b = (M + 1023) / 1024;
-  return b < 2048 ? (b > 0 ? b : 1) : 2048;
-}
-}  // namespace vs
 
 extern "C" size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C) {
   return (size_t)bn_bwd_blocks(M) * 2 * C * 8 + (size_t)3 * C * 4 + 256;
@@ -886,11 +910,11 @@ extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float*
   hipLaunchKernelGGL(bn_bwd_reduce, dim3((unsigned)nblk), dim3(256), 0, s, M, (int)C, dout, out, relu, y, mean, rstd,
                      rpb, part);
   VS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const double*)part,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, s, (const double*)part,
                      (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef);
   VS_LAUNCH_CHECK();
   const int64_t n4 = M * C / 4;
-  const int64_t blocks = (n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096;
+  const int64_t blocks = bn_ew_blocks(n4, C);
   hipLaunchKernelGGL(bn_bwd_apply, dim3((unsigned)blocks), dim3(256), 0, s, n4, (int)C, (const float4*)dout,
                      (const float4*)out, relu, (const float4*)y, mean, rstd, (const float*)coef, (float4*)dy,
                      (float4*)dres);

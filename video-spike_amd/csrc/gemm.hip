@@ -1650,7 +1650,8 @@ __device__ __forceinline__ const char* sgpr_ptr(const char* p) {
 
 struct G256Map {
   int tiles_n, tiles, per_xcd, nk;  // nk = K / 64 stages per tile
-  int dbg;  // VS_DEBUG_KNOBS builds: VS_KNOB_G256_DBG
+  int dbg;      // VS_DEBUG_KNOBS builds: VS_KNOB_G256_DBG
+  int stagger;  // odd-slot workgroups start this many s_sleep(127) (~4 us each) late (VS_KNOB_G256_STAGGER)
 };
 
 template <bool BKC, uint32_t EF>
@@ -1679,6 +1680,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     m0 = (L / g.tiles_n) * 256;
     n0 = (L % g.tiles_n) * 256;
   };
+  // Staggered start: every CU runs the same tile schedule, so without it all 256 store their epilogue
+  // at the same moment and then all stream operands at once; half of them starting late interleaves
+  // the two phases across the chip.
+  if (slot & 1)
+    for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // ---- DMA: stage s -> slot s & 1; wave w fills rows 32w .. 32w+31 of the A image (4 pieces of
   // 8 rows x 128 B) and the same of B (or k rows 8w .. 8w+7 of an N-contiguous B: 4 pieces of
@@ -2845,6 +2851,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
 #else
     g.dbg = 0;
 #endif
+    g.stagger = knob(VS_KNOB_G256_STAGGER);
     count_path(VS_PATH_GEMM_G256);
     launch_bf16_g256(d, g, (unsigned)grid, e, s);
     VS_LAUNCH_CHECK();
