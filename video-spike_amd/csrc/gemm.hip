@@ -1640,6 +1640,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_big_kernel(const bf16_t* __r
 // conflict-free ds_read_b128 over each 16-lane group); B K-contiguous likewise, or N-contiguous
 // [64 k][256 n] (512-B rows, chunk ^= swz_mc(k): conflict-free ds_read_tr16_b64 pairs).
 // ----------------------------------------------------------------------------------------------
+// chunk key of the 256 x 256 kernel's K-contiguous B image: bits 1, 3, 4 of the row
+__device__ __forceinline__ int g256_swzb(int r) { return ((r >> 1) & 1) | ((r >> 2) & 6); }
 // a wave-uniform pointer pinned to SGPRs (the saddr operand of the asm DMA)
 __device__ __forceinline__ const char* sgpr_ptr(const char* p) {
   const uint64_t v = (uint64_t)p;
@@ -1694,8 +1696,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   for (int p = 0; p < 4; ++p) {
     const int r = wid * 32 + p * 8 + (lane >> 3);
     a_off[p] = (uint32_t)(r * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4));
-    if constexpr (BKC) {
-      b_off[p] = (uint32_t)(r * ldb * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4));
+    if constexpr (BKC) {  // B image chunk key g256_swzb(r) (fragment rows are permuted, see below)
+      b_off[p] = (uint32_t)(r * ldb * 2 + ((((lane & 7) ^ g256_swzb(r))) << 4));
     } else {
       const int k = wid * 8 + 2 * p + (lane >> 5);
       b_off[p] = (uint32_t)(k * ldb * 2 + ((((lane & 31) ^ swz_mc<128>(k))) << 4));
@@ -1726,18 +1728,27 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   };
 
   // ---- fragments (per lane, stage-invariant byte offsets; kk = 32-deep half of the stage)
+  // K-contiguous B (the forward products, bf16 out): fragment j = 2p + e, row r holds output column
+  // wc*64 + 32p + 8(r >> 2) + 4e + (r & 3), so the accumulator quads of fragments 2p and 2p+1 in one
+  // lane are 8 CONSECUTIVE columns (8fc .. 8fc+7 of the 32-column half p) and the epilogue moves 16-B
+  // bf16 vectors.  The image's chunk key g256_swzb(n) reads bits 1, 3, 4 of n -- unchanged by 4e and
+  // 32p, so every fragment is the lane address + an immediate -- and keeps the ds_read_b128 groups
+  // conflict-free (checked by enumeration).  N-contiguous B keeps 4-column quads (f32 outputs are 16-B
+  // vectors already; the transposed reads of a permuted quad would conflict 2-way).
   const int fr = lane & 15, fc = lane >> 4;
   int a_rd[2], b_rd[4][2];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) a_rd[kk] = (wr * 128 + fr) * 128 + (((kk * 4 + fc) ^ ((fr >> 1) & 7)) << 4);
   if constexpr (BKC) {
+    // image row n = R0 + 32p + 4e, R0 = wc*64 + 8(fr >> 2) + (fr & 3): key(n) = key(R0)
+    const int R0 = wc * 64 + 8 * (fr >> 2) + (fr & 3);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) b_rd[kk][0] = AB + (wc * 64 + fr) * 128 + (((kk * 4 + fc) ^ ((fr >> 1) & 7)) << 4);
+    for (int kk = 0; kk < 2; ++kk) b_rd[kk][0] = AB + R0 * 128 + (((kk * 4 + fc) ^ g256_swzb(R0)) << 4);
   } else {  // k rows kr0 / kr1 of a 32-deep half (swz_mc has period 16 in k: the second half is + 16 KB)
-    const int q = fr >> 2, p4 = (lane & 3) * 4, kr0 = 8 * fc + q, kr1 = kr0 + 4;
+    const int q = fr >> 2, kr0 = 8 * fc + q, kr1 = kr0 + 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = wc * 64 + j * 16 + p4;
+      const int col = wc * 64 + j * 16 + (lane & 3) * 4;
       b_rd[j][0] = AB + kr0 * 512 + (((col >> 3) ^ swz_mc<128>(kr0)) << 4) + (col & 7) * 2;
       b_rd[j][1] = AB + kr1 * 512 + (((col >> 3) ^ swz_mc<128>(kr1)) << 4) + (col & 7) * 2;
     }
@@ -1750,7 +1761,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if constexpr (BKC) {
-        bf[j] = *(const bf16x8*)(st + b_rd[kk][0] + j * 16 * 128);
+        bf[j] = *(const bf16x8*)(st + b_rd[kk][0] + (32 * (j >> 1) + 4 * (j & 1)) * 128);
       } else {
         short4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st + b_rd[j][0] + kk * 16384));
         short4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VS_LDS short4v*)(st + b_rd[j][1] + kk * 16384));
@@ -1767,36 +1778,47 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Epilogue straight from the accumulators (C^T layout: lane (fr, fc) holds row m0+...+fr, the 4
-  // columns n0+...+4fc..+3 of each 16 x 16 block).  CDNA4's vmcnt counts stores as well as loads
-  // and retires them in order, so a "load operand -> use -> store" sequence per block would wait
-  // for every earlier store; every operand a group of rows needs is loaded before its first store:
-  // the bias once per tile, the residual / GELU' factor per 32 rows of the wave.
+  // Epilogue straight from the accumulators (C^T layout: lane (fr, fc) holds row m0+...+fr and W = 8
+  // consecutive columns per 32-column half v (K-contiguous B: acc[i][2v] | acc[i][2v+1], columns 8fc ..)
+  // or W = 4 per 16-column block v (acc[i][v], columns 4fc ..)).  CDNA4's vmcnt counts stores as well
+  // as loads and retires them in order, so a "load operand -> use -> store" sequence per vector would
+  // wait for every earlier store; every operand a group of rows needs is loaded before its first
+  // store: the bias once per tile, the residual / GELU' factor per 32 rows of the wave.
   auto epilogue = [&](int k) __attribute__((always_inline)) {
     int m0, n0;
     tile_of(k, m0, n0);
     constexpr uint32_t F = EF;
     constexpr bool BIAS = (F & VS_EPI_BIAS) != 0, RES = (F & VS_EPI_RESIDUAL) != 0;
     constexpr bool AUXIN = (F & (VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) != 0, GELU = (F & VS_EPI_GELU) != 0;
-    const int ncol = n0 + wc * 64 + 4 * fc;
-    float bias[4][4];
+    constexpr int W = BKC ? 8 : 4, NV = 16 / W;  // columns per vector, vectors per row fragment
+    constexpr int VS = BKC ? 32 : 16;            // column step between a lane's vectors
+    const int ncol = n0 + wc * 64 + W * fc;
+    auto ldv = [&](const void* p, int64_t i, int bf, float (&v)[W]) __attribute__((always_inline)) {
+      if constexpr (W == 8) ld8(p, i, bf, v);
+      else ld4(p, i, bf, v);
+    };
+    auto stv = [&](void* p, int64_t i, int bf, const float (&v)[W]) __attribute__((always_inline)) {
+      if constexpr (W == 8) st8(p, i, bf, v);
+      else st4(p, i, bf, v);
+    };
+    float bias[NV][W];
     if constexpr (BIAS) {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) ld4(e.bias, ncol + jj * 16, 0, bias[jj]);
+      for (int vv = 0; vv < NV; ++vv) ldv(e.bias, ncol + VS * vv, 0, bias[vv]);
     }
     constexpr int GR = 2;  // row fragments per operand group (32 VGPRs of f32 operands)
 #pragma unroll
     for (int h = 0; h < 8 / GR; ++h) {
-      float opnd[GR][4][4];
+      float opnd[GR][NV][W];
       if constexpr (RES || AUXIN) {
 #pragma unroll
         for (int ii = 0; ii < GR; ++ii) {
           const int64_t m = m0 + wr * 128 + (GR * h + ii) * 16 + fr;
           const int64_t mc = m < e.M ? m : e.M - 1;     // rows past M: any valid row (not stored)
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            if constexpr (RES) ld4(e.residual, mc * e.ldr + ncol + jj * 16, 0, opnd[ii][jj]);
-            else ld4(e.aux_in, mc * e.ld_aux_in + ncol + jj * 16, e.op_bf16, opnd[ii][jj]);
+          for (int vv = 0; vv < NV; ++vv) {
+            if constexpr (RES) ldv(e.residual, mc * e.ldr + ncol + VS * vv, 0, opnd[ii][vv]);
+            else ldv(e.aux_in, mc * e.ld_aux_in + ncol + VS * vv, e.op_bf16, opnd[ii][vv]);
           }
         }
       }
@@ -1806,25 +1828,25 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
         const int64_t m = m0 + wr * 128 + i * 16 + fr;
         const bool live = m < e.M;
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          float v[4], t[4];
+        for (int vv = 0; vv < NV; ++vv) {
+          float v[W], t[W];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = acc[i][jj][r] * e.alpha;
-            if constexpr (BIAS) v[r] += bias[jj][r];
+          for (int r = 0; r < W; ++r) {
+            v[r] = acc[i][(W / 4) * vv + (r >> 2)][r & 3] * e.alpha;
+            if constexpr (BIAS) v[r] += bias[vv][r];
           }
           if constexpr ((F & VS_EPI_GELU_BWD) != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] *= gelu_fast_grad(opnd[ii][jj][r]);
+            for (int r = 0; r < W; ++r) v[r] *= gelu_fast_grad(opnd[ii][vv][r]);
           }
           if constexpr ((F & VS_EPI_MUL_AUX) != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] *= opnd[ii][jj][r];
+            for (int r = 0; r < W; ++r) v[r] *= opnd[ii][vv][r];
           }
-          const int64_t n = ncol + jj * 16;
+          const int64_t n = ncol + VS * vv;
           if constexpr (GELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < W; ++r) {
               const float x = bf2f(f2bf(v[r]));
               if constexpr ((F & VS_EPI_GELU_GRAD) != 0) v[r] = gelu_fast_both(x, t[r]);
               else {
@@ -1832,14 +1854,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
                 v[r] = gelu_fast(x);
               }
             }
-            if (live && !(dbg & 2)) st4(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, t);
+            if (live && !(dbg & 2)) stv(e.aux_out, m * e.ld_aux_out + n, e.op_bf16, t);
           }
           if constexpr (RES) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += opnd[ii][jj][r];
+            for (int r = 0; r < W; ++r) v[r] += opnd[ii][vv][r];
           }
-          if (live && !(dbg & 2)) st4(e.c, m * e.ldc + n, e.out_bf16, v);
-          acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (live && !(dbg & 2)) stv(e.c, m * e.ldc + n, e.out_bf16, v);
+#pragma unroll
+          for (int q = 0; q < W / 4; ++q) acc[i][(W / 4) * vv + q] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
