@@ -328,12 +328,23 @@ def _pmc_lookup(kind):
             "attn_bwd": ("attn_bwd_bf16_pp_kernel<2, true, true>", "attn_bwd_bf16_kernel")}.get(kind)
     if kern is None:
         return None
+    clock = None   # effective clock under the kernel (scripts/attn_clock.py: GRBM cycles / duration)
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_attn_clock.json")))):
+        try:
+            for name, e in json.load(open(f))["kernels"].items():
+                if any(k in name for k in kern):
+                    clock = {"clock_ghz": e["clock_ghz"], "clock_source": os.path.relpath(f, ROOT)}
+                    break
+        except (KeyError, ValueError, OSError):
+            continue
+        if clock:
+            break
     for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_attn.json")))):
         try:
             d = json.load(open(f))
             for name, e in d["kernels"].items():
                 if name.endswith(kern) and "mfma_busy_frac" in e:
-                    return {"mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
+                    return {**(clock or {}), "mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
                             "note": "executed MFMA cycles (the backward's dQ pass recomputes S and dP: 7 products "
                                     "executed for the 5 credited)" if kind == "attn_bwd" else "executed MFMA cycles "
                                     "(incl. the row-sum MFMAs)"}

@@ -10,6 +10,6 @@ out=gpurun_out/pmc_traffic
 mkdir -p $out
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c -d $out -o $c --output-format csv -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile-steps 0 > $out/$c.log 2>&1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile-steps 0 --no-c3 --no-c4 > $out/$c.log 2>&1
 done
 python3 scripts/traffic_summary.py $out gpurun_out/${tag}_traffic.json 4
