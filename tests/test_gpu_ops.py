@@ -284,17 +284,29 @@ def test_gemm_w_resident_path(knobs, bkc, shape, epi, wv):
         assert (pre.float() - pre2.float()).abs().max() <= 1e-2 * pre2.float().abs().max()
 
 
+@pytest.mark.parametrize("kernel", ["big", "g256"])
 @pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape,epi", [((25088, 3072, 768), "gelu"), ((25088, 768, 3072), "bias_res"),
                                        ((4100, 512, 512), "bias"), ((8192, 2304, 768), "none"),
-                                       ((6000, 768, 1536), "gelu_bwd")])
-def test_gemm_big_tile_path(bkc, shape, epi):
-    """K >= 512, N >= 512 bf16 products (ViT-Base's D = 768 / F = 3072 block) run on the 256 x 128
-    8-wave big-tile kernel: every epilogue the block uses, both W layouts, ragged M (M % 256 != 0).
-    Reference fp64 on the same bf16 inputs: f32 outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (GELU'
-    1.5e-2, against a bf16 pre-activation)."""
+                                       ((6000, 768, 1536), "gelu_bwd"),
+                                       # ragged long-M tiles (M % 256 != 0) for the 256 x 256 kernel
+                                       ((17000, 3072, 768), "gelu"), ((16500, 768, 3072), "bias_res"),
+                                       ((20000, 2304, 768), "bias"), ((18000, 768, 2304), "none"),
+                                       ((17777, 3072, 768), "gelu_bwd"), ((16411, 512, 256), "gelu_grad")])
+def test_gemm_big_tile_path(bkc, shape, epi, kernel, knobs):
+    """K >= 512, N >= 512 bf16 products (ViT-Base's D = 768 / F = 3072 block) on the 256 x 128 8-wave
+    big-tile kernel and (M >= 16,384, N % 256 == 0) on the 256 x 256 persistent one, each forced by knob
+    g256: every epilogue the block uses, both W layouts, ragged M (M % 256 != 0; the 256 x 256 kernel's
+    last tile clamps its row DMA and masks its stores).  Reference fp64 on the same bf16 inputs: f32
+    outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (GELU' 1.5e-2, against a bf16 pre-activation)."""
     from vspike import ops, _lib as L
     M, N, K = shape
+    if kernel == "g256" and (M < 16384 or N % 256 or K % 64 or K < 256):
+        pytest.skip("the 256 x 256 kernel takes M >= 16,384, N % 256 == 0, K % 64 == 0")
+    if kernel == "big" and (K < 512 or N % 128):
+        pytest.skip("the big-tile kernel takes K >= 512, N % 128 == 0")
+    knobs("g256", 1 if kernel == "g256" else 2)
+    L.dispatch_reset()
     x = _rand(M, K, seed=51).to(torch.bfloat16).to(DEV)
     w = _rand(N, K, seed=52, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
     bias = _rand(N, seed=53).to(DEV)
@@ -322,6 +334,17 @@ def test_gemm_big_tile_path(bkc, shape, epi):
         torch.cuda.synchronize()
         assert rel(pre.float(), ref) < 8e-3
         ref, tol = torch.nn.functional.gelu(ref), 8e-3
+    elif epi == "gelu_grad":      # gelu(pre) out, gelu'(pre) into aux (bf16 forward)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        gp = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(x, b_dev, out, epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_GRAD, bias=bias, aux_out=gp,
+                 ld_aux_out=N, **kw)
+        pre = ref + bias.double()
+        torch.cuda.synchronize()
+        xp = pre.to(torch.bfloat16).double().requires_grad_()
+        gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
+        assert rel(gp.float(), gg) < 1.5e-2
+        ref, tol = torch.nn.functional.gelu(pre), 8e-3
     else:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         pre = _rand(M, N, seed=55).to(torch.bfloat16).to(DEV)
@@ -330,6 +353,7 @@ def test_gemm_big_tile_path(bkc, shape, epi):
         gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
         ref, tol = ref * gg, 1.5e-2
     torch.cuda.synchronize()
+    assert L.dispatch_counts()["gemm_" + kernel] == 1, L.dispatch_counts()
     assert rel(out.float(), ref) < tol
 
 
