@@ -819,8 +819,10 @@ def main():
         parity = full_batch_parity(ccfg, init_params, pixels.cpu(), target.cpu(), gpu_par, args)
 
     c3 = None
+    # the C3 / C4 sub-records are single-GPU evidence (N = 1 only): at N > 1 a rank that failed inside one
+    # while the others sit in its collectives would hang the multi-GPU run the driver times
     want_c3 = (not args.no_c3 and args.model == "vmae_tiny" and args.dtype == "bf16" and not args.graph and
-               not args.freeze and args.loss == "poisson")
+               not args.freeze and args.loss == "poisson" and world == 1)
     if want_c3:
         del run, model, pixels, target
         import gc
@@ -834,7 +836,7 @@ def main():
 
     c4 = None
     if not args.no_c4 and args.model == "vmae_tiny" and args.dtype == "bf16" and not args.graph and not args.freeze \
-            and args.loss == "poisson":
+            and args.loss == "poisson" and world == 1:
         import gc
         gc.collect()
         torch.cuda.empty_cache()
