@@ -1656,10 +1656,11 @@ struct G256Map {
   int stagger;  // odd-slot workgroups start this many s_sleep(127) (~4 us each) late (VS_KNOB_G256_STAGGER)
 };
 
-template <bool BKC, uint32_t EF>
+template <bool BKC, bool P8, uint32_t EF>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                                 const bf16_t* __restrict__ B, int64_t ldb,
                                                                 G256Map g, EpiParams e) {
+  static_assert(!BKC || P8, "K-contiguous B fragments are always column-permuted (8-column vectors)");
   constexpr int AB = 256 * 64 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
@@ -1733,8 +1734,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   // lane are 8 CONSECUTIVE columns (8fc .. 8fc+7 of the 32-column half p) and the epilogue moves 16-B
   // bf16 vectors.  The image's chunk key g256_swzb(n) reads bits 1, 3, 4 of n -- unchanged by 4e and
   // 32p, so every fragment is the lane address + an immediate -- and keeps the ds_read_b128 groups
-  // conflict-free (checked by enumeration).  N-contiguous B keeps 4-column quads (f32 outputs are 16-B
-  // vectors already; the transposed reads of a permuted quad would conflict 2-way).
+  // conflict-free (checked by enumeration).  N-contiguous B (read transposed, ds_read_tr16_b64) takes
+  // the same permutation when the output is bf16 (P8: its quads then conflict 2-way) and keeps plain
+  // 4-column quads for f32 outputs (16-B vectors already).
   const int fr = lane & 15, fc = lane >> 4;
   int a_rd[2], b_rd[4][2];
 #pragma unroll
@@ -1748,7 +1750,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     const int q = fr >> 2, kr0 = 8 * fc + q, kr1 = kr0 + 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = wc * 64 + j * 16 + (lane & 3) * 4;
+      const int col = P8 ? wc * 64 + 32 * (j >> 1) + 8 * (lane & 3) + 4 * (j & 1) : wc * 64 + j * 16 + (lane & 3) * 4;
       b_rd[j][0] = AB + kr0 * 512 + (((col >> 3) ^ swz_mc<128>(kr0)) << 4) + (col & 7) * 2;
       b_rd[j][1] = AB + kr1 * 512 + (((col >> 3) ^ swz_mc<128>(kr1)) << 4) + (col & 7) * 2;
     }
@@ -1790,8 +1792,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     constexpr uint32_t F = EF;
     constexpr bool BIAS = (F & VS_EPI_BIAS) != 0, RES = (F & VS_EPI_RESIDUAL) != 0;
     constexpr bool AUXIN = (F & (VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) != 0, GELU = (F & VS_EPI_GELU) != 0;
-    constexpr int W = BKC ? 8 : 4, NV = 16 / W;  // columns per vector, vectors per row fragment
-    constexpr int VS = BKC ? 32 : 16;            // column step between a lane's vectors
+    constexpr int W = P8 ? 8 : 4, NV = 16 / W;  // columns per vector, vectors per row fragment
+    constexpr int VS = P8 ? 32 : 16;            // column step between a lane's vectors
     const int ncol = n0 + wc * 64 + W * fc;
     auto ldv = [&](const void* p, int64_t i, int bf, float (&v)[W]) __attribute__((always_inline)) {
       if constexpr (W == 8) ld8(p, i, bf, v);
@@ -2495,10 +2497,15 @@ static void launch_bf16_g256_ef(const vs_gemm_desc* d, const G256Map& g, unsigne
                                 hipStream_t s) {
   const bf16_t* a = (const bf16_t*)d->a;
   const bf16_t* b = (const bf16_t*)d->b;
+  // P8 (8-column epilogue vectors): always with K-contiguous B; with N-contiguous B only for bf16
+  // outputs (its transposed B reads conflict 2-way, which the f32 outputs' 16-B quads do not repay:
+  // dX fc2 1,603 -> 1,463 us, dX proj 310 -> 281; dX fc1 989 -> 1,011)
   if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_g256_kernel<true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+    hipLaunchKernelGGL((gemm_bf16_g256_kernel<true, true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+  else if (e.out_bf16)
+    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
   else
-    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, false, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
 }
 
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
@@ -2855,7 +2862,10 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
                        f == (VS_EPI_BIAS | VS_EPI_GELU) || f == VS_EPI_GELU_BWD ||
                        f == (VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD) || f == VS_EPI_MUL_AUX;
   const int g256k = knob(VS_KNOB_G256);
-  const bool g256_pick = g256k == 1 || (g256k == 0 && (d->N >= 2304 || d->K >= 2304) && f != VS_EPI_MUL_AUX);
+  // measured per C3 product: the 256 x 256 kernel wins where N or K >= 2304 and
+  // on the bf16-output dX products (fc2's GELU' product, proj); the 768 x 768 forward proj stays on the
+  // 256 x 128 tile
+  const bool g256_pick = g256k == 1 || (g256k == 0 && ((d->N >= 2304 || d->K >= 2304) || (!d->b_kcontig && e.out_bf16)));
   if (g256_pick && g256_ef && d->dtype == VS_BF16 && e.op_bf16 &&
       d->a_kcontig && d->M >= 16384 && d->N % 256 == 0 &&
       d->K >= 256 && d->K % 64 == 0 && d->split_k <= 1 && !d->a_rowsum && e.vec_ok && d->ldc % 4 == 0 &&
