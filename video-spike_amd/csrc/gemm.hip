@@ -1949,7 +1949,7 @@ __global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ B, int64_t ldb, Dw256Map g,
                                                             float* __restrict__ part, float* __restrict__ sums) {
   constexpr int AB = 64 * 256 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB (+ 16 KB of bias partials)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (SUMS ? 16 * 256 * 4 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, slots = gridDim.x >> 3;
   const int i_lo = xcd * g.per_xcd;
@@ -2021,42 +2021,31 @@ __global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __rest
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // bias-gradient partials: thread -> 8-column group sg = tid & 31 of the A image, k rows
-  // (tid >> 5) + 16 i whose index is = nt (mod tiles_n); the running sums live in a thread-private
-  // LDS slot (8 floats), not in registers (the k-loop holds 232 VGPRs)
-  const int sg = tid & 31, sr = tid >> 5;
-  float* bslot = (float*)(smem + 2 * STAGE) + sr * 256 + sg * 8;
-  if constexpr (SUMS) {
-    *(float4*)bslot = make_float4(0.f, 0.f, 0.f, 0.f);
-    *(float4*)(bslot + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  int bmask = 0;  // bit ii: k row sr + 16 ii belongs to this item's share (recomputed per item)
+  // bias-gradient partials: thread -> 4-column group sg = tid & 63 of the A image, k rows
+  // (tid >> 6) + 8 i whose index is = nt (mod tiles_n), 4 running sums in registers (8-column groups
+  // in registers spilled 13 VGPRs; in a thread-private LDS slot they cost a read-modify-write per
+  // stage: dW qkv 918 us with, 826 without the sums)
+  const int sg = tid & 63, sr = tid >> 6;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  int bmask = 0;  // bit ii: k row sr + 8 ii belongs to this item's share (recomputed per item)
   auto set_bmask = [&](int it) __attribute__((always_inline)) {
     const int nt = (it % g.tiles) % g.tiles_n;
     bmask = 0;
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) bmask |= ((sr + 16 * ii) % g.tiles_n == nt) << ii;
+    for (int ii = 0; ii < 8; ++ii) bmask |= ((sr + 8 * ii) % g.tiles_n == nt) << ii;
   };
   auto bias_rows = [&](const char* st) __attribute__((always_inline)) {
-    if (!bmask) return;
-    float t[8];
-    const float4 s0 = *(const float4*)bslot, s1 = *(const float4*)(bslot + 4);
-    t[0] = s0.x; t[1] = s0.y; t[2] = s0.z; t[3] = s0.w; t[4] = s1.x; t[5] = s1.y; t[6] = s1.z; t[7] = s1.w;
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int r = sr + 16 * ii;
+    for (int ii = 0; ii < 8; ++ii) {
+      const int r = sr + 8 * ii;
       if ((bmask >> ii) & 1) {
-        const uint4 u = *(const uint4*)(st + r * 512 + ((sg ^ swz_mc<128>(r)) << 4));
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          t[2 * c] += __uint_as_float(w[c] << 16);
-          t[2 * c + 1] += __uint_as_float(w[c] & 0xffff0000u);
-        }
+        const uint2 u = *(const uint2*)(st + r * 512 + (((sg >> 1) ^ swz_mc<128>(r)) << 4) + (sg & 1) * 8);
+        bsum[0] += __uint_as_float(u.x << 16);
+        bsum[1] += __uint_as_float(u.x & 0xffff0000u);
+        bsum[2] += __uint_as_float(u.y << 16);
+        bsum[3] += __uint_as_float(u.y & 0xffff0000u);
       }
     }
-    *(float4*)bslot = make_float4(t[0], t[1], t[2], t[3]);
-    *(float4*)(bslot + 4) = make_float4(t[4], t[5], t[6], t[7]);
   };
   auto epilogue = [&](int item) __attribute__((always_inline)) {
     float* pt = part + (int64_t)item * 65536;
@@ -2068,12 +2057,10 @@ __global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __rest
         st4(pt, (wr * 128 + i * 16 + fr) * 256 + wc * 64 + jj * 16 + 4 * fc, 0, v);
         acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    if constexpr (SUMS) {  // the thread's own slot: no barrier needed
-      float* ps = sums + ((int64_t)item * 16 + sr) * 256 + sg * 8;
-      *(float4*)ps = *(const float4*)bslot;
-      *(float4*)(ps + 4) = *(const float4*)(bslot + 4);
-      *(float4*)bslot = make_float4(0.f, 0.f, 0.f, 0.f);
-      *(float4*)(bslot + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (SUMS) {
+      *(float4*)(sums + ((int64_t)item * 8 + sr) * 256 + sg * 4) = make_float4(bsum[0], bsum[1], bsum[2], bsum[3]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) bsum[c] = 0.f;
     }
   };
   auto mfma16 = [&](const bf16x8 (&bc)[4], const bf16x8 (&af)[4], int rh) __attribute__((always_inline)) {
@@ -2143,7 +2130,7 @@ __global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __rest
 }
 
 // C[m][n] += sum over splits (in order) of the items' partial tiles; bias[m] += the bias partials
-// (splits, then the tile row's N-column items, then the 16 partial rows, in order).  One thread per
+// (splits, then the tile row's N-column items, then the 8 partial rows, in order).  One thread per
 // output float4, then one per bias element.
 __global__ __launch_bounds__(256) void gemm_dw256_reduce(const float* __restrict__ part, const float* __restrict__ sums,
                                                          Dw256Map g, int splits, int64_t M, int64_t N,
@@ -2168,9 +2155,9 @@ __global__ __launch_bounds__(256) void gemm_dw256_reduce(const float* __restrict
     float a = 0.f;
     for (int sp = 0; sp < splits; ++sp)
       for (int nt = 0; nt < g.tiles_n; ++nt) {
-        const float* p = sums + ((int64_t)(sp * g.tiles + mt * g.tiles_n + nt) * 16) * 256 + ml;
+        const float* p = sums + ((int64_t)(sp * g.tiles + mt * g.tiles_n + nt) * 8) * 256 + ml;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a += p[r * 256];
+        for (int r = 0; r < 8; ++r) a += p[r * 256];
       }
     bias[m] += a;
   }
@@ -2212,7 +2199,7 @@ static Dw256Plan plan_dw256(int64_t M, int64_t N, int64_t K) {
 }
 static size_t dw256_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   const Dw256Plan p = plan_dw256(M, N, K);
-  return p.valid ? (size_t)p.g.items * (65536 + 16 * 256) * 4 : 0;
+  return p.valid ? (size_t)p.g.items * (65536 + 8 * 256) * 4 : 0;
 }
 
 // ----------------------------------------------------------------------------------------------
