@@ -624,6 +624,7 @@ int vs_dispatch_reset(void);
 #define VS_KNOB_G256_DBG    30   /* VS_DEBUG_KNOBS builds only: 256 x 256 GEMM bit 0 = no operand DMA, bit 1 = no epilogue stores (WRONG results) */
 #define VS_KNOB_NO_DW256    31   /* 1: the long-K dW products on the split-K dW kernel instead of the 256 x 256 persistent one */
 #define VS_KNOB_G256_STAGGER 32  /* 256 x 256 GEMM: odd-slot workgroups start N x s_sleep(127) (~4 us) late */
+#define VS_KNOB_CONV_DW128  33   /* 1: Conv3d weight gradient on 128-wide k tiles where K >= 128 (measured slower than the 64-wide default) */
 #define VS_KNOB_COUNT       40
 int vs_knob_get(int knob);               /* VS_EINVAL for an unknown id */
 int vs_knob_set(int knob, int value);    /* returns the previous value; VS_EINVAL for an unknown id */

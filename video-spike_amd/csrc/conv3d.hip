@@ -237,12 +237,18 @@ struct ConvDw {
   int Kp;
 };
 
+// BKK = 64 or 128 k columns per tile: the wider tile reads the dy slab (the tile's A operand) half as
+// often (the dy of one voxel row slab is re-read by every k tile of the product) but measured slower:
+// 64 is the default (VS_KNOB_CONV_DW128)
+template <int BKK>
 __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
-  constexpr int BO = 64, BKK = 64, BM = 32, LD = 80;
-  constexpr int SO = BM * LD, STAGE = 2 * SO;
+  constexpr int BO = 64, BM = 32, LDO = 80, LD = BKK + 16;   // row strides % 32 == 16: conflict-free b32 reads
+  constexpr int SO = BM * LDO, STAGE = SO + BM * LD;
+  constexpr int KCH = BKK / 4, XR = 256 / KCH, XS = BM / XR;  // x gather: float4 chunks per row, rows per pass, passes
+  constexpr int NJ = BKK / 32;                                // 16-column fragments per wave (2 waves along k)
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
-  const int tiles_o = g.Co / BO, tiles_k = g.Kp / BKK;
+  const int tiles_o = g.Co / BO, tiles_k = g.Kp / BKK;  // Kp: K rounded up to BKK
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / (tiles_o * tiles_k), rem = bid % (tiles_o * tiles_k);
   const int ot = rem / tiles_k, kt = rem % tiles_k;
@@ -251,9 +257,10 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
   int64_t me = mb + (int64_t)g.steps_per_split * BM;
   if (me > g.M) me = g.M;
   const int nsteps = me > mb ? (int)((me - mb + BM - 1) / BM) : 0;
-  const int chunk = tid & 15;  // float4 index along o (dy) / k (gather)
+  const int chunk = tid & 15;  // float4 index along o (dy)
+  const int xchunk = tid % KCH;  // float4 index along k (gather)
   // the gather's k chunk: tap and channel are fixed for the whole launch of this thread
-  const int k = k0 + chunk * 4;
+  const int k = k0 + xchunk * 4;
   const bool kok = k < g.K;
   const int tap = k >> g.cshift, c = k & (g.C - 1);
   const int khw = g.kh * g.kw;
@@ -261,13 +268,19 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
   const int oz = td - g.pd, oy = th - g.ph, ox = tw - g.pw;
   const float ihw = 1.0f / (float)g.Wo, ihh = 1.0f / (float)g.Ho, ihd = 1.0f / (float)g.Do;
 
-  auto load = [&](float4 (&rd)[2], float4 (&rx)[2], int step) {
+  auto load = [&](float4 (&rd)[2], float4 (&rx)[XS], int step) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int64_t m = mb + (int64_t)step * BM + (tid >> 4) + 16 * s;
       const bool ok = m < me;
       const int mm = ok ? (int)m : 0;
       rd[s] = ok ? *(const float4*)(g.dy + (int64_t)mm * g.Co + o0 + chunk * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      const int64_t m = mb + (int64_t)step * BM + tid / KCH + XR * s;
+      const bool ok = m < me;
+      const int mm = ok ? (int)m : 0;
       const int q1 = divq(mm, g.Wo, ihw), gw = mm - q1 * g.Wo;
       const int q2 = divq(q1, g.Ho, ihh), gh = q1 - q2 * g.Ho;
       const int n = divq(q2, g.Do, ihd), gd = q2 - n * g.Do;
@@ -278,24 +291,22 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
       rx[s] = in ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&](float* st, const float4 (&rd)[2], const float4 (&rx)[2]) {
+  auto store = [&](float* st, const float4 (&rd)[2], const float4 (&rx)[XS]) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int row = (tid >> 4) + 16 * s;
-      *(float4*)(st + row * LD + chunk * 4) = rd[s];
-      *(float4*)(st + SO + row * LD + chunk * 4) = rx[s];
-    }
+    for (int s = 0; s < 2; ++s) *(float4*)(st + ((tid >> 4) + 16 * s) * LDO + chunk * 4) = rd[s];
+#pragma unroll
+    for (int s = 0; s < XS; ++s) *(float4*)(st + SO + (tid / KCH + XR * s) * LD + xchunk * 4) = rx[s];
   };
 
   // blocked accumulation: the MFMA chain runs over 16 steps (512 voxels), then folds into tot —
   // one f32 chain over a whole split (up to ~40k voxels at 16 clips) lets rounding grow with its
   // length, and these sums cancel strongly (the gradient of a conv feeding a BatchNorm)
-  f32x4 acc[2][2], tot[2][2];
+  f32x4 acc[2][NJ], tot[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 rd[2], rx[2];
+    for (int j = 0; j < NJ; ++j) acc[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 rd[2], rx[XS];
   if (nsteps > 0) {
     load(rd, rx, 0);
     store(smem, rd, rx);
@@ -309,22 +320,22 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
 #pragma unroll
     for (int sub = 0; sub < BM / 4; ++sub) {
       const int mrow = 4 * sub + (lane >> 4);
-      float af[2], bfr[2];
+      float af[2], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = sd_[mrow * LD + wr * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 2; ++i) af[i] = sd_[mrow * LDO + wr * 32 + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = sx[mrow * LD + wc * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < NJ; ++j) bfr[j] = sx[mrow * LD + wc * (BKK / 2) + j * 16 + (lane & 15)];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) store(smem + ((t + 1) & 1) * STAGE, rd, rx);
     if ((t & 15) == 15) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           tot[i][j] += acc[i][j];
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
@@ -334,17 +345,17 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] += tot[i][j];
+    for (int j = 0; j < NJ; ++j) acc[i][j] += tot[i][j];
   // partial tile (plain stores; the reduce adds the splits in order)
   float* pt = g.part + (int64_t)split * g.Co * g.Kp;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = o0 + wr * 32 + i * 16 + 4 * (lane >> 4) + r;
-        const int kk = k0 + wc * 32 + j * 16 + (lane & 15);
+        const int kk = k0 + wc * (BKK / 2) + j * 16 + (lane & 15);
         pt[(int64_t)o * g.Kp + kk] = acc[i][j][r];
       }
 }
@@ -775,14 +786,16 @@ extern "C" int vs_conv3d_dx(const vs_conv3d_desc* d, const float* dy, const floa
 
 namespace vs {
 struct DwPlanC {
-  int tiles_o, tiles_k, Kp, splits, sps;
+  int tiles_o, tiles_k, Kp, splits, sps, bkk;
 };
 static DwPlanC plan_conv_dw(const vs_conv3d_desc* d) {
   DwPlanC p;
   const int K = d->kd * d->kh * d->kw * (int)d->Ci;
+  // 128-wide k tiles halve the dy re-reads but measured slower (conv dW 40.9 vs 39.4 ms/step at C4)
+  p.bkk = K >= 128 && knob(VS_KNOB_CONV_DW128) ? 128 : 64;
   p.tiles_o = (int)(d->Co / 64);
-  p.tiles_k = (K + 63) / 64;
-  p.Kp = p.tiles_k * 64;
+  p.tiles_k = (K + p.bkk - 1) / p.bkk;
+  p.Kp = p.tiles_k * p.bkk;
   const int64_t M = d->N * d->Do * d->Ho * d->Wo;
   const int64_t steps = (M + 31) / 32;
   const int tiles = p.tiles_o * p.tiles_k;
@@ -824,7 +837,8 @@ extern "C" int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float
   g.M = M; g.splits = p.splits; g.steps_per_split = p.sps; g.part = (float*)workspace; g.Kp = p.Kp;
   count_path(VS_PATH_CONV_DW);
   const int64_t nwg = (int64_t)p.splits * p.tiles_o * p.tiles_k;
-  hipLaunchKernelGGL(conv_dw_kernel, dim3((unsigned)nwg), dim3(256), 0, s, g);
+  if (p.bkk == 128) hipLaunchKernelGGL(conv_dw_kernel<128>, dim3((unsigned)nwg), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(conv_dw_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, s, g);
   VS_LAUNCH_CHECK();
   const int64_t n = d->Co * (int64_t)g.K;
   hipLaunchKernelGGL(conv_dw_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)workspace,
