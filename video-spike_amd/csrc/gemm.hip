@@ -1780,6 +1780,29 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue geometry (see below) and the bias, which the early-DMA variants load one stage ahead
+  constexpr int EW = P8 ? 8 : 4, ENV = 16 / EW, EVS = P8 ? 32 : 16;
+  constexpr bool EBIAS = (EF & VS_EPI_BIAS) != 0;
+  // ED (early DMA): the variants whose epilogue loads nothing per row (bias at most) issue each stage's
+  // successor DMA right after the barrier that frees its slot -- before a tile's epilogue stores --
+  // and wait for it with vmcnt(<stores issued since>), so the stores drain under the next tile's first
+  // stage instead of stalling it (vmcnt retires loads, DMA and stores in order)
+  constexpr bool ED = (EF & (VS_EPI_RESIDUAL | VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) == 0;
+  float ebias[ENV][EW];
+  auto load_bias = [&](int k) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_of(k, m0, n0);
+    (void)m0;
+#pragma unroll
+    for (int vv = 0; vv < ENV; ++vv) {
+      if constexpr (EW == 8) ld8(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
+      else ld4(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
+    }
+  };
+  // epilogue store instructions per lane (vmcnt units), all issued after the early DMA
+  const int est_c = 8 * ENV * ((EW == 8 && !e.out_bf16) ? 2 : 1);
+  const int est = est_c + ((EF & VS_EPI_GELU) ? 8 * ENV : 0);
+
   // Epilogue straight from the accumulators (C^T layout: lane (fr, fc) holds row m0+...+fr and W = 8
   // consecutive columns per 32-column half v (K-contiguous B: acc[i][2v] | acc[i][2v+1], columns 8fc ..)
   // or W = 4 per 16-column block v (acc[i][v], columns 4fc ..)).  CDNA4's vmcnt counts stores as well
@@ -1792,8 +1815,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     constexpr uint32_t F = EF;
     constexpr bool BIAS = (F & VS_EPI_BIAS) != 0, RES = (F & VS_EPI_RESIDUAL) != 0;
     constexpr bool AUXIN = (F & (VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) != 0, GELU = (F & VS_EPI_GELU) != 0;
-    constexpr int W = P8 ? 8 : 4, NV = 16 / W;  // columns per vector, vectors per row fragment
-    constexpr int VS = P8 ? 32 : 16;            // column step between a lane's vectors
+    constexpr int W = EW, NV = ENV;  // columns per vector, vectors per row fragment
+    constexpr int VS = EVS;          // column step between a lane's vectors
     const int ncol = n0 + wc * 64 + W * fc;
     auto ldv = [&](const void* p, int64_t i, int bf, float (&v)[W]) __attribute__((always_inline)) {
       if constexpr (W == 8) ld8(p, i, bf, v);
@@ -1803,11 +1826,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
       if constexpr (W == 8) st8(p, i, bf, v);
       else st4(p, i, bf, v);
     };
-    float bias[NV][W];
-    if constexpr (BIAS) {
-#pragma unroll
-      for (int vv = 0; vv < NV; ++vv) ldv(e.bias, ncol + VS * vv, 0, bias[vv]);
-    }
+    if constexpr (BIAS && !ED) load_bias(k);  // ED: loaded at the start of the tile's last stage
     constexpr int GR = 2;  // row fragments per operand group (32 VGPRs of f32 operands)
 #pragma unroll
     for (int h = 0; h < 8 / GR; ++h) {
@@ -1835,7 +1854,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
 #pragma unroll
           for (int r = 0; r < W; ++r) {
             v[r] = acc[i][(W / 4) * vv + (r >> 2)][r & 3] * e.alpha;
-            if constexpr (BIAS) v[r] += bias[vv][r];
+            if constexpr (BIAS) v[r] += ebias[vv][r];
           }
           if constexpr ((F & VS_EPI_GELU_BWD) != 0) {
 #pragma unroll
@@ -1896,9 +1915,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   //   P2: A(kk1, rh1) | MFMA B1 x A(kk1, rh0)
   //   P3: vmcnt(0) + lgkmcnt(0) + barrier (stage s+1 landed everywhere; stage s's reads retired) |
   //       B(kk0), A(kk0, rh0) of stage s+1 | MFMA B1 x A(kk1, rh1) | epilogue at a tile's last stage
+  if (ED && total > 1) issue(1);
+  int nst = 0;  // ED: store instructions issued after the DMA in flight (the previous tile's epilogue)
   for (int s = 0; s < total; ++s) {
     const char* cur = smem + (s & 1) * STAGE;
-    if (s + 1 < total) issue(s + 1);
+    const bool last = (s + 1) % g.nk == 0;
+    if (!ED && s + 1 < total) issue(s + 1);
+    if (ED && EBIAS && last) load_bias(s / g.nk);
     read_a(cur, 0, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b0, a0, 0);
@@ -1909,10 +1932,24 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     read_a(cur, 1, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage s+1 landed: vmcnt(0), or (ED) all but the nst youngest ops, the stores issued after its DMA
+    if (!ED || nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (nst <= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (nst <= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (nst <= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (ED) {
+      if (EBIAS && last) {  // the compiler's wait for the bias loads lands here, before the next DMA
+#pragma unroll
+        for (int vv = 0; vv < ENV; ++vv)
+#pragma unroll
+          for (int r = 0; r < EW; ++r) asm volatile("" : "+v"(ebias[vv][r]));
+      }
+      if (s + 2 < total) issue(s + 2);  // into slot s & 1: every wave's reads of stage s retired
+    }
     if (s + 1 < total) {
       const char* nxt = smem + ((s + 1) & 1) * STAGE;
       read_b(nxt, 0, b0);
@@ -1920,7 +1957,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a1, 1);
-    if ((s + 1) % g.nk == 0) epilogue(s / g.nk);
+    nst = 0;
+    if (last) {
+      epilogue(s / g.nk);
+      if constexpr (ED) {
+        int m0, n0;
+        tile_of(s / g.nk, m0, n0);
+        (void)n0;
+        // exact count only for a full tile (a ragged one skips the stores of all-dead rows) and real stores
+        nst = (m0 + 256 <= e.M && !(dbg & 2)) ? (est < 63 ? est : 63) : 0;
+      }
+    }
   }
 }
 
