@@ -69,6 +69,7 @@ def main():
                     help="VS_KNOB_ATTN_VARIANT values, comma-separated (low nibble: forward kernel, bits 4-7: backward)")
     ap.add_argument("--attn-scale", type=float, default=3.0, help="q, k, v ~ N(0, scale^2)")
     ap.add_argument("--cold", action="store_true", help="evict L2 / Infinity Cache before every timed launch")
+    ap.add_argument("--ln-dim", type=int, default=192, help="LayerNorm width of --only ln (768: C3 / C5)")
     a = ap.parse_args()
     global COLD
     if a.cold:
@@ -232,6 +233,7 @@ def main():
         report("linear_video L0 dW (f32 stores)", timeit(lambda: ops.linear_dw(dyf, xf, dwf, db=dbf, accumulate=False),
                                                         a.reps), (Bn + Nout) * K * 4 + Bn * K * 4, 2 * Bn * Nout * K)
     if a.only in ("", "ln"):
+        D = a.ln_dim
         x = r(M, D, dt=torch.float32)
         g, b = r(D, dt=torch.float32) + 1, r(D, dt=torch.float32)
         y = torch.empty(M, D, dtype=bf, device=dev)
@@ -247,6 +249,8 @@ def main():
         report("ln bwd (bf16 dy, +dres, + bf16 copy)", timeit(lambda: ops.layernorm_bwd(dyl, x, mu, rs, g, dx, dg, dbb,
                                                                                         dres=x, dx_lp=dxl), a.reps),
                M * D * 16, 0)
+        xc = torch.empty_like(x)
+        report("copy f32 (torch, read + write)", timeit(lambda: xc.copy_(x), a.reps), M * D * 8, 0)
 
 
 if __name__ == "__main__":

@@ -485,22 +485,40 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const flo
   if (r1 > M) r1 = M;
   double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
   const float4 mu = *(const float4*)(mean + cg * 4), rs = *(const float4*)(rstd + cg * 4);
-  if (ro < rpi)
-    for (int64_t r = r0 + ro; r < r1; r += rpi) {
-      const int64_t i = r * C + cg * 4;
-      float4 gv = *(const float4*)(dout + i);
-      if (relu) {
-        const float4 o = *(const float4*)(out + i);
-        gv.x = o.x > 0.f ? gv.x : 0.f; gv.y = o.y > 0.f ? gv.y : 0.f;
-        gv.z = o.z > 0.f ? gv.z : 0.f; gv.w = o.w > 0.f ? gv.w : 0.f;
-      }
-      const float4 yv = *(const float4*)(y + i);
-      s[0] += gv.x; s[1] += gv.y; s[2] += gv.z; s[3] += gv.w;
-      q[0] += (double)gv.x * ((yv.x - mu.x) * rs.x);
-      q[1] += (double)gv.y * ((yv.y - mu.y) * rs.y);
-      q[2] += (double)gv.z * ((yv.z - mu.z) * rs.z);
-      q[3] += (double)gv.w * ((yv.w - mu.w) * rs.w);
+  // two rows per iteration, every load of both issued before the first f64 add (the adds stay in
+  // row order r, r + rpi, ...)
+  auto load = [&](int64_t r, float4& gv, float4& yv) {
+    const int64_t i = r * C + cg * 4;
+    gv = *(const float4*)(dout + i);
+    if (relu) {
+      const float4 o = *(const float4*)(out + i);
+      gv.x = o.x > 0.f ? gv.x : 0.f; gv.y = o.y > 0.f ? gv.y : 0.f;
+      gv.z = o.z > 0.f ? gv.z : 0.f; gv.w = o.w > 0.f ? gv.w : 0.f;
     }
+    yv = *(const float4*)(y + i);
+  };
+  auto acc = [&](const float4& gv, const float4& yv) {
+    s[0] += gv.x; s[1] += gv.y; s[2] += gv.z; s[3] += gv.w;
+    q[0] += (double)gv.x * ((yv.x - mu.x) * rs.x);
+    q[1] += (double)gv.y * ((yv.y - mu.y) * rs.y);
+    q[2] += (double)gv.z * ((yv.z - mu.z) * rs.z);
+    q[3] += (double)gv.w * ((yv.w - mu.w) * rs.w);
+  };
+  if (ro < rpi) {
+    int64_t r = r0 + ro;
+    for (; r + rpi < r1; r += 2 * rpi) {
+      float4 g0, y0, g1, y1;
+      load(r, g0, y0);
+      load(r + rpi, g1, y1);
+      acc(g0, y0);
+      acc(g1, y1);
+    }
+    if (r < r1) {
+      float4 g0, y0;
+      load(r, g0, y0);
+      acc(g0, y0);
+    }
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     red[0][k][t] = s[k];
@@ -530,26 +548,46 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const flo
 
 // pass 2: per channel the totals (f64, block order), dgamma / dbeta (+=), and the apply coefficients
 // coef[0][c] = gamma rstd, coef[1][c] = gamma rstd mean(g), coef[2][c] = gamma rstd mean(g xhat)
-// 64 channels per workgroup, the partial rows split over 4 thread groups (rows b = grp mod 4, in
-// order) and the 4 group sums added in a fixed order: one thread per channel walking all the rows was
+// 64 channels per workgroup, the partial rows split over 16 thread groups (rows b = grp mod 16, in
+// order) and the 16 group sums added in a fixed order: one thread per channel walking all the rows was
 // a 116-us latency chain per call (r05 rocprof)
-__global__ __launch_bounds__(256) void bn_bwd_finalize(const double* __restrict__ part, int nblk, int C, int64_t M,
-                                                       const float* __restrict__ gamma, const float* __restrict__ rstd,
-                                                       float* dgamma, float* dbeta, float* __restrict__ coef) {
-  __shared__ double red[2][4][64];
+__global__ __launch_bounds__(1024) void bn_bwd_finalize(const double* __restrict__ part, int nblk, int C, int64_t M,
+                                                        const float* __restrict__ gamma, const float* __restrict__ rstd,
+                                                        float* dgamma, float* dbeta, float* __restrict__ coef) {
+  constexpr int NG = 16;  // thread groups over the partial rows (rows b = grp mod NG, in order)
+  __shared__ double red[2][NG][64];
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6, c = blockIdx.x * 64 + l;
   double s0 = 0.0, q0 = 0.0;
-  if (c < C)
-    for (int b = grp; b < nblk; b += 4) {
+  if (c < C) {
+    int b = grp;
+    for (; b + 7 * NG < nblk; b += 8 * NG) {  // 8 rows' loads in flight, added in row order
+      double vs[8], vq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        vs[u] = part[((int64_t)(b + u * NG) * 2) * C + c];
+        vq[u] = part[((int64_t)(b + u * NG) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += vs[u];
+        q0 += vq[u];
+      }
+    }
+    for (; b < nblk; b += NG) {
       s0 += part[((int64_t)b * 2) * C + c];
       q0 += part[((int64_t)b * 2 + 1) * C + c];
     }
+  }
   red[0][grp][l] = s0;
   red[1][grp][l] = q0;
   __syncthreads();
   if (grp != 0 || c >= C) return;
-  const double s = ((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l];
-  const double q = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
+  double s = red[0][0][l], q = red[1][0][l];
+#pragma unroll
+  for (int k = 1; k < NG; ++k) {
+    s += red[0][k][l];
+    q += red[1][k][l];
+  }
   if (dgamma) dgamma[c] += (float)q;
   if (dbeta) dbeta[c] += (float)s;
   const double a = (double)gamma[c] * (double)rstd[c];
@@ -870,9 +908,12 @@ extern "C" int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t
 }
 
 namespace vs {
-static int64_t bn_bwd_blocks(int64_t M) {
-  const int64_t b = (M + 1023) / 1024;
-  return b < 512 ? (b > 0 ? b : 1) : 512;
+// ~8K elements per workgroup (<= 2,048 partial rows): the old rows-only rule (1,024 rows per block,
+// <= 512 blocks) gave the deep layers 4-196 workgroups with 128-392 serial row steps per thread
+// (bn_bwd_reduce averaged 219 us per call at C4, 3.4x its bytes at the apply pass's rate)
+static int64_t bn_bwd_blocks(int64_t M, int64_t C) {
+  const int64_t b = (M * C + 8191) / 8192;
+  return b < 2048 ? (b > 0 ? b : 1) : 2048;
 }
 // grid of the elementwise BN passes: <= 4096 workgroups, and a stride (blocks x 1024 floats) that is
 // a multiple of C so each thread's channel offset is fixed (C <= 1024 divides 1024, or 1 round)
@@ -904,7 +945,7 @@ extern "C" int vs_bn3d_apply(int64_t M, int64_t C, const float* y, const float* 
 
 
 extern "C" size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C) {
-  return (size_t)bn_bwd_blocks(M) * 2 * C * 8 + (size_t)3 * C * 4 + 256;
+  return (size_t)bn_bwd_blocks(M, C) * 2 * C * 8 + (size_t)3 * C * 4 + 256;
 }
 
 extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
@@ -917,14 +958,14 @@ extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float*
   if (M <= 0) return VS_OK;
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_BN, s, (double)M * C * (4.0 * (relu ? 3 : 2) + 4.0 + (dres ? 4.0 : 0.0)));
-  const int64_t nblk = bn_bwd_blocks(M);
+  const int64_t nblk = bn_bwd_blocks(M, C);
   const int64_t rpb = (M + nblk - 1) / nblk;
   double* part = (double*)workspace;
   float* coef = (float*)(part + nblk * 2 * C);
   hipLaunchKernelGGL(bn_bwd_reduce, dim3((unsigned)nblk), dim3(256), 0, s, M, (int)C, dout, out, relu, y, mean, rstd,
                      rpb, part);
   VS_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(256), 0, s, (const double*)part,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(1024), 0, s, (const double*)part,
                      (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef);
   VS_LAUNCH_CHECK();
   const int64_t n4 = M * C / 4;
