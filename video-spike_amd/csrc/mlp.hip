@@ -81,26 +81,80 @@ __device__ __forceinline__ float gelu_sp_both(float x, float& grad) {
 // segment k every value advances one step of the chain, so a segment carries 16 independent
 // operations instead of the 1-2 dependent chains of 9 that left the wave waiting on VALU latency
 // (stages 5-6 / 8-9 split the exp / rcp so no segment holds 16 transcendentals).
+// Packed f32: the multiply / add / fma stages as v_pk_{mul,add,fma}_f32 on value
+// pairs (8 instructions per stage instead of 16; the min and the transcendentals stay scalar; every
+// lane's arithmetic is the scalar form's, bit for bit).  Measured (scripts/mlp_bench.py, two A/B
+// pairs, profiles/r05_mlp_pk_ab.txt): the forward with the LayerNorm epilogue 241 -> 229 us, the plain
+// forward 230-233 -> 215-229; the backward's gelu_both_stage packed the same way was SLOWER (243 ->
+// 250-260 us), so it stays scalar (the packed form is kept for diagnostic builds, -DVS_MLP_PK_BWD).
 struct GeluStages {
-  float t[16], p[16];
+  f32x2 t[8], p[8];
 };
+__device__ __forceinline__ f32x2 pk_splat(float c) { return (f32x2){c, c}; }
 __device__ __forceinline__ void gelu_stage(int k, const f32x16& x, GeluStages& s, float (&g)[16]) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (k == 0) s.t[i] = x[i] * x[i];
-    if (k == 1) s.t[i] = fminf(s.t[i], 81.f);
-    if (k == 2) s.p[i] = fmaf(s.t[i], -kGk5 * kGl2e, -kGk3 * kGl2e);
-    if (k == 3) s.p[i] = fmaf(s.t[i], s.p[i], -kGk1 * kGl2e);
-    if (k == 4) s.p[i] = x[i] * s.p[i];
-    if ((k == 5 && i < 8) || (k == 6 && i >= 8)) s.p[i] = __builtin_amdgcn_exp2f(s.p[i]);
-    if (k == 7) s.p[i] = 1.f + s.p[i];
-    if ((k == 8 && i < 8) || (k == 9 && i >= 8)) s.p[i] = __builtin_amdgcn_rcpf(s.p[i]);
-    if (k == 10) g[i] = x[i] * s.p[i];
+  for (int j = 0; j < 8; ++j) {
+    const f32x2 xv = {x[2 * j], x[2 * j + 1]};
+    if (k == 0) s.t[j] = xv * xv;
+    if (k == 1) s.t[j] = (f32x2){fminf(s.t[j][0], 81.f), fminf(s.t[j][1], 81.f)};
+    if (k == 2) s.p[j] = __builtin_elementwise_fma(s.t[j], pk_splat(-kGk5 * kGl2e), pk_splat(-kGk3 * kGl2e));
+    if (k == 3) s.p[j] = __builtin_elementwise_fma(s.t[j], s.p[j], pk_splat(-kGk1 * kGl2e));
+    if (k == 4) s.p[j] = xv * s.p[j];
+    if ((k == 5 && j < 4) || (k == 6 && j >= 4))
+      s.p[j] = (f32x2){__builtin_amdgcn_exp2f(s.p[j][0]), __builtin_amdgcn_exp2f(s.p[j][1])};
+    if (k == 7) s.p[j] = s.p[j] + pk_splat(1.f);
+    if ((k == 8 && j < 4) || (k == 9 && j >= 4))
+      s.p[j] = (f32x2){__builtin_amdgcn_rcpf(s.p[j][0]), __builtin_amdgcn_rcpf(s.p[j][1])};
+    if (k == 10) {
+      const f32x2 r = xv * s.p[j];
+      g[2 * j] = r[0];
+      g[2 * j + 1] = r[1];
+    }
   }
 }
+#ifdef VS_MLP_PK_BWD
+__device__ __forceinline__ void gelu_both_stage(int k, const f32x16& x, GeluStages& s, float (&a)[16],
+                                                float (&grad)[16]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x2 xv = {x[2 * j], x[2 * j + 1]};
+    f32x2 gr = {grad[2 * j], grad[2 * j + 1]};
+    if (k == 0) s.t[j] = xv * xv;
+    if (k == 1) s.t[j] = (f32x2){fminf(s.t[j][0], 81.f), fminf(s.t[j][1], 81.f)};
+    if (k == 2) {
+      s.p[j] = __builtin_elementwise_fma(s.t[j], pk_splat(-kGk5 * kGl2e), pk_splat(-kGk3 * kGl2e));
+      gr = __builtin_elementwise_fma(s.t[j], pk_splat(5.f * kGk5), pk_splat(3.f * kGk3));
+    }
+    if (k == 3) {
+      s.p[j] = __builtin_elementwise_fma(s.t[j], s.p[j], pk_splat(-kGk1 * kGl2e));
+      gr = __builtin_elementwise_fma(s.t[j], gr, pk_splat(kGk1));
+    }
+    if (k == 4) s.p[j] = xv * s.p[j];
+    if ((k == 5 && j < 4) || (k == 6 && j >= 4))
+      s.p[j] = (f32x2){__builtin_amdgcn_exp2f(s.p[j][0]), __builtin_amdgcn_exp2f(s.p[j][1])};
+    if (k == 7) s.p[j] = s.p[j] + pk_splat(1.f);
+    if ((k == 8 && j < 4) || (k == 9 && j >= 4))
+      s.p[j] = (f32x2){__builtin_amdgcn_rcpf(s.p[j][0]), __builtin_amdgcn_rcpf(s.p[j][1])};
+    if (k == 10) {
+      const f32x2 r = xv * s.p[j];
+      a[2 * j] = r[0];
+      a[2 * j + 1] = r[1];
+      s.t[j] = __builtin_elementwise_fma(-s.p[j], s.p[j], s.p[j]);
+    }
+    if (k == 11) gr = __builtin_elementwise_fma(xv * s.t[j], gr, s.p[j]);
+    if (k == 2 || k == 3 || k == 11) {
+      grad[2 * j] = gr[0];
+      grad[2 * j + 1] = gr[1];
+    }
+  }
+}
+#else
+struct GeluStagesS {
+  float t[16], p[16];
+};
 
 // ... and gelu with its derivative (the backward), same staging: a = x s, grad = s + x s (1 - s) u'(x)
-__device__ __forceinline__ void gelu_both_stage(int k, const f32x16& x, GeluStages& s, float (&a)[16],
+__device__ __forceinline__ void gelu_both_stage(int k, const f32x16& x, GeluStagesS& s, float (&a)[16],
                                                 float (&grad)[16]) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -125,6 +179,12 @@ __device__ __forceinline__ void gelu_both_stage(int k, const f32x16& x, GeluStag
     if (k == 11) grad[i] = fmaf(x[i] * s.t[i], grad[i], s.p[i]);
   }
 }
+#endif
+#ifdef VS_MLP_PK_BWD
+using GeluStagesB = GeluStages;
+#else
+using GeluStagesB = GeluStagesS;
+#endif
 
 __device__ __forceinline__ u32x4v mlp_pack8(const float* v) {
   u32x4v u;
@@ -657,7 +717,7 @@ __global__ __launch_bounds__(64 * kMlpWaves, 1) void mlp_bwd_da_kernel(const bf1
         // S1(t0) | S1(t1) + act(t0) | da(t0) + act(t1) | da(t1) + da-product(t0) | da-product(t1)
         float av[16], g0[16], g1[16];  // g0 / g1 become the da values in place
         const f32x16 p0 = s1_w(st, 0, mlp_bias_acc(b1s, c, 0, h), [&](int) {});
-        GeluStages gs;
+        GeluStagesB gs;
         const f32x16 p1 = s1_w(st, 1, mlp_bias_acc(b1s, c, 1, h), [&](int k) { gelu_both_stage(k, p0, gs, av, g0); });
         store16(raa, lda, c, 0, av);
         if constexpr (PF) {  // h2 fragments are dead after the last chunk's W1 products
