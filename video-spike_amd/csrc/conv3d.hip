@@ -49,13 +49,15 @@ struct Igemm {
 };
 
 __device__ __forceinline__ int divq(int x, int d, float inv) {
-  // x / d for 0 <= x < 2^24 by a float reciprocal and one correction step
+  // x / d for 0 <= x < 2^24 by a float reciprocal and one correction step (24-bit multiply: full
+  // rate, where v_mul_lo_u32 is a quarter-rate instruction)
   int q = (int)((float)x * inv);
-  int r = x - q * d;
+  int r = x - (int)__umul24(q, d);
   if (r < 0) --q;
   else if (r >= d) ++q;
   return q;
 }
+__device__ __forceinline__ int mul24(int a, int b) { return (int)__umul24(a, b); }  // a, b in [0, 2^24)
 
 // f32 MFMA operand images: row-major [rows][k], 34-float rows (conflict-free ds_read_b32 of 16 rows x
 // 2 k per 32-lane half: bank = 2 row + k), filled by two ds_write_b64 per gathered float4
@@ -73,9 +75,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
   const int n0 = nt * BN;
   const int chunk = tid & 7;  // float4 index along k of this thread's operand loads
 
-  // the 4 A rows of this thread (rows tid/8 + 32 s): voxel coordinates of the gathered input
-  int rz[4], ry[4], rx[4];
-  int64_t rbase[4];
+  // the 4 A rows of this thread (rows tid/8 + 32 s): voxel coordinates of the gathered input and the
+  // voxel index of the row's tap-(0,0,0) origin.  Operand offsets are 32-bit (the host checks the
+  // gathered volume x C < 2^31): the int64 index chain and the two integer divisions of the tap
+  // were 31 v_mul_lo_u32 + 12 64-bit multiply-adds (quarter rate) per k step
+  int rz[4], ry[4], rx[4], rvb[4];
   bool rok[4];
   {
     const float ihw = 1.0f / (float)g.Gw, ihh = 1.0f / (float)g.Gh, ihd = 1.0f / (float)g.Gd;
@@ -84,28 +88,31 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
       const int64_t m = m0 + (tid >> 3) + 32 * s;
       rok[s] = m < g.M;
       const int mm = rok[s] ? (int)m : 0;
-      const int q1 = divq(mm, g.Gw, ihw), gw = mm - q1 * g.Gw;
-      const int q2 = divq(q1, g.Gh, ihh), gh = q1 - q2 * g.Gh;
-      const int n = divq(q2, g.Gd, ihd), gd = q2 - n * g.Gd;
+      const int q1 = divq(mm, g.Gw, ihw), gw = mm - mul24(q1, g.Gw);
+      const int q2 = divq(q1, g.Gh, ihh), gh = q1 - mul24(q2, g.Gh);
+      const int n = divq(q2, g.Gd, ihd), gd = q2 - mul24(n, g.Gd);
       rz[s] = gd * g.sd;
       ry[s] = gh * g.sh;
       rx[s] = gw * g.sw;
-      rbase[s] = (int64_t)n * g.Di;
+      rvb[s] = ((n * g.Di + rz[s]) * g.Hi + ry[s]) * g.Wi + rx[s];
     }
   }
   const int chw = g.ch * g.cw;
+  const float ichw = 1.0f / (float)chw, icw = 1.0f / (float)g.cw;
   auto load_a = [&](float4 (&ra)[4], int k0) {
     const int k = k0 + chunk * 4;
     const bool kok = k < g.K;
     const int tap = k >> g.cshift, c = k & (g.C - 1);
-    const int jd = tap / chw, jr = tap - jd * chw, jh = jr / g.cw, jw = jr - jh * g.cw;
-    const int oz = g.od0 + g.ods * jd, oy = g.oh0 + g.ohs * jh, ox = g.ow0 + g.ows * jw;
+    const int jd = divq(tap, chw, ichw), jr = tap - mul24(jd, chw);
+    const int jh = divq(jr, g.cw, icw), jw = jr - mul24(jh, g.cw);
+    const int oz = g.od0 + __mul24(g.ods, jd), oy = g.oh0 + __mul24(g.ohs, jh), ox = g.ow0 + __mul24(g.ows, jw);
+    const int toff = __mul24(__mul24(oz, g.Hi) + oy, g.Wi) + ox;  // voxel offset of the tap (may be < 0)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int z = rz[s] + oz, yy = ry[s] + oy, xx = rx[s] + ox;
       const bool ok = kok && rok[s] && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
                       (unsigned)xx < (unsigned)g.Wi;
-      const float* p = g.x + (((rbase[s] + z) * g.Hi + yy) * g.Wi + xx) * g.C + c;
+      const float* p = g.x + (uint32_t)(((rvb[s] + toff) << g.cshift) + c);
       ra[s] = ok ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
@@ -268,29 +275,76 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
   const int oz = td - g.pd, oy = th - g.ph, ox = tw - g.pw;
   const float ihw = 1.0f / (float)g.Wo, ihh = 1.0f / (float)g.Ho, ihd = 1.0f / (float)g.Do;
 
+  // Operand addresses as 32-bit element offsets (the host checks M < 2^24, M Co < 2^31 and the input
+  // volume x C < 2^31).  The gather's voxel coordinates are advanced incrementally: each thread keeps
+  // the (n, z0 = gd sd, y0 = gh sh, x0 = gw sw) of its row slots and adds the mixed-radix digits of
+  // one step (32 rows) with one conditional carry per digit, instead of three divisions per row and
+  // step (the int64 index chains with three float-reciprocal divisions per row were ~200 VALU per
+  // step, VALU : MFMA 6.5 : 1 in the counters, profiles/r05_pmc_convdw.json)
+  const int me32 = (int)me, mb32 = (int)mb;
+  const int XW = g.Wo * g.sw, YH = g.Ho * g.sh, ZD = g.Do * g.sd;
+  int cW, cH, cD, cN;  // the step's digits (x0, y0, z0 strides; n count)
+  {
+    int q = BM;
+    cW = (q % g.Wo) * g.sw; q /= g.Wo;
+    cH = (q % g.Ho) * g.sh; q /= g.Ho;
+    cD = (q % g.Do) * g.sd; q /= g.Do;
+    cN = q;
+  }
+  int sx0[XS], sy0[XS], sz0[XS], sn[XS];
+#pragma unroll
+  for (int s = 0; s < XS; ++s) {
+    const int m = mb32 + tid / KCH + XR * s;
+    const int mm = m < me32 ? m : 0;  // (a slot past the split end only ever loads zeros)
+    const int q1 = divq(mm, g.Wo, ihw), gw = mm - mul24(q1, g.Wo);
+    const int q2 = divq(q1, g.Ho, ihh), gh = q1 - mul24(q2, g.Ho);
+    const int n = divq(q2, g.Do, ihd), gd = q2 - mul24(n, g.Do);
+    sx0[s] = gw * g.sw;
+    sy0[s] = gh * g.sh;
+    sz0[s] = gd * g.sd;
+    sn[s] = n;
+  }
+  auto advance = [&]() {
+#pragma unroll
+    for (int s = 0; s < XS; ++s) {
+      int x0 = sx0[s] + cW;
+      const bool cw = x0 >= XW;
+      x0 -= cw ? XW : 0;
+      int y0 = sy0[s] + cH + (cw ? g.sh : 0);
+      const bool ch = y0 >= YH;
+      y0 -= ch ? YH : 0;
+      int z0 = sz0[s] + cD + (ch ? g.sd : 0);
+      const bool cd = z0 >= ZD;
+      z0 -= cd ? ZD : 0;
+      sx0[s] = x0;
+      sy0[s] = y0;
+      sz0[s] = z0;
+      sn[s] += cN + (cd ? 1 : 0);
+    }
+  };
+  // load(step) reads the slots' current coordinates: called for steps 0, 1, 2, ... in order, each
+  // call followed by advance()
   auto load = [&](float4 (&rd)[2], float4 (&rx)[XS], int step) {
+    const int mstep = mb32 + step * BM;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int64_t m = mb + (int64_t)step * BM + (tid >> 4) + 16 * s;
-      const bool ok = m < me;
-      const int mm = ok ? (int)m : 0;
-      rd[s] = ok ? *(const float4*)(g.dy + (int64_t)mm * g.Co + o0 + chunk * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int m = mstep + (tid >> 4) + 16 * s;
+      const bool ok = m < me32;
+      rd[s] = ok ? *(const float4*)(g.dy + (uint32_t)(mul24(m, g.Co) + o0 + chunk * 4))
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int s = 0; s < XS; ++s) {
-      const int64_t m = mb + (int64_t)step * BM + tid / KCH + XR * s;
-      const bool ok = m < me;
-      const int mm = ok ? (int)m : 0;
-      const int q1 = divq(mm, g.Wo, ihw), gw = mm - q1 * g.Wo;
-      const int q2 = divq(q1, g.Ho, ihh), gh = q1 - q2 * g.Ho;
-      const int n = divq(q2, g.Do, ihd), gd = q2 - n * g.Do;
-      const int z = gd * g.sd + oz, yy = gh * g.sh + oy, xx = gw * g.sw + ox;
-      const bool in = ok && kok && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
+      const int m = mstep + tid / KCH + XR * s;
+      const int z = sz0[s] + oz, yy = sy0[s] + oy, xx = sx0[s] + ox;
+      const bool in = m < me32 && kok && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
                       (unsigned)xx < (unsigned)g.Wi;
-      const float* p = g.x + ((((int64_t)n * g.Di + z) * g.Hi + yy) * g.Wi + xx) * g.C + c;
-      rx[s] = in ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int vox = mul24(mul24(mul24(sn[s], g.Di) + z, g.Hi) + yy, g.Wi) + xx;
+      rx[s] = in ? *(const float4*)(g.x + (uint32_t)((vox << g.cshift) + c)) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    advance();
   };
+
   auto store = [&](float* st, const float4 (&rd)[2], const float4 (&rx)[XS]) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) *(float4*)(st + ((tid >> 4) + 16 * s) * LDO + chunk * 4) = rd[s];
@@ -683,6 +737,8 @@ static double conv_flops(const vs_conv3d_desc* d) {
 }
 
 static int launch_igemm(const Igemm& g, hipStream_t s) {
+  VS_REQUIRE((int64_t)g.N * g.Di * g.Hi * g.Wi * g.C < (1ll << 31) && g.M < (1ll << 24) && g.K < (1 << 24),
+             "conv3d: gathered volume too large (32-bit operand offsets)");
   const int64_t tiles_m = (g.M + 127) / 128;
   const int64_t nwg = tiles_m * (g.Ng / 64);
   VS_REQUIRE(nwg < (1ll << 31), "conv3d: grid too large");
@@ -862,7 +918,9 @@ extern "C" int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float
   VS_REQUIRE((size_t)workspace_bytes >= vs_conv3d_dw_workspace_bytes(d), "vs_conv3d_dw: workspace too small");
   VS_REQUIRE(aligned16(x) && aligned16(dy) && aligned16(workspace), "vs_conv3d_dw: pointers must be 16-byte aligned");
   const int64_t M = d->N * d->Do * d->Ho * d->Wo;
-  VS_REQUIRE(M < (1ll << 24), "vs_conv3d_dw: volume too large");
+  VS_REQUIRE(M < (1ll << 24) && M * d->Co < (1ll << 31) && d->N * d->Di * d->Hi * d->Wi < (1ll << 24) &&
+                 d->N * d->Di * d->Hi * d->Wi * d->Ci < (1ll << 31),
+             "vs_conv3d_dw: volume too large (32-bit operand offsets)");
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_CONV_DW, s, conv_flops(d));
   const DwPlanC p = plan_conv_dw(d);
