@@ -58,6 +58,15 @@ __device__ __forceinline__ int divq(int x, int d, float inv) {
   return q;
 }
 __device__ __forceinline__ int mul24(int a, int b) { return (int)__umul24(a, b); }  // a, b in [0, 2^24)
+// 16-B load through a raw buffer resource: an offset past num_records (kOob) returns zeros with no
+// exec-mask branch or zeroing moves (the host keeps every operand below 2^31 bytes)
+constexpr uint32_t kOob = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t conv_rsrc(const float* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
 
 // f32 MFMA operand images: row-major [rows][k], 34-float rows (conflict-free ds_read_b32 of 16 rows x
 // 2 k per 32-lane half: bank = 2 row + k), filled by two ds_write_b64 per gathered float4
@@ -99,6 +108,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
   }
   const int chw = g.ch * g.cw;
   const float ichw = 1.0f / (float)chw, icw = 1.0f / (float)g.cw;
+  const auto rsx = conv_rsrc(g.x, (g.N * g.Di * g.Hi * g.Wi) << (g.cshift + 2));
+  const auto rsw = conv_rsrc(g.w, g.Ng * g.K * 4);
   auto load_a = [&](float4 (&ra)[4], int k0) {
     const int k = k0 + chunk * 4;
     const bool kok = k < g.K;
@@ -112,8 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
       const int z = rz[s] + oz, yy = ry[s] + oy, xx = rx[s] + ox;
       const bool ok = kok && rok[s] && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
                       (unsigned)xx < (unsigned)g.Wi;
-      const float* p = g.x + (uint32_t)(((rvb[s] + toff) << g.cshift) + c);
-      ra[s] = ok ? *(const float4*)p : make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[s] = bload4(rsx, ok ? (uint32_t)(((rvb[s] + toff) << g.cshift) + c) * 4u : kOob);
     }
   };
   auto load_b = [&](float4 (&rb)[2], int k0) {
@@ -121,7 +131,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int n = n0 + (tid >> 3) + 32 * s;
-      rb[s] = k < g.K ? *(const float4*)(g.w + (int64_t)n * g.K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[s] = bload4(rsw, k < g.K ? (uint32_t)(n * g.K + k) * 4u : kOob);
     }
   };
   auto store = [&](float* st, const float4 (&ra)[4], const float4 (&rb)[2]) {
@@ -282,6 +292,8 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
   // step (the int64 index chains with three float-reciprocal divisions per row were ~200 VALU per
   // step, VALU : MFMA 6.5 : 1 in the counters, profiles/r05_pmc_convdw.json)
   const int me32 = (int)me, mb32 = (int)mb;
+  const auto rsx = conv_rsrc(g.x, (g.N * g.Di * g.Hi * g.Wi) << (g.cshift + 2));
+  const auto rsdy = conv_rsrc(g.dy, (int)g.M * g.Co * 4);
   const int XW = g.Wo * g.sw, YH = g.Ho * g.sh, ZD = g.Do * g.sd;
   int cW, cH, cD, cN;  // the step's digits (x0, y0, z0 strides; n count)
   {
@@ -330,8 +342,7 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     for (int s = 0; s < 2; ++s) {
       const int m = mstep + (tid >> 4) + 16 * s;
       const bool ok = m < me32;
-      rd[s] = ok ? *(const float4*)(g.dy + (uint32_t)(mul24(m, g.Co) + o0 + chunk * 4))
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      rd[s] = bload4(rsdy, ok ? (uint32_t)(mul24(m, g.Co) + o0 + chunk * 4) * 4u : kOob);
     }
 #pragma unroll
     for (int s = 0; s < XS; ++s) {
@@ -340,7 +351,7 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
       const bool in = m < me32 && kok && (unsigned)z < (unsigned)g.Di && (unsigned)yy < (unsigned)g.Hi &&
                       (unsigned)xx < (unsigned)g.Wi;
       const int vox = mul24(mul24(mul24(sn[s], g.Di) + z, g.Hi) + yy, g.Wi) + xx;
-      rx[s] = in ? *(const float4*)(g.x + (uint32_t)((vox << g.cshift) + c)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rx[s] = bload4(rsx, in ? (uint32_t)((vox << g.cshift) + c) * 4u : kOob);
     }
     advance();
   };
@@ -737,8 +748,9 @@ static double conv_flops(const vs_conv3d_desc* d) {
 }
 
 static int launch_igemm(const Igemm& g, hipStream_t s) {
-  VS_REQUIRE((int64_t)g.N * g.Di * g.Hi * g.Wi * g.C < (1ll << 31) && g.M < (1ll << 24) && g.K < (1 << 24),
-             "conv3d: gathered volume too large (32-bit operand offsets)");
+  VS_REQUIRE((int64_t)g.N * g.Di * g.Hi * g.Wi * g.C < (1ll << 29) && (int64_t)g.Ng * g.K < (1ll << 29) &&
+                 g.M < (1ll << 24) && g.K < (1 << 24),
+             "conv3d: gathered volume too large (operands must stay below 2^31 bytes)");
   const int64_t tiles_m = (g.M + 127) / 128;
   const int64_t nwg = tiles_m * (g.Ng / 64);
   VS_REQUIRE(nwg < (1ll << 31), "conv3d: grid too large");
@@ -918,9 +930,9 @@ extern "C" int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float
   VS_REQUIRE((size_t)workspace_bytes >= vs_conv3d_dw_workspace_bytes(d), "vs_conv3d_dw: workspace too small");
   VS_REQUIRE(aligned16(x) && aligned16(dy) && aligned16(workspace), "vs_conv3d_dw: pointers must be 16-byte aligned");
   const int64_t M = d->N * d->Do * d->Ho * d->Wo;
-  VS_REQUIRE(M < (1ll << 24) && M * d->Co < (1ll << 31) && d->N * d->Di * d->Hi * d->Wi < (1ll << 24) &&
-                 d->N * d->Di * d->Hi * d->Wi * d->Ci < (1ll << 31),
-             "vs_conv3d_dw: volume too large (32-bit operand offsets)");
+  VS_REQUIRE(M < (1ll << 24) && M * d->Co < (1ll << 29) && d->N * d->Di * d->Hi * d->Wi < (1ll << 24) &&
+                 d->N * d->Di * d->Hi * d->Wi * d->Ci < (1ll << 29),
+             "vs_conv3d_dw: volume too large (operands must stay below 2^31 bytes)");
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_CONV_DW, s, conv_flops(d));
   const DwPlanC p = plan_conv_dw(d);
