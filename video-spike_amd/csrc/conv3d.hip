@@ -382,19 +382,37 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     const float* sx = sd_ + SO;
     const bool more = t + 1 < nsteps;
     if (more) load(rd, rx, t + 1);
-#pragma unroll
-    for (int sub = 0; sub < BM / 4; ++sub) {
+    // operand fragments read a half-step (4 sub-steps) ahead of their MFMAs: reading each sub-step's
+    // 4 values right before its 4 MFMAs (hipcc's choice, reusing 4 registers) serialised every
+    // sub-step behind an LDS round trip (conv dW 34.0 -> 32.5 ms/step at C4; the same change in
+    // conv_igemm_kernel, 146 VGPRs, measured slower: fwd 25.1 -> 26.2, dX 26.0 -> 26.9)
+    constexpr int NS = BM / 4, HS = NS / 2;
+    float af[NS][2], bfr[NS][NJ];
+    auto rd_ops = [&](int sub) {
       const int mrow = 4 * sub + (lane >> 4);
-      float af[2], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = sd_[mrow * LDO + wr * 32 + i * 16 + (lane & 15)];
+      for (int i = 0; i < 2; ++i) af[sub][i] = sd_[mrow * LDO + wr * 32 + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = sx[mrow * LD + wc * (BKK / 2) + j * 16 + (lane & 15)];
+      for (int j = 0; j < NJ; ++j) bfr[sub][j] = sx[mrow * LD + wc * (BKK / 2) + j * 16 + (lane & 15)];
+    };
+    auto mm_ops = [&](int sub) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[sub][i], bfr[sub][j], acc[i][j], 0, 0, 0);
+    };
+#pragma unroll
+    for (int sub = 0; sub < HS; ++sub) rd_ops(sub);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sub = HS; sub < NS; ++sub) rd_ops(sub);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sub = 0; sub < HS; ++sub) mm_ops(sub);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sub = HS; sub < NS; ++sub) mm_ops(sub);
     if (more) store(smem + ((t + 1) & 1) * STAGE, rd, rx);
     if ((t & 15) == 15) {
 #pragma unroll
