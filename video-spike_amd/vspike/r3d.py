@@ -438,8 +438,13 @@ class R3D(nn.Module):
         B = st["B"]
         head32 = self.head_flat.detach()
         dr = d_logrates.reshape(B, lay.out_dim).to(torch.float32).contiguous()
-        dz = torch.empty(B, lay.enc_out, dtype=torch.float32, device=dr.device)
-        ops.linear_dx(dr, lay.head.view(head32, "dec_w"), dz)
+        # dZ = dr dec_w reduces over K = 100 * neurons (25,600 at C4) for 16 x 64 outputs: split-K with the
+        # partials summed in a fixed order (as the ViT head); one 128 x 64 tile walking K alone was
+        # 869 us per step (profiles/r05_r3d_kernel_stats_bn.txt, gemm_f32_kernel<true, false>)
+        dz = torch.zeros(B, lay.enc_out, dtype=torch.float32, device=dr.device)
+        dz_ws = torch.empty(max(ops.splitk_workspace_bytes(torch.float32, B, lay.enc_out, lay.out_dim), 16) // 4 + 64,
+                            dtype=torch.float32, device=dr.device)
+        ops.linear_dx(dr, lay.head.view(head32, "dec_w"), dz, accumulate=True, workspace=dz_ws)
         g_head = None
         if want_head:
             g_head = self._grad_buffer(self.head_flat)
