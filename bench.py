@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--c3-warmup", type=int, default=3)
     ap.add_argument("--c3-profile-steps", type=int, default=2)
+    ap.add_argument("--c3-check-clips", type=int, default=8,
+                    help="C3 check: clips of the benched batch whose loss is back-propagated and checked (0: none)")
+    ap.add_argument("--c3-b16-steps", type=int, default=20, help="timed steps of the C3 16-clips/GPU point (0: skip)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 sub-record (R3D-18, 32x112x112 clips, n = 256, fp32) the default C2 run appends")
     ap.add_argument("--c4-batch", type=int, default=16, help="C4 sub-record clips per GPU")
@@ -154,8 +157,9 @@ def cpu_baseline(cfg, params, pixels, target, seconds, reps=10):
     the CPU share (affinity / cgroup quota; OMP_NUM_THREADS on the box) and os.cpu_count() as
     BASELINE.md asks; the latter is skipped when one B=1 forward at that count takes more than 4x
     the share's (oversubscription: the box's 256-CPU count vs its 16-CPU quota), and recorded so.
-    `value` is the B=4 fwd+bwd rate of the faster count; cells report median, min and max and are
-    checked for monotonicity (fwd+bwd dearer than fwd at each batch)."""
+    `value` is the best fwd+bwd rate per clip over the cells (thread count x batch 1 / 4: VERDICT r5
+    item 8); cells report median, min and max and are checked for monotonicity (fwd+bwd dearer than
+    fwd at each batch)."""
     from oracle import cpu_ref
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or _cpu_share()
     counts = [share] + ([os.cpu_count()] if (os.cpu_count() or 0) != share else [])
@@ -227,12 +231,19 @@ def cpu_baseline(cfg, params, pixels, target, seconds, reps=10):
         per_count[str(threads)] = res
     torch.set_num_threads(share)           # the rest of the run (parity oracle) on the process's share
     elapsed = time.perf_counter() - t_start
-    best = min(per_count, key=lambda k: per_count[k]["B4_fwd_bwd"]["s_per_clip"])
-    value = 1.0 / per_count[best]["B4_fwd_bwd"]["s_per_clip"]
+    # `value`: the CPU's best per-clip training rate over the measured cells (thread count x batch).  The
+    # B = 4 backward is the dearer one per clip on the box: autograd keeps every layer's B x H x N^2 f32
+    # attention probabilities (118 MB per layer at B = 4, 1.4 GB over 12 layers, vs 29 MB at B = 1) and
+    # the backward's softmax' / matmul reads of them run from DRAM instead of the caches
+    # (scripts/cpu_baseline_profile.py), so B = 1 is the fair CPU rate there
+    best, best_b = min(((k, b) for k in per_count for b in (1, 4)),
+                       key=lambda kb: per_count[kb[0]][f"B{kb[1]}_fwd_bwd"]["s_per_clip"])
+    value = 1.0 / per_count[best][f"B{best_b}_fwd_bwd"]["s_per_clip"]
     out = {"value": round(value, 4), "unit": "clips/sec", "cores": int(best), "kind": "port",
-           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, batch 4, median of {reps} interleaved rounds "
-                     f"(all four cells per round) after 2 warm-ups per cell, {best} threads pinned to "
-                     f"{best} cores; {elapsed:.1f} s of CPU work in all",
+           "sample": f"oracle/cpu_ref.py torch-CPU fp32 train fwd+bwd, the faster per clip of batch 1 and 4 (batch "
+                     f"{best_b}), median of {reps} interleaved rounds (all four cells per round) after 2 warm-ups per "
+                     f"cell, {best} threads pinned to {best} cores; {elapsed:.1f} s of CPU work in all",
+           "batch": best_b,
            "host": {"cpu_model": _cpu_model_name(), "nproc": os.cpu_count(), "cpu_share": _cpu_share(),
                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS")},
            "detail": per_count, "skipped": skipped}
@@ -262,7 +273,7 @@ PARITY_TOL = {"fp32": {"log_rates": 1e-4, "loss": 1e-5, "grad": 1e-3},
               "fp8": None}
 
 
-def full_batch_parity(ccfg, params, pixels, target, gpu, args):
+def full_batch_parity(ccfg, params, pixels, target, gpu, args, what=None):
     """The benched step's fwd+bwd (whole batch, initial weights) vs the CPU fp32 oracle on the same
     clips: log-rates (max abs error / max |ref|), loss (relative) and every gradient (norm-relative)."""
     import numpy as np
@@ -311,8 +322,8 @@ def full_batch_parity(ccfg, params, pixels, target, gpu, args):
         from oracle.tolerances import FP8_MX12_GRAD, FP8_MX12_LOSS, FP8_MX12_OUT
         tol = {"log_rates": FP8_MX12_OUT, "loss": FP8_MX12_LOSS, "grad": FP8_MX12_GRAD}
     ok = e_out < tol["log_rates"] and e_loss < tol["loss"] and (not errs or errs[worst] < tol["grad"])
-    return {"what": f"one fwd+bwd of the whole benched batch ({pixels.shape[0]} clips, the timed step's dispatch) at "
-                    "the initial weights: HIP path vs the CPU fp32 oracle (oracle/cpu_ref.py" +
+    return {"what": (what or f"one fwd+bwd of the whole benched batch ({pixels.shape[0]} clips, the timed step's "
+                             "dispatch) at the initial weights") + ": HIP path vs the CPU fp32 oracle (oracle/cpu_ref.py" +
                     (", the four block products on MX-FP8 round trips: cpu_ref.mx_matmul)" if mm else ")"),
             "log_rates_maxrel": round(e_out, 7), "loss_rel": round(e_loss, 8), "n_grads": len(errs),
             "worst_grad": worst, "worst_grad_rel": round(errs[worst], 6) if worst else None,
@@ -578,45 +589,37 @@ def _oracle_cfg(bb):
                                                          "layer_norm_eps")})
 
 
-# bars of the C3 sub-record's micro-batch check (the bf16 log-rate bar of the full-batch check; the
-# loss of two clips is a mean over 102,400 terms)
-C3_CHECK_TOL = {"log_rates": 7e-3, "loss": 1e-3}
-
-
 def c3_subrecord(args, world, rank, dev):
     """BASELINE C3 in the same run: ViT-Base/16 (the reference plugin's own width,
     /root/reference/src/model/videomae.py:7,13) at the reference's 128 clips per process
     (config/train/vmae_video.yaml:20), n = 512, encoder trainable, bf16: timed steps at the benched
-    dispatch plus a CPU-oracle check of one micro-batch (2 clips) of the benched forward's log-rates
-    and Poisson loss.  lr 5e-8: the synthetic C3 setup diverges at the config's 5e-5 (DESIGN.md section
+    dispatch; a fwd + bwd check against the CPU oracle: the whole 128-clip batch
+    runs forward and backward through the benched dispatch with the loss taken over its first
+    `--c3-check-clips` clips (the backward then carries those clips' gradient through every benched
+    kernel, zeros elsewhere), and the oracle runs those clips one at a time: log-rates, loss and EVERY
+    gradient at C2's bf16 bars; and the DP=8 per-GPU point (global 128 = 16 clips
+    per GPU) as `b16`.  lr 5e-8: the synthetic C3 setup diverges at the config's 5e-5 (DESIGN.md section
     1), which the throughput does not depend on."""
     spec = {"model": "vmae_video", "neurons": 512, "dtype": "bf16", "frames": None, "freeze": False,
             "lr": 5e-8, "loss": "poisson", "batch": args.c3_batch}
     config, criterion, model, B, pixels, target = _setup(spec, dev, rank)
     bb = model.backbone
     check = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import cpu_ref
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.c3_check_clips > 0:
+        nchk = min(args.c3_check_clips, B)
         init = {k: v.detach().cpu().numpy() for k, v in model.reference_state_dict(modern_names=True).items()}
-        with torch.no_grad():
-            out0 = model(pixels)
-            gl = out0[:2].float().cpu()
-            gloss = float(criterion(out0[:2], target[:2]))
-        del out0
-        t0 = time.perf_counter()
-        P = cpu_ref.to_torch(init, requires_grad=False)
-        with torch.no_grad():
-            ref = cpu_ref.videomae_plugin_forward(pixels[:2].cpu(), P, _oracle_cfg(bb), False)
-            rloss = float(cpu_ref.poisson_nll_mean(ref, target[:2].cpu()))
-        e_out = float((gl - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-        e_loss = abs(gloss - rloss) / abs(rloss)
-        check = {"what": f"clips 0..1 of the benched {B}-clip forward (log-rates are per clip) and their Poisson "
-                         "loss vs the CPU fp32 oracle (oracle/cpu_ref.py) at the initial weights",
-                 "log_rates_maxrel": round(e_out, 7), "loss_rel": round(e_loss, 8), "tolerance": C3_CHECK_TOL,
-                 "ok": bool(e_out < C3_CHECK_TOL["log_rates"] and e_loss < C3_CHECK_TOL["loss"]),
-                 "cpu_seconds": round(time.perf_counter() - t0, 1)}
-        del P
-        _progress(f"C3 micro-batch check: {check}")
+        out0 = model(pixels)
+        loss0 = criterion(out0[:nchk], target[:nchk])
+        loss0.backward()
+        gpu = {"loss": float(loss0), "log_rates": out0[:nchk].detach().float().cpu(), "grads": _reference_grads(model)}
+        model.zero_grad(set_to_none=True)
+        del out0, loss0
+        chk_args = argparse.Namespace(dtype="bf16", loss="poisson")
+        check = full_batch_parity(_oracle_cfg(bb), init, pixels[:nchk].cpu(), target[:nchk].cpu(), gpu, chk_args,
+                                  what=f"fwd of the whole benched {B}-clip batch and bwd of the Poisson loss over its first "
+                                       f"{nchk} clips, at the benched dispatch and the initial weights (every gradient)")
+        del init, gpu
+        _progress(f"C3 check: {check}")
     run = _train_and_time(model, config, criterion, pixels, target, world, rank, dev, args.c3_steps, args.c3_warmup,
                           args.c3_profile_steps, tag="C3: ")
     roof_all, roofline = _roofline(run["kern"], args.c3_profile_steps, bb, B, "bf16")
@@ -635,7 +638,21 @@ def c3_subrecord(args, world, rank, dev):
            "roofline": {k: roofline[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac",
                                                  "avg_launch_ms")} if roofline else None}
     out["mfma_util_pct"] = round(100.0 * out["model_tflops"] / PEAK_BF16_TFLOPS, 2)
-    del run, model
+    del run, model, pixels, target
+    if args.c3_b16_steps > 0:
+        # the DP=8 per-GPU batch of the reference config (global 128 over 8 GPUs = 16 clips per GPU),
+        # timed on this GPU alone: what each rank of the driver's 8-GPU C3 run would compute per step
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        config, criterion, model, B16, pixels, target = _setup({**spec, "batch": 16}, dev, rank)
+        r16 = _train_and_time(model, config, criterion, pixels, target, world, rank, dev, args.c3_b16_steps,
+                              args.c3_warmup, 0, tag="C3 b16: ")
+        out["b16"] = {"value": round(world * B16 * args.c3_b16_steps / r16["elapsed"], 3), "unit": "clips/sec",
+                      "clips_per_gpu": B16, "steps": args.c3_b16_steps, "warmup": args.c3_warmup,
+                      "ms_per_step": round(1e3 * r16["elapsed"] / args.c3_b16_steps, 3),
+                      "what": "SURVEY.md 8(d): C3's per-GPU batch under DP=8 (global 128, vmae_video.yaml:20), one GPU"}
+        del r16, model, pixels, target
     return out
 
 

@@ -446,8 +446,9 @@ typedef struct vs_conv3d_desc {
   int32_t pd, ph, pw;               /* zero padding */
   int32_t reserved;
 } vs_conv3d_desc;
-/* y = conv(x, w); optional stats [ceil(N Do Ho Wo / 128)][2][Co]: per 128-row tile the column sums of
-   y and y^2 (the BatchNorm3d batch statistics, finished by vs_bn3d_stats).  Co % 64 == 0. */
+/* y = conv(x, w); optional stats [ceil(N Do Ho Wo / 128)][2][Co]: per 128-row tile t (output rows
+   [128 t, min(128 t + 128, rows))) the column sum of y and the column sum of (y - the tile's column mean)^2
+   (the BatchNorm3d batch statistics, merged by vs_bn3d_stats).  Co % 64 == 0. */
 int vs_conv3d_fwd(const vs_conv3d_desc* d, const float* x, const float* w, float* y, float* stats, void* stream);
 size_t vs_conv3d_stats_rows(const vs_conv3d_desc* d);
 /* dx (=|+=) the input gradient of dy: stride 1 as the flipped-kernel conv of dy, stride 2 as one
@@ -463,8 +464,9 @@ int vs_conv3d_dx(const vs_conv3d_desc* d, const float* dy, const float* w, float
 size_t vs_conv3d_dw_workspace_bytes(const vs_conv3d_desc* d);
 int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
                  void* workspace, int64_t workspace_bytes, void* stream);
-/* BatchNorm3d (training): from the conv's stats partials (rows of [2][C]) -> mean, rstd over count
-   values per channel (biased variance, eps), scale = gamma rstd, shift = beta - mean scale; the
+/* BatchNorm3d (training): from the conv's stats partials (rows = ceil(count / 128) tiles of [2][C] as
+   vs_conv3d_fwd writes them) -> mean, rstd over count values per channel (biased variance, eps; the
+   tiles merged in f64 with Chan's formula, no E[y^2] - mean^2 cancellation), scale = gamma rstd, shift = beta - mean scale; the
    running buffers (nullable) move by momentum with the unbiased variance (torch semantics). */
 size_t vs_bn3d_stats_workspace_bytes(int64_t rows, int64_t C);
 int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t count, const float* gamma,
@@ -480,6 +482,12 @@ size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C);
 int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
                 const float* mean, const float* rstd, const float* gamma, float* dy, float* dres, float* dgamma,
                 float* dbeta, void* workspace, void* stream);
+/* The same for an eval-mode (running-statistics) BatchNorm: mean / rstd are the running statistics,
+   constants of the forward, so dy = gamma rstd g (no batch-statistics terms); dgamma / dbeta / dres
+   as vs_bn3d_bwd (nn.BatchNorm3d.eval() under autograd: frozen-BN fine-tuning). */
+int vs_bn3d_bwd_eval(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
+                     const float* mean, const float* rstd, const float* gamma, float* dy, float* dres,
+                     float* dgamma, float* dbeta, void* workspace, void* stream);
 /* pixels (B, T, C, H, W) f32 -> channels-last (B, T, H, W, Cp) with channels C..Cp-1 zero (Cp = 4 or 8). */
 int vs_to_channels_last(int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int64_t Cp, const float* x,
                         float* out, void* stream);
@@ -585,6 +593,10 @@ int vs_timing_bytes(int timer, double* algorithmic_bytes);   /* call before vs_t
 /* copies min(n, VS_PATH_COUNT) counters into out; returns VS_PATH_COUNT */
 int vs_dispatch_counts(int64_t* out, int n);
 int vs_dispatch_reset(void);
+/* 1 when every compiled instance of the 256 x 256 forward / dX GEMM (VS_PATH_GEMM_G256) has no private
+   (scratch) segment: its early-DMA wait counts the epilogue's stores exactly.  An instance that spills
+   falls back to vmcnt(0) on its own; this is the test's view of the same check. */
+int vs_g256_scratch_free(void);
 
 /* ------------------------------------------------------------------------------------------
  * A/B and test knobs.  Each is read ONCE from the environment (VSPIKE_<NAME>, an integer; unset =

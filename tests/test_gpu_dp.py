@@ -232,3 +232,82 @@ def test_rccl_comm_c_abi_single_rank():
         assert torch.equal(t, ref)
     comm.allreduce_(torch.empty(0, device=DEV))
     comm.close()
+
+
+# ------------------------------------------------------------------------------------------------
+# R3D (BASELINE C4) under the exchange: the plugin hands each conv unit's span of its gradient buffer
+# over as soon as that unit's backward has run (reverse order), so buckets all-reduce under the
+# earlier units' backward (src/train.py:61-64, src/trainer/base.py:150)
+# ------------------------------------------------------------------------------------------------
+def _r3d(n=16):
+    from vspike import R3D
+    cfg = cpu_ref.R3DCfg(num_frames=4, image_size=56)
+    conf = {"model_class": "R3D", "compute_dtype": "fp32", "freeze_encoder": False,
+            "backbone": {"num_frames": cfg.num_frames, "image_size": cfg.image_size, "num_channels": cfg.num_channels},
+            "encoder": {"output_dim": 64}, "decoder": {"output_dim": 100 * n}}
+    m = R3D(conf).to(DEV)
+    m.load_reference_state_dict({k: torch.from_numpy(v) for k, v in cpu_ref.make_r3d_params(cfg, 64, n).items()},
+                                strict=False)
+    return cfg, m
+
+
+def _r3d_batch(cfg, n=16):
+    px = torch.from_numpy(cpu_ref.make_r3d_pixels(cfg, 4, seed=31))
+    y = torch.from_numpy(prng.spike_targets(32, (4, 100, n)))
+    return px, y
+
+
+def _worker_r3d(rank, world, port, out):
+    import torch.distributed as dist
+    from vspike import poisson_nll_mean
+    from vspike.dp import GradExchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg, m = _r3d()
+    if rank == 1:                                   # different replicas: the broadcast aligns them
+        with torch.no_grad():
+            m.enc_flat.mul_(1.5)
+    ex = GradExchange(m, bucket_mb=0.25)
+    px, y = _r3d_batch(cfg)
+    per = 4 // world
+    loss = poisson_nll_mean(m(px[rank * per:(rank + 1) * per].to(DEV)), y[rank * per:(rank + 1) * per].to(DEV))
+    loss.backward()
+    launched_in_backward = len(ex._works)           # collectives started before the backward returned
+    ex.finish()
+    torch.cuda.synchronize()
+    out[rank] = (m.enc_flat.grad.detach().cpu() / world, m.head_flat.grad.detach().cpu() / world,
+                 launched_in_backward)
+    dist.destroy_process_group()
+
+
+def test_r3d_two_ranks_exchange_overlaps_and_matches():
+    """Two ranks (gloo, one GPU) each train the R3D plugin on half of a 4-clip batch with the exchange.
+    Training-mode BatchNorm normalises by each rank's own batch (DDP without SyncBatchNorm does the
+    same), so the reference is the average of the two halves' single-process gradients.  The
+    per-unit hand-off must have launched several all-reduces before the backward returned."""
+    import torch.multiprocessing as mp
+    from vspike import poisson_nll_mean
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_r3d, args=(world, _free_port(), out), nprocs=world, join=True)
+    cfg, m = _r3d()
+    px, y = _r3d_batch(cfg)
+    ge, gh = 0.0, 0.0
+    for h in range(2):
+        m.zero_grad(set_to_none=True)
+        poisson_nll_mean(m(px[2 * h:2 * h + 2].to(DEV)), y[2 * h:2 * h + 2].to(DEV)).backward()
+        torch.cuda.synchronize()
+        ge = ge + m.enc_flat.grad.detach().cpu() / 2
+        gh = gh + m.head_flat.grad.detach().cpu() / 2
+    for r in range(world):
+        e, h, launched = out[r]
+        ee = float((e - ge).norm() / ge.norm())
+        eh = float((h - gh).norm() / gh.norm())
+        print(f"\n[r3d exchange rank {r}] encoder {ee:.2e} head {eh:.2e}, {launched} all-reduces launched "
+              "during the backward")
+        assert ee < 1e-5 and eh < 1e-5
+        assert launched >= 4
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

@@ -438,6 +438,15 @@ def test_gemm_big_tile_c3_bench128(prod, kernel, knobs):
     assert err < tol
 
 
+def test_g256_early_dma_instances_have_no_scratch():
+    """The 256 x 256 kernel's early-DMA wait is vmcnt(<the epilogue's store count>): exact only while
+    the epilogue issues no other vector-memory op (a register spill adds scratch loads / stores).  The
+    launcher falls back to vmcnt(0) per instance on its own; this pins that the benched instances keep
+    the fast path."""
+    from vspike import _lib as L
+    assert L.lib().vs_g256_scratch_free() == 1
+
+
 @pytest.mark.parametrize("M", [25088, 9000])
 def test_patch_embed_gemm_pos_on_row_slab(M):
     """The patch embedding x0 = cols W^T + b + sinusoid[token] (K = 1536, N = 192, pos rows = 1568)

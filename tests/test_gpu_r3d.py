@@ -43,6 +43,17 @@ def _cl(x):           # NCDHW -> channels-last NDHWC
     return x.permute(0, 2, 3, 4, 1).contiguous()
 
 
+def _tile_partials(yr):
+    """The BatchNorm statistics partials vs_conv3d_fwd writes, in f64: per 128-row tile the column sum
+    and the column sum of squared deviations from the tile mean."""
+    S, M2 = [], []
+    for i in range(0, yr.shape[0], 128):
+        t = yr[i:i + 128].double()
+        S.append(t.sum(0))
+        M2.append(((t - t.mean(0)) ** 2).sum(0))
+    return torch.stack(S), torch.stack(M2)
+
+
 def _spec(ci, co, k, s, p):
     from vspike.r3d import ConvSpec
     return ConvSpec("t.0", ci, co, k, s, p, ci)
@@ -90,10 +101,13 @@ def test_conv3d_fwd_dx_dw_match_torch(case):
     assert L.dispatch_counts()["conv_igemm"] >= 1 and L.dispatch_counts()["conv_dw"] == 1
     assert _maxrel(y, _cl(ref.detach())) < 1e-5
     yr = _cl(ref.detach()).reshape(-1, Co)
-    st = stats.double().cpu().sum(0)
-    # column sums: rounding is relative to the sum of |y| (the sums themselves can cancel to ~0)
-    assert float(((st[0] - yr.sum(0)).abs() / yr.abs().sum(0)).max()) < 1e-5
-    assert _maxrel(st[1], (yr * yr).sum(0)) < 1e-5
+    s_ref, m2_ref = _tile_partials(yr)
+    st = stats.double().cpu()
+    # per 128-row tile: the column sum (rounding relative to the sum of |y|: the sums can cancel to ~0)
+    # and the sum of squared deviations from the tile's own mean
+    tabs = torch.stack([yr[i:i + 128].abs().sum(0) for i in range(0, yr.shape[0], 128)])
+    assert float(((st[:, 0] - s_ref).abs() / tabs).max()) < 1e-5
+    assert _maxrel(st[:, 1], m2_ref) < 1e-5
     assert _maxrel(dw, rdw.permute(0, 2, 3, 4, 1)) < 1e-5
     if Ci % 64 == 0:
         dx = torch.full((N, D, H, W, Ci), float("nan"), device=DEV)      # every element must be written
@@ -137,12 +151,12 @@ def test_bn3d_train_forward_backward_match_torch(C, relu, res):
     dy_r, dg_r, db_r, dres_r = torch.autograd.grad(o, (yd, gd, bd, rd), go, allow_unused=True)
     M = N * D * H * W
     y_cl = _cl(y).to(DEV)
-    part = y_cl.view(M, C).double()
-    stats = torch.stack([part.sum(0), (part * part).sum(0)]).float().view(1, 2, C)
+    ts, tm2 = _tile_partials(y_cl.view(M, C).cpu())
+    stats = torch.stack([ts, tm2], 1).float()
     mean, rstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
     rm_d, rv_d = rm.clone().to(DEV), rv.clone().to(DEV)
     g_d, b_d = gamma.to(DEV), beta.to(DEV)
-    r3d.bn3d_stats(stats.to(DEV), 1, M, g_d, b_d, 1e-5, 0.1, mean, rstd, scale, shift, rm_d, rv_d)
+    r3d.bn3d_stats(stats.to(DEV), stats.shape[0], M, g_d, b_d, 1e-5, 0.1, mean, rstd, scale, shift, rm_d, rv_d)
     out = torch.empty_like(y_cl)
     res_cl = _cl(resid).to(DEV) if res else None
     r3d.bn3d_apply(y_cl, scale, shift, out, residual=res_cl, relu=relu)
@@ -157,6 +171,73 @@ def test_bn3d_train_forward_backward_match_torch(C, relu, res):
     assert _maxrel(dgam, dg_r) < 1e-5 and _maxrel(dbet, db_r) < 1e-5
     if res:
         assert _maxrel(dres, _cl(dres_r)) < 1e-6
+
+
+def test_bn3d_stats_large_channel_offset():
+    """Batch statistics when |mean| >> std (mean ~1e3, std ~1: trained weights can reach this), through
+    the conv epilogue's partials and vs_bn3d_stats, vs f64: a one-pass sum of y^2 in f32 loses the
+    variance to cancellation (E[y^2] - mean^2 with E[y^2] ~ 1e6); the tile-mean-centred partials merged
+    with Chan's formula keep it."""
+    from vspike import r3d
+    C, N, D, H, W = 64, 2, 4, 10, 13
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, C, D, H, W, generator=g) + 1000.0 + torch.arange(C).view(1, C, 1, 1, 1) * 3.0
+    w = torch.eye(C).view(C, C, 1, 1, 1)                       # 1x1x1 identity conv: y = x
+    d = r3d._desc(_spec(C, C, (1, 1, 1), (1, 1, 1), (0, 0, 0)), N, D, H, W)
+    y = torch.empty(N, D, H, W, C, device=DEV)
+    rows = r3d.conv3d_stats_rows(d)
+    stats = torch.empty(rows, 2, C, device=DEV)
+    r3d.conv3d_fwd(d, _cl(x).to(DEV), w.permute(0, 2, 3, 4, 1).contiguous().to(DEV), y, stats)
+    mean, rstd, scale, shift = (torch.empty(C, device=DEV) for _ in range(4))
+    M = N * D * H * W
+    r3d.bn3d_stats(stats, rows, M, torch.ones(C, device=DEV), torch.zeros(C, device=DEV), 1e-5, 0.1, mean, rstd,
+                   scale, shift)
+    torch.cuda.synchronize()
+    yd = _cl(x).reshape(M, C).double()
+    var = yd.var(0, unbiased=False)
+    assert _maxrel(mean, yd.mean(0)) < 1e-6
+    got_var = 1.0 / rstd.double().cpu() ** 2 - 1e-5
+    err = float(((got_var - var).abs() / var).max())
+    print(f"\n[bn stats, mean ~1e3, std ~1] variance rel err {err:.2e}")
+    assert err < 1e-4
+
+
+@pytest.mark.parametrize("relu,res", [(True, True), (False, False)])
+def test_bn3d_eval_backward_matches_torch(relu, res):
+    """vs_bn3d_bwd_eval: the backward of an eval-mode (running-statistics) BatchNorm3d + residual + ReLU
+    vs torch autograd through F.batch_norm(training=False): dy = gamma rstd g."""
+    from vspike import r3d
+    C = 128
+    g = torch.Generator().manual_seed(3)
+    N, D, H, W = 2, 3, 5, 6
+    y = torch.randn(N, C, D, H, W, generator=g) * 1.3 + 0.2
+    gamma = torch.randn(C, generator=g) * 0.1 + 1.0
+    beta = torch.randn(C, generator=g) * 0.1
+    resid = torch.randn(N, C, D, H, W, generator=g)
+    rm, rv = torch.randn(C, generator=g) * 0.3, torch.rand(C, generator=g) + 0.5
+    yd, gd, bd = y.double().requires_grad_(), gamma.double().requires_grad_(), beta.double().requires_grad_()
+    o = F.batch_norm(yd, rm.double(), rv.double(), gd, bd, training=False, eps=1e-5)
+    if res:
+        o = o + resid.double()
+    if relu:
+        o = F.relu(o)
+    go = torch.randn(o.shape, generator=g).double()
+    dy_r, dg_r, db_r = torch.autograd.grad(o, (yd, gd, bd), go)
+    y_cl = _cl(y).to(DEV)
+    rstd = torch.rsqrt(rv + 1e-5).to(DEV)
+    mean = rm.to(DEV)
+    g_d = gamma.to(DEV)
+    scale, shift = g_d * rstd, beta.to(DEV) - mean * g_d * rstd
+    out = torch.empty_like(y_cl)
+    r3d.bn3d_apply(y_cl, scale, shift, out, residual=_cl(resid).to(DEV) if res else None, relu=relu)
+    dy = torch.empty_like(y_cl)
+    dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    r3d.bn3d_bwd(_cl(go.float()).to(DEV), out, relu, y_cl, mean, rstd, g_d, dy, None, dgam, dbet,
+                 batch_stats=False)
+    torch.cuda.synchronize()
+    assert _maxrel(out, _cl(o.detach())) < 1e-5
+    assert _maxrel(dy, _cl(dy_r)) < 1e-5
+    assert _maxrel(dgam, dg_r) < 1e-5 and _maxrel(dbet, db_r) < 1e-5
 
 
 def _r3d_model(cfg, n, enc_out=64):
@@ -287,6 +368,30 @@ def test_r3d_plugin_loss_curve_and_eval_match_oracle():
                                     training=False)
     print(f"[r3d eval] {_maxrel(ev, ref):.3e}")
     assert _maxrel(ev, ref) < 1e-4
+    # backward through the eval-mode forward (frozen-BN fine-tuning): the running
+    # statistics are constants, so BN' is gamma rstd g with no batch-statistics terms; vs the f64 oracle
+    yy = batches[0][1]
+    Pd = {k: torch.from_numpy(v).double().requires_grad_() for k, v in params.items()}
+    rund = {k: v.double() for k, v in running.items()}
+    rl = cpu_ref.poisson_nll_mean(cpu_ref.r3d18_forward(xe.double(), Pd, cfg, running=rund, training=False),
+                                  yy.double())
+    rl.backward()
+    loss = poisson_nll_mean(m2(xe.to(DEV)), yy.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    lay = m2.layout
+    worst = 0.0
+    for c in lay.convs:
+        gw = lay.enc.view(m2.enc_flat.grad, c.name + ".weight")[..., :c.ci_ref].permute(0, 4, 1, 2, 3)
+        rg = Pd[c.name + ".weight"].grad
+        worst = max(worst, float((gw.double().cpu() - rg).norm() / rg.norm()))
+        bn = c.name[:-2] + ".1"
+        for suf in (".weight", ".bias"):
+            gb, rb = lay.enc.view(m2.enc_flat.grad, bn + suf), Pd[bn + suf].grad
+            worst = max(worst, float((gb.double().cpu() - rb).norm() / rb.norm()))
+    print(f"[r3d eval backward] loss {abs(loss.item() - rl.item()) / abs(rl.item()):.3e} worst grad {worst:.3e}")
+    assert abs(loss.item() - rl.item()) / abs(rl.item()) < 1e-5
+    assert worst < 1e-3
 
 
 def test_r3d_raw_video_input_and_registry():

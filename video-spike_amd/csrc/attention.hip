@@ -1553,7 +1553,12 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
 extern "C" int vs_attn_redo_count(int64_t* out, int32_t reset) {
   VS_REQUIRE(out, "vs_attn_redo_count: null pointer");
   unsigned long long v = 0;
-  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(vs::g_attn_redo), sizeof(v), 0, hipMemcpyDeviceToHost);
+  // synchronising (as the header says): forward launches on any stream (torch's side streams are
+  // not ordered against the null-stream symbol copies) have finished their atomicAdd before the
+  // read, and none is in flight when the counter is reset
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(vs::g_attn_redo), sizeof(v), 0, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return (int)e;
   *out = (int64_t)v;
   if (reset) {

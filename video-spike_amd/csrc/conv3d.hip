@@ -19,7 +19,7 @@
 //   * dW: tiles of (64 out channels x 64 k) summed over the output voxels (the gather as the B
 //     operand), split over the voxel rows; partial tiles summed in split order (no atomics).
 //   * BatchNorm3d statistics ride in the forward conv's epilogue (per 128-row tile column sums of y and
-//     y^2), finished in f64 in a fixed order; apply (+ residual + ReLU) and the backward are
+//     of the squared deviations from the tile mean), merged in f64 in a fixed order (Chan); apply (+ residual + ReLU) and the backward are
 //     channel-vectorised elementwise passes with fixed-order reductions.
 #include <cstdlib>
 
@@ -44,7 +44,7 @@ struct Igemm {
   int Od, Oh, Ow;
   int ysd, ysh, ysw, yod, yoh, yow;   // output voxel = g * ys + yo
   int accumulate;
-  float* stats;               // [tiles_m][2][Ng] column sums of y and y^2 per 128-row tile, or null
+  float* stats;               // [tiles_m][2][Ng] per 128-row tile: column sum of y, sum of (y - tile mean)^2; or null
   int64_t M;
 };
 
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
   }
 
   // epilogue: acc[i][j][r] = C[wr*64 + i*16 + 4*(lane>>4) + r][wc*32 + j*16 + (lane&15)]
-  float csum[2] = {0.f, 0.f}, csq[2] = {0.f, 0.f};
+  float csum[2] = {0.f, 0.f};
   {
     const float ihw = 1.0f / (float)g.Gw, ihh = 1.0f / (float)g.Gh, ihd = 1.0f / (float)g.Gd;
 #pragma unroll
@@ -208,26 +208,45 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(Igemm g) {
           float v = acc[i][j][r];
           if (g.accumulate) v += dst[j * 16];
           dst[j * 16] = v;
+          acc[i][j][r] = v;  // the stored value, for the tile's second statistics pass
           csum[j] += v;
-          csq[j] += v * v;
         }
       }
   }
   if (g.stats) {
-    // column sums over this wave's 64 rows: the 4 lane groups (lane >> 4), then the two row waves
+    // BatchNorm partials per 128-row tile: the column sum S and the sum of squared deviations from
+    // the TILE's own column mean, M2 = sum (y - S/n)^2 (two passes over the registers), merged later
+    // with Chan's formula in f64.  A single-pass sum of y^2 loses the variance to cancellation in f32
+    // when |mean| >> std (trained weights): E[y^2] - mean^2.
     __shared__ float red[2][2][64];
     __syncthreads();  // (smem reads done; red is a separate array written once)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      float s = csum[j], q = csq[j];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
+      float v = csum[j];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) red[wr][0][wc * 32 + j * 16 + lane] = v;
+    }
+    __syncthreads();
+    const int64_t nrows = g.M - m0 < BM ? g.M - m0 : BM;
+    const float inv_n = 1.0f / (float)nrows;
+    float csq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = wc * 32 + j * 16 + (lane & 15);
+      const float mu = (red[0][0][col] + red[1][0][col]) * inv_n;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+          const float dv = acc[i][j][r] - mu;
+          csq[j] += m < g.M ? dv * dv : 0.f;
+        }
+      float q = csq[j];
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
-      if (lane < 16) {
-        red[wr][0][wc * 32 + j * 16 + lane] = s;
-        red[wr][1][wc * 32 + j * 16 + lane] = q;
-      }
+      if (lane < 16) red[wr][1][wc * 32 + j * 16 + lane] = q;
     }
     __syncthreads();
     if (tid < 128) {
@@ -475,23 +494,44 @@ __global__ __launch_bounds__(256) void conv_dx_weights(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 // BatchNorm3d
 // ------------------------------------------------------------------------------------------------
-// level 1: rows [r0, r0 + 256) of the [rows][2][C] partials, 64 channels per block: f64 sums
+// The partials are per 128-row tile t (rows [128 t, min(128 t + 128, count))): S_t = sum y and
+// M2_t = sum (y - S_t / n_t)^2.  Merged in f64 in a fixed order with Chan's formula: over a set of
+// tiles, S = sum S_t, mean = S / n, M2 = sum M2_t + sum n_t (S_t / n_t - mean)^2.
+constexpr int kBnTile = 128;
+__device__ __forceinline__ double bn_tile_n(int64_t t, int64_t count) {
+  const int64_t r = count - t * kBnTile;
+  return (double)(r < kBnTile ? r : kBnTile);
+}
+
+// level 1: tiles [r0, r0 + 256) of the [rows][2][C] partials, 64 channels per block -> (S_b, M2_b)
 __global__ __launch_bounds__(256) void bn_stats_l1(const float* __restrict__ part, int64_t rows, int C,
-                                                   double* __restrict__ out) {
+                                                   int64_t count, double* __restrict__ out) {
   __shared__ double red[2][4][64];
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  __shared__ double mean_b[64];
+  const int l = threadIdx.x & 63, c = blockIdx.y * 64 + l, grp = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * 256;
-  double s = 0.0, q = 0.0;
+  const int64_t r1 = r0 + 256 < rows ? r0 + 256 : rows;
+  double s = 0.0;
   if (c < C)
-    for (int64_t r = r0 + grp; r < r0 + 256 && r < rows; r += 4) {
-      s += (double)part[(r * 2) * C + c];
-      q += (double)part[(r * 2 + 1) * C + c];
+    for (int64_t r = r0 + grp; r < r1; r += 4) s += (double)part[(r * 2) * C + c];
+  red[0][grp][l] = s;
+  __syncthreads();
+  if (grp == 0) {
+    const double n_b = fmin((double)(r1 - r0) * kBnTile, (double)(count - r0 * kBnTile));
+    mean_b[l] = (((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l]) / n_b;
+  }
+  __syncthreads();
+  const double mu = mean_b[l];
+  double q = 0.0;
+  if (c < C)
+    for (int64_t r = r0 + grp; r < r1; r += 4) {
+      const double n_t = bn_tile_n(r, count);
+      const double d = (double)part[(r * 2) * C + c] / n_t - mu;
+      q += (double)part[(r * 2 + 1) * C + c] + n_t * d * d;
     }
-  red[0][grp][threadIdx.x & 63] = s;
-  red[1][grp][threadIdx.x & 63] = q;
+  red[1][grp][l] = q;
   __syncthreads();
   if (grp == 0 && c < C) {
-    const int l = threadIdx.x & 63;
     out[((int64_t)blockIdx.x * 2) * C + c] = ((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l];
     out[((int64_t)blockIdx.x * 2 + 1) * C + c] = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
   }
@@ -503,13 +543,17 @@ __global__ __launch_bounds__(256) void bn_stats_l2(const double* __restrict__ l1
                                                    float* shift, float* rmean, float* rvar) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s += l1[((int64_t)b * 2) * C + c];
-    q += l1[((int64_t)b * 2 + 1) * C + c];
-  }
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += l1[((int64_t)b * 2) * C + c];
   const double mu = s / (double)count;
-  double var = q / (double)count - mu * mu;
+  double m2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {   // block b holds tiles [256 b, 256 b + 256): rows [32768 b, ...)
+    const int64_t rem = count - (int64_t)b * 256 * kBnTile;
+    const double n_b = (double)(rem < 256 * kBnTile ? rem : 256 * kBnTile);
+    const double d = l1[((int64_t)b * 2) * C + c] / n_b - mu;
+    m2 += l1[((int64_t)b * 2 + 1) * C + c] + n_b * d * d;
+  }
+  double var = m2 / (double)count;
   if (var < 0.0) var = 0.0;
   const float rs = (float)(1.0 / sqrt(var + (double)eps));
   mean[c] = (float)mu;
@@ -636,7 +680,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce(int64_t M, int C, const flo
 // a 116-us latency chain per call (r05 rocprof)
 __global__ __launch_bounds__(1024) void bn_bwd_finalize(const double* __restrict__ part, int nblk, int C, int64_t M,
                                                         const float* __restrict__ gamma, const float* __restrict__ rstd,
-                                                        float* dgamma, float* dbeta, float* __restrict__ coef) {
+                                                        float* dgamma, float* dbeta, float* __restrict__ coef,
+                                                        int batch_stats) {
   constexpr int NG = 16;  // thread groups over the partial rows (rows b = grp mod NG, in order)
   __shared__ double red[2][NG][64];
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6, c = blockIdx.x * 64 + l;
@@ -675,8 +720,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize(const double* __restrict
   if (dbeta) dbeta[c] += (float)s;
   const double a = (double)gamma[c] * (double)rstd[c];
   coef[c] = (float)a;
-  coef[C + c] = (float)(a * (s / (double)M));
-  coef[2 * C + c] = (float)(a * (q / (double)M));
+  // batch statistics (training mode): the mean and xhat terms of d(batch mean, batch var); running
+  // statistics (eval mode) are constants, so dy = gamma rstd g
+  coef[C + c] = batch_stats ? (float)(a * (s / (double)M)) : 0.f;
+  coef[2 * C + c] = batch_stats ? (float)(a * (q / (double)M)) : 0.f;
 }
 
 // pass 3: dy = a g - b - c xhat;  dres = g
@@ -981,13 +1028,14 @@ extern "C" int vs_bn3d_stats(int64_t rows, int64_t C, const float* part, int64_t
                              const float* beta, float eps, float momentum, float* mean, float* rstd, float* scale,
                              float* shift, float* running_mean, float* running_var, void* workspace, void* stream) {
   VS_REQUIRE(part && gamma && beta && mean && rstd && scale && shift && workspace, "vs_bn3d_stats: null pointer");
-  VS_REQUIRE(rows > 0 && C > 0 && count > 0 && C % 4 == 0, "vs_bn3d_stats: bad extents");
+  VS_REQUIRE(rows > 0 && C > 0 && count > 0 && C % 4 == 0 && (count + kBnTile - 1) / kBnTile == rows,
+             "vs_bn3d_stats: bad extents (rows = ceil(count / 128) tiles)");
   hipStream_t s = (hipStream_t)stream;
   ScopedTimer timer(VS_TIMER_BN, s, (double)rows * 2.0 * (double)C * 4.0);
   const int64_t nblk = (rows + 255) / 256;
   double* l1 = (double*)workspace;   // level-1 f64 partial sums [nblk][2][C]
   hipLaunchKernelGGL(bn_stats_l1, dim3((unsigned)nblk, (unsigned)((C + 63) / 64)), dim3(256), 0, s, part, rows,
-                     (int)C, l1);
+                     (int)C, count, l1);
   VS_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_stats_l2, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, (const double*)l1, (int)nblk,
                      (int)C, count, gamma, beta, eps, momentum, mean, rstd, scale, shift, running_mean, running_var);
@@ -1036,9 +1084,9 @@ extern "C" size_t vs_bn3d_bwd_workspace_bytes(int64_t M, int64_t C) {
   return (size_t)bn_bwd_blocks(M, C) * 2 * C * 8 + (size_t)3 * C * 4 + 256;
 }
 
-extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
-                           const float* mean, const float* rstd, const float* gamma, float* dy, float* dres,
-                           float* dgamma, float* dbeta, void* workspace, void* stream) {
+static int bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
+                    const float* mean, const float* rstd, const float* gamma, float* dy, float* dres, float* dgamma,
+                    float* dbeta, void* workspace, void* stream, int batch_stats) {
   VS_REQUIRE(dout && y && mean && rstd && gamma && dy && workspace && (!relu || out), "vs_bn3d_bwd: null pointer");
   VS_REQUIRE(C % 4 == 0 && C <= 1024 && aligned16(dout) && aligned16(y) && aligned16(dy) &&
                  (!out || aligned16(out)) && (!dres || aligned16(dres)) && aligned16(workspace),
@@ -1054,7 +1102,7 @@ extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float*
                      rpb, part);
   VS_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((unsigned)((C + 63) / 64)), dim3(1024), 0, s, (const double*)part,
-                     (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef);
+                     (int)nblk, (int)C, M, gamma, rstd, dgamma, dbeta, coef, batch_stats);
   VS_LAUNCH_CHECK();
   const int64_t n4 = M * C / 4;
   const int64_t blocks = bn_ew_blocks(n4, C);
@@ -1063,6 +1111,18 @@ extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float*
                      (float4*)dres);
   VS_LAUNCH_CHECK();
   return VS_OK;
+}
+
+extern "C" int vs_bn3d_bwd(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu, const float* y,
+                           const float* mean, const float* rstd, const float* gamma, float* dy, float* dres,
+                           float* dgamma, float* dbeta, void* workspace, void* stream) {
+  return bn3d_bwd(M, C, dout, out, relu, y, mean, rstd, gamma, dy, dres, dgamma, dbeta, workspace, stream, 1);
+}
+
+extern "C" int vs_bn3d_bwd_eval(int64_t M, int64_t C, const float* dout, const float* out, int32_t relu,
+                                const float* y, const float* mean, const float* rstd, const float* gamma, float* dy,
+                                float* dres, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  return bn3d_bwd(M, C, dout, out, relu, y, mean, rstd, gamma, dy, dres, dgamma, dbeta, workspace, stream, 0);
 }
 
 extern "C" int vs_to_channels_last(int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int64_t Cp, const float* x,

@@ -1654,6 +1654,9 @@ struct G256Map {
   int tiles_n, tiles, per_xcd, nk;  // nk = K / 64 stages per tile
   int dbg;      // VS_DEBUG_KNOBS builds: VS_KNOB_G256_DBG
   int stagger;  // odd-slot workgroups start this many s_sleep(127) (~4 us each) late (VS_KNOB_G256_STAGGER)
+  int ed_ok;    // the early-DMA counted wait may be used: set by the host only when the instance has no
+                // private (scratch) segment, i.e. its epilogue issues exactly `est` vector-memory ops
+                // (a spill would add scratch loads / stores the count does not include)
 };
 
 template <bool BKC, bool P8, uint32_t EF>
@@ -1965,7 +1968,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
         tile_of(s / g.nk, m0, n0);
         (void)n0;
         // exact count only for a full tile (a ragged one skips the stores of all-dead rows) and real stores
-        nst = (m0 + 256 <= e.M && !(dbg & 2)) ? (est < 63 ? est : 63) : 0;
+        nst = (g.ed_ok && m0 + 256 <= e.M && !(dbg & 2)) ? (est < 63 ? est : 63) : 0;
       }
     }
   }
@@ -2534,12 +2537,42 @@ static void launch_bf16_g256_ef(const vs_gemm_desc* d, const G256Map& g, unsigne
   // P8 (8-column epilogue vectors): always with K-contiguous B; with N-contiguous B only for bf16
   // outputs (its transposed B reads conflict 2-way, which the f32 outputs' 16-B quads do not repay:
   // dX fc2 1,603 -> 1,463 us, dX proj 310 -> 281; dX fc1 989 -> 1,011)
+  G256Map gm = g;
+  auto go = [&](auto kern) {
+    // the early-DMA wait counts the epilogue's stores exactly (`est`); an instance that spills to scratch
+    // issues more vector-memory ops than that, so it falls back to vmcnt(0) (checked once per instance)
+    static const int ok = [&] {
+      hipFuncAttributes fa{};
+      return hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.localSizeBytes == 0 ? 1 : 0;
+    }();
+    gm.ed_ok = ok;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, gm, e);
+  };
   if (d->b_kcontig)
-    hipLaunchKernelGGL((gemm_bf16_g256_kernel<true, true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+    go(gemm_bf16_g256_kernel<true, true, EF>);
   else if (e.out_bf16)
-    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, true, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+    go(gemm_bf16_g256_kernel<false, true, EF>);
   else
-    hipLaunchKernelGGL((gemm_bf16_g256_kernel<false, false, EF>), dim3(grid), dim3(512), 0, s, a, d->lda, b, d->ldb, g, e);
+    go(gemm_bf16_g256_kernel<false, false, EF>);
+}
+
+// G256 early-DMA guard, for tests: 1 when every compiled 256 x 256 forward / dX instance has no private
+// segment (the counted vmcnt of the early DMA is then exact), else 0
+template <bool BKC, bool P8>
+static int g256_no_scratch_all() {
+  int ok = 1;
+#define CHK_(EF)                                                                                    \
+  {                                                                                                 \
+    hipFuncAttributes fa{};                                                                          \
+    if (hipFuncGetAttributes(&fa, (const void*)gemm_bf16_g256_kernel<BKC, P8, EF>) != hipSuccess || \
+        fa.localSizeBytes != 0)                                                                     \
+      ok = 0;                                                                                       \
+  }
+  CHK_(0u) CHK_((uint32_t)VS_EPI_BIAS) CHK_((uint32_t)(VS_EPI_BIAS | VS_EPI_RESIDUAL))
+  CHK_((uint32_t)(VS_EPI_BIAS | VS_EPI_GELU)) CHK_((uint32_t)VS_EPI_GELU_BWD)
+  CHK_((uint32_t)(VS_EPI_BIAS | VS_EPI_GELU | VS_EPI_GELU_GRAD)) CHK_((uint32_t)VS_EPI_MUL_AUX)
+#undef CHK_
+  return ok;
 }
 
 // compile-time epilogue variants: the flag sets of the ViT block (vit_exec.hip) and patch embed
@@ -2555,6 +2588,10 @@ static void launch_bf16_g256_ef(const vs_gemm_desc* d, const G256Map& g, unsigne
     case VS_EPI_MUL_AUX: CALL((uint32_t)VS_EPI_MUL_AUX); break;                            \
     default: CALL(kEpiRuntime); break;                                                     \
   }
+
+extern "C" int vs_g256_scratch_free(void) {
+  return g256_no_scratch_all<true, true>() & g256_no_scratch_all<false, true>() & g256_no_scratch_all<false, false>();
+}
 
 static void launch_bf16_g256(const vs_gemm_desc* d, const G256Map& g, unsigned grid, const EpiParams& e,
                              hipStream_t s) {
@@ -2919,6 +2956,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
     g.dbg = 0;
 #endif
     g.stagger = knob(VS_KNOB_G256_STAGGER);
+    g.ed_ok = 1;  // launch_bf16_g256_ef clears it for an instance with a private segment
     count_path(VS_PATH_GEMM_G256);
     launch_bf16_g256(d, g, (unsigned)grid, e, s);
     VS_LAUNCH_CHECK();

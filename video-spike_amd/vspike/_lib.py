@@ -99,6 +99,7 @@ PROTOTYPES = {
     "vs_build_id": (ctypes.c_char_p, []),
     "vs_dispatch_counts": (ctypes.c_int, [ctypes.POINTER(c_i64), ctypes.c_int]),
     "vs_dispatch_reset": (ctypes.c_int, []),
+    "vs_g256_scratch_free": (ctypes.c_int, []),
     "vs_knob_get": (ctypes.c_int, [ctypes.c_int]),
     "vs_knob_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "vs_knob_default": (ctypes.c_int, [ctypes.c_int]),
@@ -179,6 +180,7 @@ PROTOTYPES = {
     "vs_bn3d_apply": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_p]),
     "vs_bn3d_bwd_workspace_bytes": (c_sz, [c_i64, c_i64]),
     "vs_bn3d_bwd": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "vs_bn3d_bwd_eval": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "vs_to_channels_last": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "vs_avgpool3d": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "vs_avgpool3d_bwd": (ctypes.c_int, [c_i64, c_i64, c_i64, c_p, c_p, c_p]),

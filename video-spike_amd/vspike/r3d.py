@@ -114,6 +114,11 @@ class R3DLayout:
         h.add("dec_w", (out_dim, enc_out))
         h.add("dec_b", (out_dim,))
         self.head = h
+        # each conv unit's span of enc_flat (its weight, BN gamma and beta, padding included, up to the
+        # next unit's first slot): the range the data-parallel exchange may reduce once that unit's
+        # backward has run (the spans tile the buffer, so adjacent finished units coalesce)
+        starts = [e.slots[c.name + ".weight"].offset for c in self.convs] + [e.numel]
+        self.unit_span = {c.name: (starts[i], starts[i + 1]) for i, c in enumerate(self.convs)}
         # running statistics (buffers): [mean | var] per BN
         self.bn_off = {}
         off = 0
@@ -180,14 +185,17 @@ def bn3d_apply(y, scale, shift, out, residual=None, relu=True):
                               L.ptr(residual), int(relu), out.data_ptr(), stream()), "vs_bn3d_apply")
 
 
-def bn3d_bwd(dout, out, relu, y, mean, rstd, gamma, dy, dres, dgamma, dbeta):
+def bn3d_bwd(dout, out, relu, y, mean, rstd, gamma, dy, dres, dgamma, dbeta, batch_stats=True):
+    """batch_stats: the forward normalised by the batch statistics (training mode); False: by the
+    running statistics (eval mode), whose backward has no mean / variance terms."""
     C = y.shape[-1]
     M = y.numel() // C
     nb = int(lib().vs_bn3d_bwd_workspace_bytes(M, C))
     ws = torch.empty(nb // 4 + 64, dtype=torch.float32, device=y.device)
-    check(lib().vs_bn3d_bwd(M, C, dout.data_ptr(), L.ptr(out), int(relu), y.data_ptr(), mean.data_ptr(),
-                            rstd.data_ptr(), gamma.data_ptr(), dy.data_ptr(), L.ptr(dres), L.ptr(dgamma),
-                            L.ptr(dbeta), ws.data_ptr(), stream()), "vs_bn3d_bwd")
+    fn = lib().vs_bn3d_bwd if batch_stats else lib().vs_bn3d_bwd_eval
+    check(fn(M, C, dout.data_ptr(), L.ptr(out), int(relu), y.data_ptr(), mean.data_ptr(),
+             rstd.data_ptr(), gamma.data_ptr(), dy.data_ptr(), L.ptr(dres), L.ptr(dgamma),
+             L.ptr(dbeta), ws.data_ptr(), stream()), "vs_bn3d_bwd")
 
 
 def to_channels_last(x, cp=4):
@@ -377,7 +385,7 @@ class R3D(nn.Module):
         bn3d_apply(y, scale, shift, out, residual=residual, relu=relu)
         if save is not None:
             save[c.name] = {"x": x, "y": y, "out": out, "mean": mean, "rstd": rstd, "shape": shape, "d": d,
-                            "relu": relu}
+                            "relu": relu, "batch_stats": bool(self.training)}
         return out, (N, d.Do, d.Ho, d.Wo)
 
     def _run_forward(self, pixels, save_encoder: bool):
@@ -423,8 +431,10 @@ class R3D(nn.Module):
         bn = _bn_name(c.name)
         dy = torch.empty_like(s["y"])
         bn3d_bwd(dout, s["out"], s["relu"], s["y"], s["mean"], s["rstd"], self._bn(c, ".weight"), dy, dres,
-                 G(bn + ".weight"), G(bn + ".bias"))
+                 G(bn + ".weight"), G(bn + ".bias"), batch_stats=s["batch_stats"])
         conv3d_dw(s["d"], s["x"], dy, G(c.name + ".weight"), accumulate=False)
+        if self.grad_sink is not None:      # this unit's weight / gamma / beta gradients are final
+            self.grad_sink.mark_ready(self.enc_flat, *lay.unit_span[c.name])
         if not want_dx:
             return None
         if dx is None:
@@ -476,8 +486,9 @@ class R3D(nn.Module):
                     dx = dres                                                     # identity shortcut
                 d = self._unit_bwd(c1, s1, dh, g_enc, dx=dx, dx_accumulate=True)
         self._unit_bwd(convs["stem.0"], save["stem.0"], d, g_enc, want_dx=False)
-        if self.grad_sink is not None:
-            self.grad_sink.mark_ready(self.enc_flat, 0, self.enc_flat.numel())
+        # (every unit marked its span ready as its backward finished, in reverse order: the exchange
+        # all-reduces each >= bucket-sized run of finished spans while the earlier units' backward runs,
+        # as DDP's reducer does for src/trainer/base.py:150's accelerator.backward)
         return g_enc, g_head
 
 
