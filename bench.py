@@ -353,7 +353,7 @@ def _pmc_lookup(kind):
     (scripts/pmc_attn.sh passes -> scripts/pmc_json.py: SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
     GRBM_GUI_ACTIVE / 8), the executed-MFMA cross-check of the hipEvent roofline."""
     kern = {"attn_fwd": ("attn_fwd_bf16_kernel",),
-            "attn_bwd": ("attn_bwd_bf16_pp_kernel<2, true, true>", "attn_bwd_bf16_kernel")}.get(kind)
+            "attn_bwd": ("attn_bwd_bf16_pp_kernel", "attn_bwd_bf16_kernel")}.get(kind)
     if kern is None:
         return None
     clock = None   # effective clock under the kernel (scripts/attn_clock.py: GRBM cycles / duration)
@@ -371,7 +371,7 @@ def _pmc_lookup(kind):
         try:
             d = json.load(open(f))
             for name, e in d["kernels"].items():
-                if name.endswith(kern) and "mfma_busy_frac" in e:
+                if any(k in name for k in kern) and "mfma_busy_frac" in e:
                     return {**(clock or {}), "mfma_busy_frac": round(e["mfma_busy_frac"], 4), "source": os.path.relpath(f, ROOT),
                             "note": "executed MFMA cycles (the backward's dQ pass recomputes S and dP: 7 products "
                                     "executed for the 5 credited)" if kind == "attn_bwd" else "executed MFMA cycles "
@@ -702,7 +702,10 @@ def c4_subrecord(args, world, rank, dev):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import cpu_ref
         sd = {k: v.detach().cpu() for k, v in model.reference_state_dict().items()}
+        model.keep_relu_masks = True      # the oracle below takes the same ReLU decisions (see cpu_ref)
         out0 = model(pixels)
+        masks = {k: v.cpu() for k, v in model.relu_masks.items()}
+        model.keep_relu_masks, model.relu_masks = False, None
         loss0 = criterion(out0, target)
         loss0.backward()
         lay = model.layout
@@ -728,7 +731,8 @@ def c4_subrecord(args, world, rank, dev):
         # would not say which side is off
         P = {k: v.double().clone().requires_grad_() for k, v in sd.items()
              if not k.endswith(("running_mean", "running_var"))}
-        ref = cpu_ref.r3d18_forward(pixels.cpu().double(), P, ccfg)
+        flips = {}
+        ref = cpu_ref.r3d18_forward(pixels.cpu().double(), P, ccfg, relu_masks=masks, mask_log=flips)
         rloss = cpu_ref.poisson_nll_mean(ref, target.cpu().double())
         rloss.backward()
         e_out = float((gl - ref.detach()).abs().max() / ref.detach().abs().max())
@@ -738,23 +742,31 @@ def c4_subrecord(args, world, rank, dev):
         # torch's own f32 CPU kernels against the same f64 result: the scale of f32 rounding on these
         # strongly cancelling BatchNorm-path gradients (the bars below are relative to it)
         P32 = {k: v.clone().requires_grad_() for k, v in sd.items() if not k.endswith(("running_mean", "running_var"))}
-        cpu_ref.poisson_nll_mean(cpu_ref.r3d18_forward(pixels.cpu(), P32, ccfg), target.cpu()).backward()
+        cpu_ref.poisson_nll_mean(cpu_ref.r3d18_forward(pixels.cpu(), P32, ccfg, relu_masks=masks),
+                                 target.cpu()).backward()
+        nflip = sum(f[0] for f in flips.values())
+        tie = max((f[1] / f[2] for f in flips.values() if f[0]), default=0.0)
+        del masks
         e32 = {k: float((P32[k].grad.double() - P[k].grad.double()).norm() / P[k].grad.double().norm())
                for k in gpu_grads}
         del P32
         worst_conv = max((k for k in errs if not k.endswith((".1.weight", ".1.bias"))), key=errs.get)
         worst_bn = max((k for k in errs if k.endswith((".1.weight", ".1.bias"))), key=errs.get)
         tol = {"log_rates": 1e-4, "loss": 1e-5, "grad_conv_head": 1e-3, "grad_bn_affine": 3e-3,
-               "grad_rule": "a gradient passes at its bar or at 3x torch-f32's distance from f64, the larger"}
+               "grad_rule": "a gradient passes at its bar or at 3x torch-f32's distance from f64, the larger",
+               "relu_tie": 1e-5}
         check = {"what": f"one fwd+bwd of the whole benched batch ({B} clips, training-mode BatchNorm) at the initial "
-                         "weights vs the CPU oracle's R3D-18 restatement run in f64 (oracle/cpu_ref.py r3d18_forward); "
-                         "parity UNPINNED: the reference has no CNN encoder",
+                         "weights vs the CPU oracle's R3D-18 restatement run in f64 (oracle/cpu_ref.py r3d18_forward), "
+                         "conditioned on the plugin's ReLU decisions (the flipped ones must be rounding-level ties: "
+                         "|pre-activation| < relu_tie of the unit's max); parity UNPINNED: the reference has no CNN "
+                         "encoder",
+                 "relu_flips": nflip, "relu_flip_max_rel": tie,
                  "log_rates_maxrel": round(e_out, 8), "loss_rel": round(e_loss, 9),
                  "worst_conv_head_grad": worst_conv, "worst_conv_head_grad_rel": round(errs[worst_conv], 6),
                  "worst_conv_head_grad_torch_f32_rel": round(e32[worst_conv], 6),
                  "worst_bn_grad": worst_bn, "worst_bn_grad_rel": round(errs[worst_bn], 6),
                  "worst_bn_grad_torch_f32_rel": round(e32[worst_bn], 6), "tolerance": tol,
-                 "ok": bool(e_out < tol["log_rates"] and e_loss < tol["loss"] and all(
+                 "ok": bool(e_out < tol["log_rates"] and e_loss < tol["loss"] and tie < tol["relu_tie"] and all(
                      errs[k] <= max(tol["grad_bn_affine"] if k.endswith((".1.weight", ".1.bias"))
                                     else tol["grad_conv_head"], 3.0 * e32[k]) for k in errs)),
                  "cpu_seconds": round(time.perf_counter() - t0, 1)}

@@ -530,10 +530,18 @@ def make_r3d_pixels(cfg: R3DCfg, batch: int, seed: int = 0) -> np.ndarray:
 
 
 def r3d18_forward(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: R3DCfg, running=None,
-                  training: bool = True) -> torch.Tensor:
+                  training: bool = True, relu_masks=None, mask_log=None) -> torch.Tensor:
     """log-rates (B, 100, N): the R3D-18 encoder (training-mode BatchNorm: batch statistics; `running`
     = dict of running_mean / running_var tensors updated in place when given) -> AdaptiveAvgPool3d(1)
-    -> the reference head."""
+    -> the reference head.
+
+    relu_masks (checker option): {conv name: bool tensor (N, D, H, W, C), channels-last} -- the ReLU
+    decisions the implementation under test took.  A pre-activation within rounding of zero can land
+    on either side of the ReLU in two correct f32 / f64 computations, and one flipped element moves a
+    gradient that sums ~10^5 cancelling terms by a whole element; conditioning the oracle on the same
+    discrete decisions (out = pre * mask) leaves only arithmetic differences to compare.  mask_log
+    (a dict) receives per unit the count of flipped decisions and the largest |pre-activation| among
+    them, so a caller can check the flips are only rounding-level ties."""
     import torch.nn.functional as F
     B = pixels.shape[0]
     x = pixels.permute(0, 2, 1, 3, 4)                       # (B, C, T, H, W): torch's NCDHW
@@ -547,6 +555,14 @@ def r3d18_forward(pixels: torch.Tensor, P: Dict[str, torch.Tensor], cfg: R3DCfg,
                          momentum=cfg.bn_momentum, eps=cfg.bn_eps)
         if residual is not None:
             y = y + residual
+        if relu and relu_masks is not None and name in relu_masks:
+            m = relu_masks[name].permute(0, 4, 1, 2, 3).to(y.dtype)
+            if mask_log is not None:
+                with torch.no_grad():
+                    flip = (y.detach() > 0) != (m > 0)
+                    mask_log[name] = (int(flip.sum()), float(y.detach().abs()[flip].max()) if flip.any() else 0.0,
+                                      float(y.detach().abs().max()))
+            return y * m
         return F.relu(y) if relu else y
 
     specs = {s[0]: s for s in r3d_conv_specs(cfg)}

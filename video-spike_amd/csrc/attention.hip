@@ -380,9 +380,15 @@ __device__ __forceinline__ bf16x8 rowsum_selector(int lane) {
 // left the fast pass's band): read / reset by vs_attn_redo_count
 __device__ unsigned long long g_attn_redo = 0;
 
-// SW: QK(b) is issued before PV(a), so softmax(b) waits on a chain that ran under PV(a)'s MFMAs
-template <bool SW = false>
-__global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+// ORD: the order of a 64-key tile's work (blocks a = keys 0..31, b = 32..63)
+//   0: QK(a), softmax(a), PV(a), QK(b), softmax(b), PV(b)                (round 2)
+//   1: QK(b) issued before PV(a), so softmax(b) waits on a chain that ran under PV(a)'s MFMAs (round 3)
+//   2: software-pipelined across tiles: every softmax runs under the NEXT block's QK MFMAs, including
+//      softmax(b) under QK(a) of tile kt + 1 (ORD 1 leaves softmax(b) with only its two row-sum
+//      MFMAs to hide under): per tile  [QK(b) | softmax(a)] [PV(a) | V(b) reads] barrier
+//      [QK(a') | softmax(b)] [PV(b) | V(a'), K(b') reads]  (round 6)
+template <int ORD = 1>
+__global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                bf16_t* __restrict__ o, int64_t ldo,
                                                                float* __restrict__ lse, int N, int H,
                                                                float scale_log2) {
@@ -509,9 +515,12 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
   //  SAFE pass (SAFE = 1): online softmax against a running reference that is raised lazily (a
   //    wave-uniform rare branch when a score exceeds it by 2^kRefBand, guide T13) and is set from
   //    the first block's maximum; p = exp2(s - m); VALU row sums.
-  auto softmax = [&](auto safec, f32x16& acc, int key0, bool first_blk, bf16x8& pa, bf16x8& pb) {
+  // maskc: IC<1> where the block may hold keys past N (the last tile), IC<0> in the pipelined loop's
+  // full tiles (no tail branch there: a branch between QK(b)'s MFMAs and softmax(a)'s VALU splits the
+  // basic block and the in-order wave then issues the two back to back instead of interleaved)
+  auto softmax_m = [&](auto safec, auto maskc, f32x16& acc, int key0, bool first_blk, bf16x8& pa, bf16x8& pb) {
     constexpr bool SAFE = decltype(safec)::value;
-    if (key0 + 32 > N) {
+    if (decltype(maskc)::value && key0 + 32 > N) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) acc[r] = -INFINITY;
@@ -547,6 +556,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
       lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pb, lacc, 0, 0, 0);
     }
   };
+  auto softmax = [&](auto safec, f32x16& acc, int key0, bool first_blk, bf16x8& pa, bf16x8& pb) {
+    softmax_m(safec, IC<1>{}, acc, key0, first_blk, pa, pb);
+  };
 
   // Software pipeline over 64-key tiles (halves a, b).  Fragments are read one phase before their
   // MFMAs; sched_barriers pin the reads where they are issued (left alone, the scheduler sinks each
@@ -573,8 +585,13 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
     __syncthreads();
     if (nkt > 1) load_tile(1, smem1);
     KFrag ka = kread(smem0, 0);
-    auto iter = [&](int kt, auto bufc) {
+    // modec: 2 = runtime tail checks (ORD 0 / 1); ORD 3 peels the last tile: 0 = a full tile with a
+    // successor (no mask, no branch between a QK chain and the softmax it overlaps), 1 = the last tile
+    auto iter = [&](int kt, auto bufc, auto modec) {
       constexpr int BUF = decltype(bufc)::value;
+      constexpr int MODE = decltype(modec)::value;
+      using MaskC = IC<MODE != 0 ? 1 : 0>;
+      const bool has_next = MODE == 2 ? kt + 1 < nkt : MODE == 0;
       char* cur = BUF ? smem1 : smem0;
       const char* nxt = BUF ? smem0 : smem1;
       bf16x8 b0, b1;
@@ -588,10 +605,10 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
         const KFrag kb = kread(cur, 1);
         __builtin_amdgcn_sched_barrier(0);
         bf16x8 a0, a1;
-        softmax(safec, sa, kt * 64, kt == 0, a0, a1);
+        softmax_m(safec, MaskC{}, sa, kt * 64, kt == 0, a0, a1);
         f32x16 sb;
         VFrag vb;
-        if constexpr (SW) {
+        if constexpr (ORD == 1 || ORD == 3) {
           sb = mfma32p(kb.k[0], qf[0], zero16);
 #pragma unroll
           for (int s = 1; s < 4; ++s) sb = mfma32p(kb.k[s], qf[s], sb);
@@ -609,9 +626,9 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
 #pragma unroll
           for (int s = 1; s < 4; ++s) sb = mfma32p(kb.k[s], qf[s], sb);
         }
-        softmax(safec, sb, kt * 64 + 32, false, b0, b1);
+        softmax_m(safec, MaskC{}, sb, kt * 64 + 32, false, b0, b1);
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + 1 < nkt) {
+        if (has_next) {
 #ifdef VS_STAMP
           const unsigned long long c0 = VS_CLK();
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -628,15 +645,99 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16_kernel(const bf16_t* __r
         }
         __builtin_amdgcn_sched_barrier(0);
         pv(vb, b0, b1);
-      } else if (kt + 1 < nkt) {
+      } else if (has_next) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
       }
     };
-    for (int kt = 0; kt < nkt; kt += 2) {
-      iter(kt, IC<0>{});
-      if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+    if constexpr (ORD == 0 || ORD == 1) {
+      for (int kt = 0; kt < nkt; kt += 2) {
+        iter(kt, IC<0>{}, IC<2>{});
+        if (kt + 1 < nkt) iter(kt + 1, IC<1>{}, IC<2>{});
+      }
+    } else if constexpr (ORD == 3) {
+      int kt = 0;
+      for (; kt + 2 < nkt; kt += 2) {
+        iter(kt, IC<0>{}, IC<0>{});
+        iter(kt + 1, IC<1>{}, IC<0>{});
+      }
+      if (kt + 1 < nkt) {
+        iter(kt, IC<0>{}, IC<0>{});
+        iter(kt + 1, IC<1>{}, IC<1>{});
+      } else {
+        iter(kt, IC<0>{}, IC<1>{});
+      }
+    } else {
+      // ORD 2: S(a), V(a) and K(b) of tile kt are in registers when iteration kt starts
+      f32x16 sa_c;
+      VFrag va_c;
+      KFrag kb_c;
+      if (active) {
+        sa_c = mfma32p(ka.k[0], qf[0], zero16);
+#pragma unroll
+        for (int s = 1; s < 4; ++s) sa_c = mfma32p(ka.k[s], qf[s], sa_c);
+        __builtin_amdgcn_sched_barrier(0);
+        va_c = vread(smem0, 0);
+        kb_c = kread(smem0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // LAST: the final tile (its blocks may hold keys past N: masked softmax; no next tile)
+      auto iter2 = [&](int kt, auto bufc, auto lastc) {
+        constexpr int BUF = decltype(bufc)::value;
+        constexpr bool LAST = decltype(lastc)::value;
+        char* cur = BUF ? smem1 : smem0;
+        const char* nxt = BUF ? smem0 : smem1;
+        if (active) {
+          // [QK(b) | softmax(a)]
+          f32x16 sb = mfma32p(kb_c.k[0], qf[0], zero16);
+#pragma unroll
+          for (int s = 1; s < 4; ++s) sb = mfma32p(kb_c.k[s], qf[s], sb);
+          bf16x8 a0, a1;
+          softmax_m(safec, lastc, sa_c, kt * 64, kt == 0, a0, a1);
+          __builtin_amdgcn_sched_barrier(0);
+          // [PV(a) | V(b) reads]
+          const VFrag vb = vread(cur, 1);
+          pv(va_c, a0, a1);
+          __builtin_amdgcn_sched_barrier(0);
+          bf16x8 b0, b1;
+          if constexpr (!LAST) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt+1 landed
+            __syncthreads();                                  // ... every wave's; all reads of `cur` retired
+            if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
+            // [QK(a') | softmax(b)]
+            const KFrag ka2 = kread(nxt, 0);
+            sa_c = mfma32p(ka2.k[0], qf[0], zero16);
+#pragma unroll
+            for (int s = 1; s < 4; ++s) sa_c = mfma32p(ka2.k[s], qf[s], sa_c);
+            softmax_m(safec, IC<0>{}, sb, kt * 64 + 32, false, b0, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            // [PV(b) | V(a'), K(b') reads]
+            va_c = vread(nxt, 0);
+            kb_c = kread(nxt, 1);
+            pv(vb, b0, b1);
+            __builtin_amdgcn_sched_barrier(0);
+          } else {
+            softmax_m(safec, IC<1>{}, sb, kt * 64 + 32, false, b0, b1);
+            pv(vb, b0, b1);
+          }
+        } else if (!LAST) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
+        }
+      };
+      int kt = 0;
+      for (; kt + 2 < nkt; kt += 2) {
+        iter2(kt, IC<0>{}, IC<0>{});
+        iter2(kt + 1, IC<1>{}, IC<0>{});
+      }
+      if (kt + 1 < nkt) {
+        iter2(kt, IC<0>{}, IC<0>{});
+        iter2(kt + 1, IC<1>{}, IC<1>{});
+      } else {
+        iter2(kt, IC<0>{}, IC<1>{});
+      }
     }
   };
 
@@ -1456,8 +1557,230 @@ __device__ __forceinline__ void attn_bwd_dq_pp(char* __restrict__ kv0, char* __r
   }
 }
 
-// PKV / PQ: the pipelined (true) or the 3-wave (false) dK/dV / dQ body
-template <int WPS, bool PKV, bool PQ>
+// ------------------------------------------------------------------ backward: dQ, software-pipelined
+// The 3-wave dQ body runs each 32-key block as [S, dP chains: 8 MFMAs, LDS reads only] then
+// [exp / mul / cvt: 16 v_exp + 24 VALU] + [dQ: 4 MFMAs]: one wave issues the two halves back to back,
+// so its VALU never overlaps its own MFMAs and the block's issue stream is unbalanced (the other
+// waves of the SIMD must fill both gaps).  Here every block's dS work runs under the NEXT block's S /
+// dP MFMAs (round 6; the forward's ORD 2 structure):
+//   per 64-key tile   [S, dP(b) | dS(a)] [dQ(a) | K^T(b) reads] barrier [S, dP(a') | dS(b)]
+//                     [dQ(b) | K, V(b') and K^T(a') reads]
+// Same numerics as attn_bwd_dq_body (the same MFMA chains in the same order: bitwise equal dQ).
+// 2 waves per SIMD (the two blocks' S / dP accumulators are live together: ~230 VGPRs).
+__device__ __forceinline__ void attn_bwd_dq_pl(char* __restrict__ kv0, char* __restrict__ kv1, int blk,
+                                               const bf16_t* __restrict__ qkv, int64_t ldq,
+                                               const bf16_t* __restrict__ dout, int64_t lddo,
+                                               const float* __restrict__ nlse2, const float* __restrict__ ndel,
+                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
+                                               float scale) {
+  constexpr int TILE = 64 * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
+  const int nb128 = (N + 127) / 128, qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const bf16_t* Dp = dout + row0 * lddo + h * 64;
+  const int qi = qb * 128 + wid * 32 + (lane & 31);
+  const float c2 = scale * kLog2e;
+
+  bf16x8 qf[4], df[4];
+  {
+    const int qr = qi < N ? qi : N - 1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c2;
+      qf[s] = __builtin_convertvector(v, bf16x8);
+      df[s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 sinit, dinit, dqacc[2];
+  {
+    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
+    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
+    const float nd = qi < N ? ndel[w] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sinit[r] = nl;
+      dinit[r] = nd;
+      dqacc[0][r] = 0.f;
+      dqacc[1][r] = 0.f;
+    }
+  }
+  int roff[4];
+  {
+    const int key = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
+  }
+  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
+  int toff[2][2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
+    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
+  }
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
+  const uint32_t ko0 = (uint32_t)(prow * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
+  const uint32_t ko1 = (uint32_t)((prow + 8) * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
+  auto load_tile = [&](int kt, char* buf) {
+    const char* kb_ = (const char*)Kp + kt * tile_bytes;
+    char* dk = buf + wid * 2048;
+    char* dv = buf + TILE + wid * 2048;
+    if ((kt + 1) * 64 <= N) {
+      glds16_asm_so(kb_, ko0, dk);
+      glds16_asm_so(kb_, ko1, dk + 1024);
+      glds16_asm_so(kb_ + vdelta, ko0, dv);
+      glds16_asm_so(kb_ + vdelta, ko1, dv + 1024);
+    } else {  // partial last tile: rows past N re-read row N-1 (masked below)
+      const int r0 = kt * 64 + prow < N ? prow : N - 1 - kt * 64;
+      const int r1 = kt * 64 + prow + 8 < N ? prow + 8 : N - 1 - kt * 64;
+      const uint32_t c0 = (uint32_t)(r0 * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
+      const uint32_t c1 = (uint32_t)(r1 * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
+      glds16_asm_so(kb_, c0, dk);
+      glds16_asm_so(kb_, c1, dk + 1024);
+      glds16_asm_so(kb_ + vdelta, c0, dv);
+      glds16_asm_so(kb_ + vdelta, c1, dv + 1024);
+    }
+  };
+  struct Rows {
+    bf16x8 k[4], v[4];
+  };
+  struct KT {
+    bf16x8 f[4];
+  };
+  auto rows = [&](const char* sK, int kb) {
+    Rows r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      r.k[s] = *(const bf16x8*)(sK + kb * 4096 + roff[s]);
+      r.v[s] = *(const bf16x8*)(sK + TILE + kb * 4096 + roff[s]);
+    }
+    return r;
+  };
+  auto ktr = [&](const char* sK, int kb) {
+    KT t;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int o = kb * 4096 + s2 * 2048;
+        t.f[2 * s2 + dt] = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
+      }
+    return t;
+  };
+  auto sdp = [&](const Rows& r, f32x16& sacc, f32x16& dpacc) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sacc = mfma32p(r.k[s], qf[s], s == 0 ? sinit : sacc);
+      dpacc = mfma32p(r.v[s], df[s], s == 0 ? dinit : dpacc);
+    }
+  };
+  // dS = P * (dP - delta), bf16-packed B operands of the two dQ products (keys past N masked where
+  // the block may hold them: the last tile only)
+  auto dsp = [&](auto maskc, f32x16& sacc, const f32x16& dpacc, int key0, bf16x8 (&db)[2]) {
+    if (decltype(maskc)::value && key0 + 32 > N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[r] = -INFINITY;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float ds[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[8 * s2 + r]) * dpacc[8 * s2 + r];
+      db[s2] = pack8f(ds);
+    }
+  };
+  auto dq = [&](const KT& t, const bf16x8 (&db)[2]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) dqacc[dt] = mfma32p(t.f[2 * s2 + dt], db[s2], dqacc[dt]);
+  };
+
+  const int nkt = (N + 63) / 64;
+  load_tile(0, kv0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (nkt > 1) load_tile(1, kv1);
+  f32x16 sA, dA;
+  Rows rB;
+  KT tA;
+  {
+    const Rows rA = rows(kv0, 0);
+    sdp(rA, sA, dA);
+    __builtin_amdgcn_sched_barrier(0);
+    rB = rows(kv0, 1);
+    tA = ktr(kv0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  auto iter = [&](int kt, auto bufc, auto lastc) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool LAST = decltype(lastc)::value;
+    char* cur = BUF ? kv1 : kv0;
+    const char* nxt = BUF ? kv0 : kv1;
+    // [S, dP(b) | dS(a)]
+    f32x16 sB, dB;
+    sdp(rB, sB, dB);
+    bf16x8 dbA[2];
+    dsp(lastc, sA, dA, kt * 64, dbA);
+    __builtin_amdgcn_sched_barrier(0);
+    // [dQ(a) | K^T(b) reads]
+    const KT tB = ktr(cur, 1);
+    dq(tA, dbA);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 dbB[2];
+    if constexpr (!LAST) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt+1 landed
+      __syncthreads();                                  // ... every wave's; every read of `cur` retired
+      if (kt + 2 < nkt && !((VS_ATTN_DIAG & 2) && kt >= 1)) load_tile(kt + 2, cur);
+      // [S, dP(a') | dS(b)]
+      const Rows rA = rows(nxt, 0);
+      sdp(rA, sA, dA);
+      dsp(IC<0>{}, sB, dB, kt * 64 + 32, dbB);
+      __builtin_amdgcn_sched_barrier(0);
+      // [dQ(b) | K, V(b') and K^T(a') reads]
+      rB = rows(nxt, 1);
+      tA = ktr(nxt, 0);
+      dq(tB, dbB);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      dsp(IC<1>{}, sB, dB, kt * 64 + 32, dbB);
+      dq(tB, dbB);
+    }
+  };
+  int kt = 0;
+  for (; kt + 2 < nkt; kt += 2) {
+    iter(kt, IC<0>{}, IC<0>{});
+    iter(kt + 1, IC<1>{}, IC<0>{});
+  }
+  if (kt + 1 < nkt) {
+    iter(kt, IC<0>{}, IC<0>{});
+    iter(kt + 1, IC<1>{}, IC<1>{});
+  } else {
+    iter(kt, IC<0>{}, IC<1>{});
+  }
+  if (qi < N) {
+    bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        *(uint2*)(qrow + d) = pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
+                                    dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale);
+      }
+  }
+}
+
+// PKV: the pipelined pair (true) or the 3-wave (false) dK/dV body; PQ: 0 the 3-wave dQ body, 1 the
+// pipelined pair, 2 the cross-tile software pipeline (attn_bwd_dq_pl)
+template <int WPS, bool PKV, int PQ>
 __global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                     const bf16_t* __restrict__ dout, int64_t lddo,
                                                                     const float* __restrict__ nlse2,
@@ -1474,7 +1797,10 @@ __global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t
     else
       attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
   } else {
-    if constexpr (PQ)
+    if constexpr (PQ == 2)
+      attn_bwd_dq_pl(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
+                     scale);
+    else if constexpr (PQ == 1)
       attn_bwd_dq_pp(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
                      scale);
     else
@@ -1535,7 +1861,12 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     // section 5) were removed.
     const int fv = knob(VS_KNOB_ATTN_VARIANT) & 15;
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
-    auto kern = fv == 6 ? attn_fwd_bf16_kernel<false> : attn_fwd_bf16_kernel<true>;
+    // 7: the cross-tile software pipeline (ORD 2, round 6)
+    // 8: the round-3 order (ORD 1) with the last tile peeled (ORD 3: no tail branch in the steady loop)
+    auto kern = fv == 6   ? attn_fwd_bf16_kernel<0>
+                : fv == 7 ? attn_fwd_bf16_kernel<2>
+                : fv == 8 ? attn_fwd_bf16_kernel<3>
+                          : attn_fwd_bf16_kernel<1>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse, (int)N, (int)H,
                        scale * kLog2e);
   } else if (dtype == VS_F32) {
@@ -1625,9 +1956,19 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
 #endif
     const unsigned g = (unsigned)(cdiv(N, 128) * H * B);  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     if (bv == 6) {
-      hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, true>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
+      hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, 1>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
                          ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
                          (int)npad, scale, (int)g, skip);
+    } else if (bv == 10 || bv == 11) {  // the pipelined dQ body (2 waves / SIMD) beside the 3-wave (10) or the
+                                        // pipelined-pair (11) dK/dV body
+      if (bv == 10)
+        hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, false, 2>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
+                           ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
+                           (int)npad, scale, (int)g, skip);
+      else
+        hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, 2>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
+                           ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
+                           (int)npad, scale, (int)g, skip);
     } else {  // 9: the 3-wave kernel (round-2 default)
       hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                          (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,

@@ -255,6 +255,11 @@ class R3D(nn.Module):
         self.register_buffer("frame_indices", (torch.linspace(0, 1, self.backbone.num_frames) * 119).long(),
                              persistent=False)
         self.grad_sink = None
+        # checker support: when True, every forward leaves its ReLU decisions in `relu_masks`
+        # ({conv name: bool (N, D, H, W, C)}), so a parity check can condition its oracle on them
+        # (oracle/cpu_ref.r3d18_forward relu_masks); off in training
+        self.keep_relu_masks = False
+        self.relu_masks = None
         self.reset_parameters()
 
     @torch.no_grad()
@@ -383,6 +388,8 @@ class R3D(nn.Module):
             torch.sub(beta, mean * scale, out=shift)
         out = torch.empty_like(y)
         bn3d_apply(y, scale, shift, out, residual=residual, relu=relu)
+        if relu and self.keep_relu_masks:
+            self.relu_masks[c.name] = out > 0
         if save is not None:
             save[c.name] = {"x": x, "y": y, "out": out, "mean": mean, "rstd": rstd, "shape": shape, "d": d,
                             "relu": relu, "batch_stats": bool(self.training)}
@@ -393,6 +400,8 @@ class R3D(nn.Module):
         B = pixels.shape[0]
         lay = self.layout
         save = {} if save_encoder else None
+        if self.keep_relu_masks:
+            self.relu_masks = {}
         x = to_channels_last(pixels.view(B, cfg.num_frames, cfg.num_channels, cfg.image_size, cfg.image_size), 4)
         shape = (B, cfg.num_frames, cfg.image_size, cfg.image_size)
         convs = {c.name: c for c in lay.convs}
