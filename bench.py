@@ -317,7 +317,7 @@ def full_batch_parity(ccfg, params, pixels, target, gpu, args, what=None):
         r = r.detach().numpy().reshape(g.shape)
         errs[k] = float(np.linalg.norm((g - r).ravel()) / max(np.linalg.norm(r.ravel()), 1e-30))
     worst = max(errs, key=errs.get) if errs else None
-    tol = PARITY_TOL[args.dtype]
+    tol = getattr(args, "tol", None) or PARITY_TOL[args.dtype]
     if tol is None:   # fp8: the MX-aware reference's bars at the bench geometry (oracle/tolerances.py)
         from oracle.tolerances import FP8_MX12_GRAD, FP8_MX12_LOSS, FP8_MX12_OUT
         tol = {"log_rates": FP8_MX12_OUT, "loss": FP8_MX12_LOSS, "grad": FP8_MX12_GRAD}
@@ -589,6 +589,12 @@ def _oracle_cfg(bb):
                                                          "layer_norm_eps")})
 
 
+# bars of the C3 sub-record's check (bf16, ViT-Base: 12 layers of d = 768, 8 clips' gradients through the
+# 128-clip dispatch): about 2x the values measured on MI355X in r06 (log-rates 5.3e-3, loss 7.7e-5, worst of
+# 186 gradients 8.7e-3, encoder layer 9's key weight); C2's bars at 128 clips of ViT-Tiny are 7e-3 / 1e-4 / 1e-2
+C3_CHECK_TOL = {"log_rates": 1e-2, "loss": 2e-4, "grad": 2e-2}
+
+
 def c3_subrecord(args, world, rank, dev):
     """BASELINE C3 in the same run: ViT-Base/16 (the reference plugin's own width,
     /root/reference/src/model/videomae.py:7,13) at the reference's 128 clips per process
@@ -614,7 +620,7 @@ def c3_subrecord(args, world, rank, dev):
         gpu = {"loss": float(loss0), "log_rates": out0[:nchk].detach().float().cpu(), "grads": _reference_grads(model)}
         model.zero_grad(set_to_none=True)
         del out0, loss0
-        chk_args = argparse.Namespace(dtype="bf16", loss="poisson")
+        chk_args = argparse.Namespace(dtype="bf16", loss="poisson", tol=C3_CHECK_TOL)
         check = full_batch_parity(_oracle_cfg(bb), init, pixels[:nchk].cpu(), target[:nchk].cpu(), gpu, chk_args,
                                   what=f"fwd of the whole benched {B}-clip batch and bwd of the Poisson loss over its first "
                                        f"{nchk} clips, at the benched dispatch and the initial weights (every gradient)")
