@@ -62,10 +62,13 @@ def ref64(qkv, B, N, H):
     return o.view(B * N, D), lse, smax
 
 
+@pytest.mark.parametrize("variant", [0, 8])
 @pytest.mark.parametrize("smax,spiky", [(10.0, False), (30.0, False), (38.0, True), (50.0, False), (60.0, True),
                                         (90.0, False)])
-def test_attention_fast_pass_at_trained_logit_scales(smax, spiky):
+def test_attention_fast_pass_at_trained_logit_scales(knobs, variant, smax, spiky):
+    """variant 8: the 16x16x32-MFMA forward (two queries per lane: its safe pass keeps two references)."""
     from vspike import ops, _lib as L
+    knobs("attn_variant", variant)
     B, N, H = 4, 1568, 3
     qkv = make_qkv(B, N, H, smax, spiky)
     o = torch.empty(B * N, H * 64, dtype=torch.bfloat16, device=DEV)

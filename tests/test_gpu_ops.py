@@ -801,12 +801,12 @@ def _attn_ref(qkv, B, N, H, scale=0.125):
 ATTN_SHAPES = [(1, 100, 1), (2, 196, 2), (1, 1568, 3), (2, 130, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 6])
+@pytest.mark.parametrize("variant", [0, 6, 8])
 @pytest.mark.parametrize("shape", ATTN_SHAPES + [(2, 3136, 1), (1, 1600, 2), (3, 33, 1), (1, 1, 1)])
 def test_attention_fwd_variants(knobs, variant, shape):
     """The bf16 forward kernels (VS_KNOB_ATTN_VARIANT low nibble: 0 = 3 waves/SIMD x 32 rows with
-    QK(b) issued ahead of PV(a); 6 = the same body in the round-2 order) against fp64 on the same
-    bf16 inputs, at tails of
+    QK(b) issued ahead of PV(a); 6 = the same body in the round-2 order; 8 = the same tile on
+    16x16x32 MFMAs) against fp64 on the same bf16 inputs, at tails of
     every kind: N = 1 / 33 / 100 / 130 / 196 (partial 32-key block), 1568 (= 4 x 384 + 32: a
     workgroup with one live q-block), 1600 (partial 64-key tile), 3136 (C5: 98 blocks)."""
     from vspike import ops
@@ -902,7 +902,7 @@ def test_attention_bf16_matches_f32_kernel_on_same_inputs():
     assert rel(l16, l32) < 3e-3
 
 
-@pytest.mark.parametrize("variant", [0, 6])
+@pytest.mark.parametrize("variant", [0, 6, 8])
 def test_attention_rescale_branch_forced(knobs, variant):
     """A huge score late in the sequence forces the online-softmax rescale (guide rule 26)."""
     from vspike import ops
@@ -920,7 +920,7 @@ def test_attention_rescale_branch_forced(knobs, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 6])
+@pytest.mark.parametrize("variant", [0, 6, 8])
 def test_attention_extreme_logits_move_reference(knobs, variant):
     """Queries whose scores all lie far below / above 0 force the forward's softmax reference off
     its default 0 on the first block (m < -32 or > 32 in log2 units), then a late larger score

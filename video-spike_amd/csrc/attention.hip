@@ -386,7 +386,11 @@ __device__ unsigned long long g_attn_redo = 0;
 //   2: software-pipelined across tiles: every softmax runs under the NEXT block's QK MFMAs, including
 //      softmax(b) under QK(a) of tile kt + 1 (ORD 1 leaves softmax(b) with only its two row-sum
 //      MFMAs to hide under): per tile  [QK(b) | softmax(a)] [PV(a) | V(b) reads] barrier
-//      [QK(a') | softmax(b)] [PV(b) | V(a'), K(b') reads]  (round 6)
+//      [QK(a') | softmax(b)] [PV(b) | V(a'), K(b') reads]  (round 6, VS_KNOB_ATTN_VARIANT 7).  Its two
+//      blocks' live state needs ~206 VGPRs: 2 waves per SIMD, measured 9 % SLOWER than ORD 1's 3 waves
+//      (at 3 waves / 168 VGPRs it spills 81); bitwise the same outputs
+//   ORD 1 with the last tile peeled (no tail branch in the steady loop, so QK(b)'s MFMAs and softmax(a)
+//   share one basic block) spilled 52 VGPRs at 168 and was dropped (round 6)
 template <int ORD = 1>
 __global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                bf16_t* __restrict__ o, int64_t ldo,
@@ -585,13 +589,10 @@ __global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(co
     __syncthreads();
     if (nkt > 1) load_tile(1, smem1);
     KFrag ka = kread(smem0, 0);
-    // modec: 2 = runtime tail checks (ORD 0 / 1); ORD 3 peels the last tile: 0 = a full tile with a
-    // successor (no mask, no branch between a QK chain and the softmax it overlaps), 1 = the last tile
-    auto iter = [&](int kt, auto bufc, auto modec) {
+    auto iter = [&](int kt, auto bufc) {
       constexpr int BUF = decltype(bufc)::value;
-      constexpr int MODE = decltype(modec)::value;
-      using MaskC = IC<MODE != 0 ? 1 : 0>;
-      const bool has_next = MODE == 2 ? kt + 1 < nkt : MODE == 0;
+      using MaskC = IC<1>;
+      const bool has_next = kt + 1 < nkt;
       char* cur = BUF ? smem1 : smem0;
       const char* nxt = BUF ? smem0 : smem1;
       bf16x8 b0, b1;
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(co
         softmax_m(safec, MaskC{}, sa, kt * 64, kt == 0, a0, a1);
         f32x16 sb;
         VFrag vb;
-        if constexpr (ORD == 1 || ORD == 3) {
+        if constexpr (ORD == 1) {
           sb = mfma32p(kb.k[0], qf[0], zero16);
 #pragma unroll
           for (int s = 1; s < 4; ++s) sb = mfma32p(kb.k[s], qf[s], sb);
@@ -651,22 +652,10 @@ __global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(co
         if (kt + 2 < nkt && !(VS_ATTN_DIAG & 1)) load_tile(kt + 2, cur);
       }
     };
-    if constexpr (ORD == 0 || ORD == 1) {
+    if constexpr (ORD != 2) {
       for (int kt = 0; kt < nkt; kt += 2) {
-        iter(kt, IC<0>{}, IC<2>{});
-        if (kt + 1 < nkt) iter(kt + 1, IC<1>{}, IC<2>{});
-      }
-    } else if constexpr (ORD == 3) {
-      int kt = 0;
-      for (; kt + 2 < nkt; kt += 2) {
-        iter(kt, IC<0>{}, IC<0>{});
-        iter(kt + 1, IC<1>{}, IC<0>{});
-      }
-      if (kt + 1 < nkt) {
-        iter(kt, IC<0>{}, IC<0>{});
-        iter(kt + 1, IC<1>{}, IC<1>{});
-      } else {
-        iter(kt, IC<0>{}, IC<1>{});
+        iter(kt, IC<0>{});
+        if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
       }
     } else {
       // ORD 2: S(a), V(a) and K(b) of tile kt are in registers when iteration kt starts
@@ -812,6 +801,320 @@ __global__ __launch_bounds__(256, ORD == 2 ? 2 : 3) void attn_fwd_bf16_kernel(co
   (void)t_bar;
   (void)t_begin;
 #endif
+}
+
+// ------------------------------------------------------------------ forward on 16x16x32 MFMAs
+// The same wave tile as attn_fwd_bf16_kernel (32 queries x 64 dims of O, 64-key K/V tiles by LDS-DMA,
+// fast pass with the safe-pass redo) on v_mfma_f32_16x16x32_bf16 (VS_KNOB_ATTN_VARIANT 8, round 6):
+// same MFMA cycles per FLOP in twice the instructions; MI355X_MICROARCH.md "DVFS give-back" item 7
+// measures this shape holding a higher clock on random data.  Lane l = (c, g) = (l & 15, l >> 4):
+//   S^T tile (ks, qt) = K[16 keys] (cQ)^T[16 queries]: A = K rows (key c, dims 8g..8g+7, ds_read_b128),
+//     B = this lane's Q fragment (query qt*16 + c); the lane holds query qt*16+c, keys 16ks + 4g + i;
+//   P (qt) = {p(ks 0)[0..3], p(ks 1)[0..3]} is the B operand of O^T += V^T P^T with k-slot 8g + j <->
+//     key 4g + j (j < 4) or 16 + 4g + j - 4; the V^T A operand (dim c, those keys) is two
+//     ds_read_tr16_b64 of rows 4g..4g+3 and 16+4g..: a 16-lane group reads 4 rows x 16 dims;
+//   row sums: A = all ones, so every lane's 4 accumulators hold its query's sum (no broadcast);
+//   V image swizzle: 16-B chunk ^ 2((row >> 1) & 3): the 16 rows x 32 B of one tr read cover the 64
+//     banks twice (the K image keeps swz_row: 16 rows x 16 B per group, conflict-free).
+// A lane holds two queries (qt = 0, 1): the safe pass keeps two running references and reduces a
+// query's max / sum over its four lanes (xor 16, xor 32).
+__device__ __forceinline__ int swz_v16(int r) { return ((r >> 1) & 3) << 1; }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256, 3) void attn_fwd16_bf16_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
+                                                                bf16_t* __restrict__ o, int64_t ldo,
+                                                                float* __restrict__ lse, int N, int H,
+                                                                float scale_log2) {
+  constexpr int TILE = 64 * 128;
+  __shared__ __attribute__((aligned(16))) char smem0[2 * TILE];
+  __shared__ __attribute__((aligned(16))) char smem1[2 * TILE];
+  __shared__ int redo_flag;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb128 = (N + 127) / 128, blk = xcd_remap(blockIdx.x, gridDim.x), qb = blk % nb128;
+  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
+  const int64_t row0 = (int64_t)b * N;
+  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
+  const bf16_t* Kp = Qp + D;
+  const int q0w = qb * 128 + wid * 32;
+  if (tid == 0) redo_flag = 0;
+
+  bf16x8 qf[2][2];  // [query tile][32-dim chunk]
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0w + qt * 16 + c, qr = qi < N ? qi : N - 1;
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc) {
+      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + dc * 32 + 8 * g);
+      f32x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * scale_log2;
+      qf[qt][dc] = __builtin_convertvector(v, bf16x8);
+    }
+  }
+  const bf16x8 ones = __builtin_convertvector((f32x8){1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f}, bf16x8);
+  f32x4 oacc[4][2], lacc[2];
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  float m_run[2], l_half[2];
+
+  int kbase[2], vbase[4];
+#pragma unroll
+  for (int dc = 0; dc < 2; ++dc) kbase[dc] = c * 128 + (((dc * 4 + g) ^ swz_row(c)) << 4);
+  {
+    const int r = 4 * g + (c >> 2), sw = swz_v16(r);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) vbase[dt] = TILE + r * 128 + (((dt * 2 + ((c & 3) >> 1)) ^ sw) << 4) + (c & 1) * 8;
+  }
+  const int prow0 = wid * 16 + (lane >> 3), ppos = lane & 7;
+  const uint32_t gk0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_row(prow0)) << 4));
+  const uint32_t gk1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_row(prow0 + 8)) << 4));
+  const uint32_t gv0 = (uint32_t)(prow0 * 2 * ldq + ((ppos ^ swz_v16(prow0)) << 4));
+  const uint32_t gv1 = (uint32_t)((prow0 + 8) * 2 * ldq + ((ppos ^ swz_v16(prow0 + 8)) << 4));
+  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
+  auto load_tile = [&](int kt, char* buf) {
+    const char* kb = (const char*)Kp + kt * tile_bytes;
+    const char* vb = kb + vdelta;
+    char* dk = buf + wid * 2048;
+    char* dv = buf + TILE + wid * 2048;
+    if ((kt + 1) * 64 <= N) {
+      glds16_asm_so(kb, gk0, dk);
+      glds16_asm_so(kb, gk1, dk + 1024);
+      glds16_asm_so(vb, gv0, dv);
+      glds16_asm_so(vb, gv1, dv + 1024);
+    } else {
+      const int r0 = kt * 64 + prow0, r1 = r0 + 8;
+      const uint32_t c0 = (uint32_t)((r0 < N ? r0 : N - 1) - kt * 64) * (uint32_t)(2 * ldq);
+      const uint32_t c1 = (uint32_t)((r1 < N ? r1 : N - 1) - kt * 64) * (uint32_t)(2 * ldq);
+      glds16_asm_so(kb, c0 + ((ppos ^ swz_row(prow0)) << 4), dk);
+      glds16_asm_so(kb, c1 + ((ppos ^ swz_row(prow0 + 8)) << 4), dk + 1024);
+      glds16_asm_so(vb, c0 + ((ppos ^ swz_v16(prow0)) << 4), dv);
+      glds16_asm_so(vb, c1 + ((ppos ^ swz_v16(prow0 + 8)) << 4), dv + 1024);
+    }
+  };
+  struct KFrag {
+    bf16x8 k[2][2];  // [16-key subtile][32-dim chunk]
+  };
+  struct VFrag {
+    bf16x8 v[4];  // [16-dim tile]
+  };
+  struct SAcc {
+    f32x4 s[2][2];  // [16-key subtile][query tile]
+  };
+  auto kread = [&](const char* base, int kb) {
+    KFrag f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int dc = 0; dc < 2; ++dc) f.k[ks][dc] = *(const bf16x8*)(base + kb * 4096 + ks * 2048 + kbase[dc]);
+    return f;
+  };
+  auto vread = [&](const char* base, int kb) {
+    VFrag f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) f.v[dt] = tr_pair(base + kb * 4096, vbase[dt], vbase[dt] + 2048);
+    return f;
+  };
+  auto qk_first = [&](const KFrag& f, SAcc& a) { a.s[0][0] = mfma16(f.k[0][0], qf[0][0], zero4); };
+  auto qk_rest = [&](const KFrag& f, SAcc& a) {
+    a.s[0][1] = mfma16(f.k[0][0], qf[1][0], zero4);
+    a.s[1][0] = mfma16(f.k[1][0], qf[0][0], zero4);
+    a.s[1][1] = mfma16(f.k[1][0], qf[1][0], zero4);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) a.s[ks][qt] = mfma16(f.k[ks][1], qf[qt][1], a.s[ks][qt]);
+  };
+  auto pv = [&](const VFrag& f, const bf16x8 (&p)[2]) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = mfma16(f.v[dt], p[qt], oacc[dt][qt]);
+  };
+  auto qmax4 = [&](float v) {  // max over the query's four lanes (c, g = 0..3)
+    v = fmaxf(v, __shfl_xor(v, 16));
+    return fmaxf(v, __shfl_xor(v, 32));
+  };
+  auto softmax = [&](auto safec, SAcc& a, int key0, bool first_blk, bf16x8 (&p)[2]) {
+    constexpr bool SAFE = decltype(safec)::value;
+    if (key0 + 32 > N) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * ks + 4 * g + i >= N) a.s[ks][qt][i] = -INFINITY;
+    }
+    float e[2][2][4];
+    if constexpr (!SAFE) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) e[ks][qt][i] = __builtin_amdgcn_exp2f(a.s[ks][qt][i]);
+    } else {
+      float mx[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        mx[qt] = max3f(max3f(a.s[0][qt][0], a.s[0][qt][1], a.s[0][qt][2]),
+                       max3f(a.s[0][qt][3], a.s[1][qt][0], a.s[1][qt][1]), max3f(a.s[1][qt][2], a.s[1][qt][3], -INFINITY));
+      if (__any(first_blk || mx[0] > m_run[0] + kRefBand || mx[1] > m_run[1] + kRefBand)) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const float mq = qmax4(mx[qt]);
+          const bool move = first_blk || mq > m_run[qt] + kRefBand;
+          const float m_new = move ? mq : m_run[qt];
+          const float alpha = first_blk ? 1.f : __builtin_amdgcn_exp2f(m_run[qt] - m_new);
+          m_run[qt] = m_new;
+          l_half[qt] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) oacc[dt][qt][i] *= alpha;
+        }
+      }
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            e[ks][qt][i] = __builtin_amdgcn_exp2f(a.s[ks][qt][i] - m_run[qt]);
+            sum += e[ks][qt][i];
+          }
+        l_half[qt] += sum;
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const f32x8 v = {e[0][qt][0], e[0][qt][1], e[0][qt][2], e[0][qt][3],
+                       e[1][qt][0], e[1][qt][1], e[1][qt][2], e[1][qt][3]};
+      p[qt] = __builtin_convertvector(v, bf16x8);
+    }
+    if constexpr (!SAFE) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) lacc[qt] = mfma16(ones, p[qt], lacc[qt]);
+    }
+  };
+
+  // the tile order of attn_fwd_bf16_kernel<1>: QK(a) [V(a) reads] | K(b) reads, softmax(a) |
+  // QK(b) | V(b) reads | PV(a) | softmax(b) | vmcnt(0) + barrier, DMA tile kt+2, K(a') reads | PV(b)
+  const int nkt = (N + 63) / 64;
+  const bool active = q0w < N;
+  auto pass = [&](auto safec) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) oacc[dt][qt] = zero4;
+    lacc[0] = zero4;
+    lacc[1] = zero4;
+    m_run[0] = m_run[1] = 0.f;
+    l_half[0] = l_half[1] = 0.f;
+    load_tile(0, smem0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (nkt > 1) load_tile(1, smem1);
+    KFrag ka = kread(smem0, 0);
+    auto iter = [&](int kt, auto bufc) {
+      constexpr int BUF = decltype(bufc)::value;
+      const bool has_next = kt + 1 < nkt;
+      char* cur = BUF ? smem1 : smem0;
+      const char* nxt = BUF ? smem0 : smem1;
+      if (active) {
+        SAcc sa, sb;
+        qk_first(ka, sa);
+        __builtin_amdgcn_sched_barrier(0);
+        const VFrag va = vread(cur, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        qk_rest(ka, sa);
+        const KFrag kb = kread(cur, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 pa[2], pb[2];
+        softmax(safec, sa, kt * 64, kt == 0, pa);
+        qk_first(kb, sb);
+        qk_rest(kb, sb);
+        __builtin_amdgcn_sched_barrier(0);
+        const VFrag vb = vread(cur, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        pv(va, pa);
+        __builtin_amdgcn_sched_barrier(0);
+        softmax(safec, sb, kt * 64 + 32, false, pb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (has_next) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (kt + 2 < nkt) load_tile(kt + 2, cur);
+          ka = kread(nxt, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        pv(vb, pb);
+      } else if (has_next) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 2 < nkt) load_tile(kt + 2, cur);
+      }
+    };
+    for (int kt = 0; kt < nkt; kt += 2) {
+      iter(kt, IC<0>{});
+      if (kt + 1 < nkt) iter(kt + 1, IC<1>{});
+    }
+  };
+
+  pass(IC<0>{});
+  float l[2] = {lacc[0][0], lacc[1][0]};  // every accumulator row holds the query's sum
+  bool ofin = true;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ofin = ofin && __builtin_isfinite(oacc[dt][qt][i]);
+  bool bad = false;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+    bad = bad || (q0w + qt * 16 + c < N && !(l[qt] >= 0x1p-100f && l[qt] <= 0x1p96f && ofin));
+  bad = active && bad;
+  __syncthreads();
+  if (__any(bad) && lane == 0) redo_flag = 1;
+  __syncthreads();
+  if (redo_flag) {
+    if (tid == 0) atomicAdd(&g_attn_redo, 1ull);
+    pass(IC<1>{});
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float v = l_half[qt];
+      v += __shfl_xor(v, 16);
+      l[qt] = v + __shfl_xor(v, 32);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane (c, g) holds query qt*16 + c, dims 16dt + 4g .. +3 -> wave-private LDS rows
+  char* so = (wid < 2 ? smem0 : smem1) + (wid & 1) * 4096;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float inv = 1.f / l[qt];
+    const int qr = qt * 16 + c;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int chunk = dt * 2 + (g >> 1);
+      *(uint2*)(so + qr * 128 + ((chunk ^ (qr & 7)) << 4) + (g & 1) * 8) =
+          pack4(oacc[dt][qt][0] * inv, oacc[dt][qt][1] * inv, oacc[dt][qt][2] * inv, oacc[dt][qt][3] * inv);
+    }
+    if (g == 0 && q0w + qr < N) lse[((int64_t)b * H + h) * N + q0w + qr] = (m_run[qt] + __log2f(l[qt])) * kLn2;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+  for (int pss = 0; pss < 4; ++pss) {
+    const int r = pss * 8 + (lane >> 3), ch = lane & 7;
+    const uint4 v = *(const uint4*)(so + r * 128 + ((ch ^ (r & 7)) << 4));
+    if (q0w + r < N) *(uint4*)(o + (row0 + q0w + r) * ldo + h * 64 + ch * 8) = v;
+  }
 }
 
 // ------------------------------------------------------------------ backward: row constants
@@ -1557,230 +1860,8 @@ __device__ __forceinline__ void attn_bwd_dq_pp(char* __restrict__ kv0, char* __r
   }
 }
 
-// ------------------------------------------------------------------ backward: dQ, software-pipelined
-// The 3-wave dQ body runs each 32-key block as [S, dP chains: 8 MFMAs, LDS reads only] then
-// [exp / mul / cvt: 16 v_exp + 24 VALU] + [dQ: 4 MFMAs]: one wave issues the two halves back to back,
-// so its VALU never overlaps its own MFMAs and the block's issue stream is unbalanced (the other
-// waves of the SIMD must fill both gaps).  Here every block's dS work runs under the NEXT block's S /
-// dP MFMAs (round 6; the forward's ORD 2 structure):
-//   per 64-key tile   [S, dP(b) | dS(a)] [dQ(a) | K^T(b) reads] barrier [S, dP(a') | dS(b)]
-//                     [dQ(b) | K, V(b') and K^T(a') reads]
-// Same numerics as attn_bwd_dq_body (the same MFMA chains in the same order: bitwise equal dQ).
-// 2 waves per SIMD (the two blocks' S / dP accumulators are live together: ~230 VGPRs).
-__device__ __forceinline__ void attn_bwd_dq_pl(char* __restrict__ kv0, char* __restrict__ kv1, int blk,
-                                               const bf16_t* __restrict__ qkv, int64_t ldq,
-                                               const bf16_t* __restrict__ dout, int64_t lddo,
-                                               const float* __restrict__ nlse2, const float* __restrict__ ndel,
-                                               bf16_t* __restrict__ dqkv, int64_t ldd, int N, int H, int Npad,
-                                               float scale) {
-  constexpr int TILE = 64 * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), hh = lane >> 5;
-  const int nb128 = (N + 127) / 128, qb = blk % nb128;
-  const int h = (blk / nb128) % H, b = blk / nb128 / H, D = H * 64;
-  const int64_t row0 = (int64_t)b * N;
-  const bf16_t* Qp = qkv + row0 * ldq + h * 64;
-  const bf16_t* Kp = Qp + D;
-  const bf16_t* Dp = dout + row0 * lddo + h * 64;
-  const int qi = qb * 128 + wid * 32 + (lane & 31);
-  const float c2 = scale * kLog2e;
-
-  bf16x8 qf[4], df[4];
-  {
-    const int qr = qi < N ? qi : N - 1;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 q = *(const bf16x8*)(Qp + (int64_t)qr * ldq + 16 * s + 8 * hh);
-      f32x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (float)q[j] * c2;
-      qf[s] = __builtin_convertvector(v, bf16x8);
-      df[s] = *(const bf16x8*)(Dp + (int64_t)qr * lddo + 16 * s + 8 * hh);
-    }
-  }
-  f32x16 sinit, dinit, dqacc[2];
-  {
-    const int64_t w = ((int64_t)b * H + h) * Npad + qi;
-    const float nl = qi < N ? nlse2[w] : -INFINITY;  // a padded query: p = 0
-    const float nd = qi < N ? ndel[w] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sinit[r] = nl;
-      dinit[r] = nd;
-      dqacc[0][r] = 0.f;
-      dqacc[1][r] = 0.f;
-    }
-  }
-  int roff[4];
-  {
-    const int key = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) roff[s] = key * 128 + (((2 * s + hh) ^ swz_rt(key)) << 4);
-  }
-  const int q4 = (lane & 15) >> 2, p4 = (lane & 3) * 4, g16 = ((lane >> 4) & 1) * 16, kt0 = 4 * hh + q4;
-  int toff[2][2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    toff[dt][0] = off_rtswz(kt0, dt * 32 + g16 + p4);
-    toff[dt][1] = off_rtswz(kt0 + 8, dt * 32 + g16 + p4);
-  }
-  const int64_t tile_bytes = 64 * 2 * ldq, vdelta = 2 * (int64_t)D;
-  const int prow = wid * 16 + (lane >> 3), ppos = lane & 7;
-  const uint32_t ko0 = (uint32_t)(prow * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
-  const uint32_t ko1 = (uint32_t)((prow + 8) * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
-  auto load_tile = [&](int kt, char* buf) {
-    const char* kb_ = (const char*)Kp + kt * tile_bytes;
-    char* dk = buf + wid * 2048;
-    char* dv = buf + TILE + wid * 2048;
-    if ((kt + 1) * 64 <= N) {
-      glds16_asm_so(kb_, ko0, dk);
-      glds16_asm_so(kb_, ko1, dk + 1024);
-      glds16_asm_so(kb_ + vdelta, ko0, dv);
-      glds16_asm_so(kb_ + vdelta, ko1, dv + 1024);
-    } else {  // partial last tile: rows past N re-read row N-1 (masked below)
-      const int r0 = kt * 64 + prow < N ? prow : N - 1 - kt * 64;
-      const int r1 = kt * 64 + prow + 8 < N ? prow + 8 : N - 1 - kt * 64;
-      const uint32_t c0 = (uint32_t)(r0 * 2 * ldq + ((ppos ^ swz_rt(prow)) << 4));
-      const uint32_t c1 = (uint32_t)(r1 * 2 * ldq + ((ppos ^ swz_rt(prow + 8)) << 4));
-      glds16_asm_so(kb_, c0, dk);
-      glds16_asm_so(kb_, c1, dk + 1024);
-      glds16_asm_so(kb_ + vdelta, c0, dv);
-      glds16_asm_so(kb_ + vdelta, c1, dv + 1024);
-    }
-  };
-  struct Rows {
-    bf16x8 k[4], v[4];
-  };
-  struct KT {
-    bf16x8 f[4];
-  };
-  auto rows = [&](const char* sK, int kb) {
-    Rows r;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      r.k[s] = *(const bf16x8*)(sK + kb * 4096 + roff[s]);
-      r.v[s] = *(const bf16x8*)(sK + TILE + kb * 4096 + roff[s]);
-    }
-    return r;
-  };
-  auto ktr = [&](const char* sK, int kb) {
-    KT t;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int o = kb * 4096 + s2 * 2048;
-        t.f[2 * s2 + dt] = tr_pair(sK, o + toff[dt][0], o + toff[dt][1]);
-      }
-    return t;
-  };
-  auto sdp = [&](const Rows& r, f32x16& sacc, f32x16& dpacc) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sacc = mfma32p(r.k[s], qf[s], s == 0 ? sinit : sacc);
-      dpacc = mfma32p(r.v[s], df[s], s == 0 ? dinit : dpacc);
-    }
-  };
-  // dS = P * (dP - delta), bf16-packed B operands of the two dQ products (keys past N masked where
-  // the block may hold them: the last tile only)
-  auto dsp = [&](auto maskc, f32x16& sacc, const f32x16& dpacc, int key0, bf16x8 (&db)[2]) {
-    if (decltype(maskc)::value && key0 + 32 > N) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (key0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= N) sacc[r] = -INFINITY;
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float ds[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[8 * s2 + r]) * dpacc[8 * s2 + r];
-      db[s2] = pack8f(ds);
-    }
-  };
-  auto dq = [&](const KT& t, const bf16x8 (&db)[2]) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) dqacc[dt] = mfma32p(t.f[2 * s2 + dt], db[s2], dqacc[dt]);
-  };
-
-  const int nkt = (N + 63) / 64;
-  load_tile(0, kv0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (nkt > 1) load_tile(1, kv1);
-  f32x16 sA, dA;
-  Rows rB;
-  KT tA;
-  {
-    const Rows rA = rows(kv0, 0);
-    sdp(rA, sA, dA);
-    __builtin_amdgcn_sched_barrier(0);
-    rB = rows(kv0, 1);
-    tA = ktr(kv0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  auto iter = [&](int kt, auto bufc, auto lastc) {
-    constexpr int BUF = decltype(bufc)::value;
-    constexpr bool LAST = decltype(lastc)::value;
-    char* cur = BUF ? kv1 : kv0;
-    const char* nxt = BUF ? kv0 : kv1;
-    // [S, dP(b) | dS(a)]
-    f32x16 sB, dB;
-    sdp(rB, sB, dB);
-    bf16x8 dbA[2];
-    dsp(lastc, sA, dA, kt * 64, dbA);
-    __builtin_amdgcn_sched_barrier(0);
-    // [dQ(a) | K^T(b) reads]
-    const KT tB = ktr(cur, 1);
-    dq(tA, dbA);
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 dbB[2];
-    if constexpr (!LAST) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces of tile kt+1 landed
-      __syncthreads();                                  // ... every wave's; every read of `cur` retired
-      if (kt + 2 < nkt && !((VS_ATTN_DIAG & 2) && kt >= 1)) load_tile(kt + 2, cur);
-      // [S, dP(a') | dS(b)]
-      const Rows rA = rows(nxt, 0);
-      sdp(rA, sA, dA);
-      dsp(IC<0>{}, sB, dB, kt * 64 + 32, dbB);
-      __builtin_amdgcn_sched_barrier(0);
-      // [dQ(b) | K, V(b') and K^T(a') reads]
-      rB = rows(nxt, 1);
-      tA = ktr(nxt, 0);
-      dq(tB, dbB);
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      dsp(IC<1>{}, sB, dB, kt * 64 + 32, dbB);
-      dq(tB, dbB);
-    }
-  };
-  int kt = 0;
-  for (; kt + 2 < nkt; kt += 2) {
-    iter(kt, IC<0>{}, IC<0>{});
-    iter(kt + 1, IC<1>{}, IC<0>{});
-  }
-  if (kt + 1 < nkt) {
-    iter(kt, IC<0>{}, IC<0>{});
-    iter(kt + 1, IC<1>{}, IC<1>{});
-  } else {
-    iter(kt, IC<0>{}, IC<1>{});
-  }
-  if (qi < N) {
-    bf16_t* qrow = dqkv + (row0 + qi) * ldd + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
-        *(uint2*)(qrow + d) = pack4(dqacc[dt][4 * g] * scale, dqacc[dt][4 * g + 1] * scale,
-                                    dqacc[dt][4 * g + 2] * scale, dqacc[dt][4 * g + 3] * scale);
-      }
-  }
-}
-
-// PKV: the pipelined pair (true) or the 3-wave (false) dK/dV body; PQ: 0 the 3-wave dQ body, 1 the
-// pipelined pair, 2 the cross-tile software pipeline (attn_bwd_dq_pl)
-template <int WPS, bool PKV, int PQ>
+// PKV / PQ: the pipelined pair (true) or the 3-wave (false) dK/dV / dQ body
+template <int WPS, bool PKV, bool PQ>
 __global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t* __restrict__ qkv, int64_t ldq,
                                                                     const bf16_t* __restrict__ dout, int64_t lddo,
                                                                     const float* __restrict__ nlse2,
@@ -1797,10 +1878,7 @@ __global__ __launch_bounds__(256, WPS) void attn_bwd_bf16_pp_kernel(const bf16_t
     else
       attn_bwd_dkdv_body(st0, st1, xcd_remap(id, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad, scale);
   } else {
-    if constexpr (PQ == 2)
-      attn_bwd_dq_pl(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
-                     scale);
-    else if constexpr (PQ == 1)
+    if constexpr (PQ)
       attn_bwd_dq_pp(st0, st1, xcd_remap(id - nblk, nblk), qkv, ldq, dout, lddo, nlse2, ndel, dqkv, ldd, N, H, Npad,
                      scale);
     else
@@ -1862,10 +1940,11 @@ extern "C" int vs_attn_fwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
     const int fv = knob(VS_KNOB_ATTN_VARIANT) & 15;
     dim3 grid((unsigned)(cdiv(N, 128) * H * B));  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     // 7: the cross-tile software pipeline (ORD 2, round 6)
-    // 8: the round-3 order (ORD 1) with the last tile peeled (ORD 3: no tail branch in the steady loop)
+    // (round-6 A/B, profiles/r06_attn_ab_c2.json: 283.6 vs 260.7 us at C2, 1,100 vs 1,019 at C3 -- slower)
+    // 8: the 16x16x32-MFMA forward (round 6)
     auto kern = fv == 6   ? attn_fwd_bf16_kernel<0>
                 : fv == 7 ? attn_fwd_bf16_kernel<2>
-                : fv == 8 ? attn_fwd_bf16_kernel<3>
+                : fv == 8 ? attn_fwd16_bf16_kernel
                           : attn_fwd_bf16_kernel<1>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv, (bf16_t*)o, ld_o, lse, (int)N, (int)H,
                        scale * kLog2e);
@@ -1956,19 +2035,9 @@ extern "C" int vs_attn_bwd(int32_t dtype, int64_t B, int64_t N, int64_t H, int64
 #endif
     const unsigned g = (unsigned)(cdiv(N, 128) * H * B);  // 1D: xcd_remap groups a (b, h)'s blocks on one XCD
     if (bv == 6) {
-      hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, 1>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
+      hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, true>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
                          ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
                          (int)npad, scale, (int)g, skip);
-    } else if (bv == 10 || bv == 11) {  // the pipelined dQ body (2 waves / SIMD) beside the 3-wave (10) or the
-                                        // pipelined-pair (11) dK/dV body
-      if (bv == 10)
-        hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, false, 2>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
-                           ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
-                           (int)npad, scale, (int)g, skip);
-      else
-        hipLaunchKernelGGL((attn_bwd_bf16_pp_kernel<2, true, 2>), dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv,
-                           ld_qkv, (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H,
-                           (int)npad, scale, (int)g, skip);
     } else {  // 9: the 3-wave kernel (round-2 default)
       hipLaunchKernelGGL(attn_bwd_bf16_kernel, dim3(2 * g), dim3(256), 0, s, (const bf16_t*)qkv, ld_qkv,
                          (const bf16_t*)dout, ld_do, nlse2, ndel, (bf16_t*)dqkv, ld_dqkv, (int)N, (int)H, (int)npad,

@@ -276,8 +276,14 @@ struct ConvDw {
 // BKK = 64 or 128 k columns per tile: the wider tile reads the dy slab (the tile's A operand) half as
 // often (the dy of one voxel row slab is re-read by every k tile of the product) but measured slower:
 // 64 is the default (VS_KNOB_CONV_DW128)
-template <int BKK>
+// M32 (BKK = 64 only, VS_KNOB_CONV_MFMA = 1): v_mfma_f32_32x32x2_f32 on each wave's 32 x 32 output block
+// instead of four v_mfma_f32_16x16x4_f32: the same MACs and operand reads (one A and one B dword per lane
+// per 2 k) with half the MFMA instructions (half the issue slots the matrix pipe takes from the gather's
+// VALU / LDS work).  Measured SLOWER at C4 (conv dW 37.3 vs 32.5 ms/step, profiles/r06_r3d_ab_mfma.json:
+// one dependent 64-cycle accumulation chain per wave instead of four independent 32-cycle ones)
+template <int BKK, bool M32 = false>
 __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
+  static_assert(!M32 || BKK == 64, "M32: one 32 x 32 block per wave");
   constexpr int BO = 64, BM = 32, LDO = 80, LD = BKK + 16;   // row strides % 32 == 16: conflict-free b32 reads
   constexpr int SO = BM * LDO, STAGE = SO + BM * LD;
   constexpr int KCH = BKK / 4, XR = 256 / KCH, XS = BM / XR;  // x gather: float4 chunks per row, rows per pass, passes
@@ -390,6 +396,9 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = tot[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x16 acc32, tot32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc32[r] = tot32[r] = 0.f;
   float4 rd[2], rx[XS];
   if (nsteps > 0) {
     load(rd, rx, 0);
@@ -405,6 +414,37 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     // 4 values right before its 4 MFMAs (hipcc's choice, reusing 4 registers) serialised every
     // sub-step behind an LDS round trip (conv dW 34.0 -> 32.5 ms/step at C4; the same change in
     // conv_igemm_kernel, 146 VGPRs, measured slower: fwd 25.1 -> 26.2, dX 26.0 -> 26.9)
+    if constexpr (M32) {
+      // 16 two-row sub-steps: A = dy^T (o = lane & 31, m = 2 sub + lane / 32), B = the gather (k = lane & 31)
+      constexpr int NS2 = BM / 2, HS2 = NS2 / 2;
+      float a2[NS2], b2[NS2];
+      auto rd2 = [&](int sub) {
+        const int mrow = 2 * sub + (lane >> 5);
+        a2[sub] = sd_[mrow * LDO + wr * 32 + (lane & 31)];
+        b2[sub] = sx[mrow * LD + wc * 32 + (lane & 31)];
+      };
+#pragma unroll
+      for (int sub = 0; sub < HS2; ++sub) rd2(sub);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = HS2; sub < NS2; ++sub) rd2(sub);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = 0; sub < HS2; ++sub) acc32 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sub], b2[sub], acc32, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = HS2; sub < NS2; ++sub) acc32 = __builtin_amdgcn_mfma_f32_32x32x2f32(a2[sub], b2[sub], acc32, 0, 0, 0);
+      if (more) store(smem + ((t + 1) & 1) * STAGE, rd, rx);
+      if ((t & 15) == 15) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          tot32[r] += acc32[r];
+          acc32[r] = 0.f;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     constexpr int NS = BM / 4, HS = NS / 2;
     float af[NS][2], bfr[NS][NJ];
     auto rd_ops = [&](int sub) {
@@ -450,6 +490,16 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     for (int j = 0; j < NJ; ++j) acc[i][j] += tot[i][j];
   // partial tile (plain stores; the reduce adds the splits in order)
   float* pt = g.part + (int64_t)split * g.Co * g.Kp;
+  if constexpr (M32) {
+    // 32 x 32 accumulator layout: register r = row 8 (r / 4) + 4 (lane / 32) + r % 4, column lane & 31
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o0 + wr * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+      const int kk = k0 + wc * 32 + (lane & 31);
+      pt[(int64_t)o * g.Kp + kk] = acc32[r] + tot32[r];
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1010,8 +1060,11 @@ extern "C" int vs_conv3d_dw(const vs_conv3d_desc* d, const float* x, const float
   g.M = M; g.splits = p.splits; g.steps_per_split = p.sps; g.part = (float*)workspace; g.Kp = p.Kp;
   count_path(VS_PATH_CONV_DW);
   const int64_t nwg = (int64_t)p.splits * p.tiles_o * p.tiles_k;
-  if (p.bkk == 128) hipLaunchKernelGGL(conv_dw_kernel<128>, dim3((unsigned)nwg), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(conv_dw_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, s, g);
+  if (p.bkk == 128) hipLaunchKernelGGL((conv_dw_kernel<128, false>), dim3((unsigned)nwg), dim3(256), 0, s, g);
+  else if (knob(VS_KNOB_CONV_MFMA) == 1)   // 32x32x2: measured slower (conv dW 37.3 vs 32.5 ms/step, r06)
+    hipLaunchKernelGGL((conv_dw_kernel<64, true>), dim3((unsigned)nwg), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((conv_dw_kernel<64, false>), dim3((unsigned)nwg), dim3(256), 0, s, g);
   VS_LAUNCH_CHECK();
   const int64_t n = d->Co * (int64_t)g.K;
   hipLaunchKernelGGL(conv_dw_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)workspace,
