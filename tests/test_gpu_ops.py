@@ -284,7 +284,7 @@ def test_gemm_w_resident_path(knobs, bkc, shape, epi, wv):
         assert (pre.float() - pre2.float()).abs().max() <= 1e-2 * pre2.float().abs().max()
 
 
-@pytest.mark.parametrize("kernel", ["big", "g256"])
+@pytest.mark.parametrize("kernel", ["big", "g256", "g256a3"])
 @pytest.mark.parametrize("bkc", [True, False])
 @pytest.mark.parametrize("shape,epi", [((25088, 3072, 768), "gelu"), ((25088, 768, 3072), "bias_res"),
                                        ((4100, 512, 512), "bias"), ((8192, 2304, 768), "none"),
@@ -301,11 +301,12 @@ def test_gemm_big_tile_path(bkc, shape, epi, kernel, knobs):
     outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (GELU' 1.5e-2, against a bf16 pre-activation)."""
     from vspike import ops, _lib as L
     M, N, K = shape
-    if kernel == "g256" and (M < 16384 or N % 256 or K % 64 or K < 256):
+    if kernel != "big" and (M < 16384 or N % 256 or K % 64 or K < 256):
         pytest.skip("the 256 x 256 kernel takes M >= 16,384, N % 256 == 0, K % 64 == 0")
     if kernel == "big" and (K < 512 or N % 128):
         pytest.skip("the big-tile kernel takes K >= 512, N % 128 == 0")
-    knobs("g256", 1 if kernel == "g256" else 2)
+    knobs("g256", 2 if kernel == "big" else 1)
+    knobs("g256_a3", 1 if kernel == "g256a3" else 2)    # g256a3: A in three LDS slots (VS_KNOB_G256_A3)
     L.dispatch_reset()
     x = _rand(M, K, seed=51).to(torch.bfloat16).to(DEV)
     w = _rand(N, K, seed=52, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
@@ -353,7 +354,7 @@ def test_gemm_big_tile_path(bkc, shape, epi, kernel, knobs):
         gg = torch.autograd.grad(torch.nn.functional.gelu(xp).sum(), xp)[0]
         ref, tol = ref * gg, 1.5e-2
     torch.cuda.synchronize()
-    assert L.dispatch_counts()["gemm_" + kernel] == 1, L.dispatch_counts()
+    assert L.dispatch_counts()["gemm_big" if kernel == "big" else "gemm_g256"] == 1, L.dispatch_counts()
     assert rel(out.float(), ref) < tol
 
 
@@ -369,7 +370,7 @@ C3_PRODUCTS = {
 }
 
 
-@pytest.mark.parametrize("kernel", ["big", "g256"])
+@pytest.mark.parametrize("kernel", ["big", "g256", "g256a3"])
 @pytest.mark.parametrize("prod", sorted(C3_PRODUCTS))
 def test_gemm_big_tile_c3_bench128(prod, kernel, knobs):
     """Every C3 block product at its benched size (200,704 rows: VERDICT r4 item 1) on the big-tile
@@ -378,9 +379,10 @@ def test_gemm_big_tile_c3_bench128(prod, kernel, knobs):
     outputs 1e-5 of max|ref|, bf16 outputs 8e-3 (one bf16 rounding)."""
     from vspike import ops, _lib as L
     (N, K), bkc, epi = C3_PRODUCTS[prod]
-    if kernel == "g256" and epi == "bias_pos":
+    if kernel != "big" and epi == "bias_pos":
         pytest.skip("the 256 x 256 kernel has no position-table epilogue (the patch embedding stays on the big tile)")
-    knobs("g256", 1 if kernel == "g256" else 2)
+    knobs("g256", 2 if kernel == "big" else 1)
+    knobs("g256_a3", 1 if kernel == "g256a3" else 2)
     M = 200704
     g = torch.Generator(device=DEV).manual_seed(N + 7 * K)
     x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
@@ -432,7 +434,7 @@ def test_gemm_big_tile_c3_bench128(prod, kernel, knobs):
         ops.gemm(x, b_dev, out, epilogue=L.EPI_MUL_AUX, aux_in=aux, ld_aux_in=N, **kw)
         ref, tol = ref.mul_(aux.double()), 8e-3
     torch.cuda.synchronize()
-    assert L.dispatch_counts()["gemm_" + kernel] == 1, L.dispatch_counts()
+    assert L.dispatch_counts()["gemm_big" if kernel == "big" else "gemm_g256"] == 1, L.dispatch_counts()
     err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
     print(f"\n[{prod}] M={M} N={N} K={K} max err / max|ref| = {err:.3e}")
     assert err < tol

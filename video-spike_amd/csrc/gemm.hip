@@ -1657,6 +1657,8 @@ struct G256Map {
   int ed_ok;    // the early-DMA counted wait may be used: set by the host only when the instance has no
                 // private (scratch) segment, i.e. its epilogue issues exactly `est` vector-memory ops
                 // (a spill would add scratch loads / stores the count does not include)
+  int a3;       // A (the streamed token-row operand) in THREE 32-KB slots, B in two: A's DMA is issued two
+                // stages ahead and the stage wait is counted (vmcnt(4 + stores)), never 0 (VS_KNOB_G256_A3)
 };
 
 template <bool BKC, bool P8, uint32_t EF>
@@ -1664,8 +1666,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ B, int64_t ldb,
                                                                 G256Map g, EpiParams e) {
   static_assert(!BKC || P8, "K-contiguous B fragments are always column-permuted (8-column vectors)");
-  constexpr int AB = 256 * 64 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int AB = 256 * 64 * 2, STAGE = 2 * AB;  // 2 slots x 64 KB (a3: A 3 x 32 KB + B 2 x 32 KB)
+  __shared__ __attribute__((aligned(16))) char smem[5 * AB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 2, wc = wid & 3;
   // this workgroup's tiles: XCD x = blockIdx % 8 owns logical tiles [x * per_xcd, (x+1) * per_xcd)
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, slots = gridDim.x >> 3;
@@ -1707,28 +1709,49 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
       b_off[p] = (uint32_t)(k * ldb * 2 + ((((lane & 31) ^ swz_mc<128>(k))) << 4));
     }
   }
-  auto issue = [&](int s) __attribute__((always_inline)) {
+  // stage s's images: A at a_slot(s), B at b_slot(s) + AB (the B read offsets include + AB)
+  const bool a3 = g.a3 != 0;
+  auto a_slot = [&](int s) __attribute__((always_inline)) -> char* {
+    return a3 ? smem + (s % 3) * AB : smem + (s & 1) * STAGE;
+  };
+  auto b_slot = [&](int s) __attribute__((always_inline)) -> char* {
+    return a3 ? smem + 2 * AB + (s & 1) * AB : smem + (s & 1) * STAGE;
+  };
+  auto issue_a = [&](int s, int p0 = 0, int p1 = 4) __attribute__((always_inline)) {  // pieces [p0, p1)
     if (dbg & 1) return;
     const int k = s / g.nk, t = s - k * g.nk;
     int m0, n0;
     tile_of(k, m0, n0);
-    char* st = smem + (s & 1) * STAGE + wid * 4096;
+    (void)n0;
+    char* st = a_slot(s) + wid * 4096;
     const int64_t mrows = e.M - m0;  // rows past M re-read row M-1 (never stored)
     const char* abase = sgpr_ptr((const char*)(A + (int64_t)m0 * lda + (int64_t)t * 64));
     if (mrows >= 256) {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
+      for (int p = p0; p < p1; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
     } else {
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = p0; p < p1; ++p) {
         const int r = wid * 32 + p * 8 + (lane >> 3), rc = r < mrows ? r : (int)mrows - 1;
         glds16_asm_so(abase, (uint32_t)(rc * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4)), st + p * 1024);
       }
     }
+  };
+  auto issue_b = [&](int s) __attribute__((always_inline)) {
+    if (dbg & 1) return;
+    const int k = s / g.nk, t = s - k * g.nk;
+    int m0, n0;
+    tile_of(k, m0, n0);
+    (void)m0;
+    char* st = b_slot(s) + wid * 4096;
     const char* bbase = sgpr_ptr(BKC ? (const char*)(B + (int64_t)n0 * ldb + (int64_t)t * 64)
                                      : (const char*)(B + (int64_t)t * 64 * ldb + n0));
 #pragma unroll
     for (int p = 0; p < 4; ++p) glds16_asm_so(bbase, b_off[p], st + AB + p * 1024);
+  };
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    issue_a(s);
+    issue_b(s);
   };
 
   // ---- fragments (per lane, stage-invariant byte offsets; kk = 32-deep half of the stage)
@@ -1905,11 +1928,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   // prologue: stage 0 landed, its first fragments in registers
   bf16x8 a0[4], a1[4], b0[4], b1[4];
   issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a3 && total > 1) {
+    issue_a(1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A(0), B(0) landed; A(1) in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  read_b(smem, 0, b0);
-  read_a(smem, 0, 0, a0);
+  read_b(b_slot(0), 0, b0);
+  read_a(a_slot(0), 0, 0, a0);
 
   // Stage s (slot s & 1), four phases; fragments of the next phase are read before this phase's MFMAs:
   //   P0: DMA stage s+1 into the other slot (every wave's reads of stage s-1 retired before the
@@ -1918,28 +1946,55 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   //   P2: A(kk1, rh1) | MFMA B1 x A(kk1, rh0)
   //   P3: vmcnt(0) + lgkmcnt(0) + barrier (stage s+1 landed everywhere; stage s's reads retired) |
   //       B(kk0), A(kk0, rh0) of stage s+1 | MFMA B1 x A(kk1, rh1) | epilogue at a tile's last stage
-  if (ED && total > 1) issue(1);
+  // a3: A(s+2) is issued with B(s+1) at P0 (ED: B(s+2) and A(s+3) after the barrier of stage s, into the
+  // slots stage s just freed); the P3 wait keeps the youngest A stage (4 pieces per wave) and the stores in
+  // flight.  Spreading A's pieces over the phases instead (one per phase, the guide's 8-phase interleave)
+  // measured 1-11 % SLOWER on every dX product (profiles/r06_g256_a3s_ab.json)
+  if (ED && total > 1) {
+    if (a3) {
+      issue_b(1);
+      if (total > 2) issue_a(2);
+    } else {
+      issue(1);
+    }
+  }
   int nst = 0;  // ED: store instructions issued after the DMA in flight (the previous tile's epilogue)
   for (int s = 0; s < total; ++s) {
-    const char* cur = smem + (s & 1) * STAGE;
+    const char* cur = a_slot(s);
+    const char* curb = b_slot(s);
     const bool last = (s + 1) % g.nk == 0;
-    if (!ED && s + 1 < total) issue(s + 1);
+    const bool a_next = a3 && s + 2 < total;  // A(s+2) in flight at this stage's wait
+    if (!ED) {
+      if (a3) {
+        if (s + 1 < total) issue_b(s + 1);
+        if (a_next) issue_a(s + 2);
+      } else if (s + 1 < total) {
+        issue(s + 1);
+      }
+    }
     if (ED && EBIAS && last) load_bias(s / g.nk);
     read_a(cur, 0, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b0, a0, 0);
-    read_b(cur, 1, b1);
+    read_b(curb, 1, b1);
     read_a(cur, 1, 0, a0);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b0, a1, 1);
     read_a(cur, 1, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a0, 0);
-    // stage s+1 landed: vmcnt(0), or (ED) all but the nst youngest ops, the stores issued after its DMA
-    if (!ED || nst == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (nst <= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (nst <= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    else if (nst <= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    // stage s+1 landed: vmcnt(0), or all but the youngest `allow` ops -- (ED) the nst stores issued after
+    // its DMA, (a3) the 4 pieces of A(s+2) -- as the largest encodable count <= allow (waiting for more
+    // than needed is always safe)
+    const int allow = (ED ? nst : 0) + (a_next ? 4 : 0);
+    if (allow < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (allow < 16) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (allow < 20) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (allow < 32) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (allow < 36) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (allow < 48) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+    else if (allow < 52) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (allow < 63) asm volatile("s_waitcnt vmcnt(52)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1951,12 +2006,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
 #pragma unroll
           for (int r = 0; r < EW; ++r) asm volatile("" : "+v"(ebias[vv][r]));
       }
-      if (s + 2 < total) issue(s + 2);  // into slot s & 1: every wave's reads of stage s retired
+      // into the slots of stage s: every wave's reads of stage s retired
+      if (a3) {
+        if (s + 2 < total) issue_b(s + 2);
+        if (s + 3 < total) issue_a(s + 3);
+      } else if (s + 2 < total) {
+        issue(s + 2);
+      }
     }
     if (s + 1 < total) {
-      const char* nxt = smem + ((s + 1) & 1) * STAGE;
-      read_b(nxt, 0, b0);
-      read_a(nxt, 0, 0, a0);
+      read_b(b_slot(s + 1), 0, b0);
+      read_a(a_slot(s + 1), 0, 0, a0);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a1, 1);
@@ -2957,6 +3017,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
 #endif
     g.stagger = knob(VS_KNOB_G256_STAGGER);
     g.ed_ok = 1;  // launch_bf16_g256_ef clears it for an instance with a private segment
+    g.a3 = knob(VS_KNOB_G256_A3) == 1;
     count_path(VS_PATH_GEMM_G256);
     launch_bf16_g256(d, g, (unsigned)grid, e, s);
     VS_LAUNCH_CHECK();
