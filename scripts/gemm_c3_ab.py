@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rows", type=int, default=200704)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--dw", action="store_true", help="also time the four dW products")
     a = ap.parse_args()
     M, D, F = a.rows, 768, 3072
     dev = "cuda"
@@ -41,6 +42,7 @@ def main():
     prods = {"fwd_qkv": (3 * D, D, L.EPI_BIAS, bf, True),
              "fwd_proj": (D, D, L.EPI_BIAS | L.EPI_RESIDUAL, torch.float32, True),
              "fwd_fc1": (F, D, L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_GRAD, bf, True),
+             "fwd_fc1plain": (F, D, L.EPI_BIAS, bf, True),   # diagnostic: fc1's shape without the GELU epilogue
              "fwd_fc2": (D, F, L.EPI_BIAS | L.EPI_RESIDUAL, torch.float32, True),
              "dx_fc2": (F, D, L.EPI_MUL_AUX, bf, False), "dx_fc1": (D, F, 0, torch.float32, False),
              "dx_proj": (D, D, 0, bf, False), "dx_qkv": (D, 3 * D, 0, torch.float32, False)}
@@ -95,6 +97,36 @@ def main():
                                           f"({ent[str(v)]['frac']:.3f}) {'=' if same[v] else 'DIFF'}"
                                           for v in values), flush=True)
         del x, w, wb, c, res, aux_out, aux_in, ref
+    if a.dw:   # the weight-gradient products (dW = dY^T X over the 200,704 tokens, + bias gradient)
+        for name, (Mo, No) in {"dw_qkv": (3 * D, D), "dw_proj": (D, D), "dw_fc1": (F, D), "dw_fc2": (D, F)}.items():
+            if a.only and not name.startswith(a.only):
+                continue
+            dy = rnd(M, Mo)
+            xx = rnd(M, No)
+            c = torch.zeros(Mo, No, device=dev)
+            db = torch.zeros(Mo, device=dev)
+            ws = torch.empty(ops.splitk_workspace_bytes(bf, Mo, No, M) // 4 + 64, device=dev)
+            times = {v: [] for v in values}
+            for r in range(a.rounds):
+                order = values[r % len(values):] + values[:r % len(values)]
+                for v in order:
+                    L.knob_set(a.knob, v)
+                    ops.linear_dw(dy, xx, c, db=db, workspace=ws)
+                    s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    s0.record()
+                    for _ in range(a.reps):
+                        ops.linear_dw(dy, xx, c, db=db, workspace=ws)
+                    e0.record()
+                    torch.cuda.synchronize()
+                    times[v].append(s0.elapsed_time(e0) / a.reps * 1e3)
+            fl = 2.0 * M * Mo * No
+            ent = {str(v): {"median_us": round(statistics.median(times[v]), 1), "min_us": round(min(times[v]), 1),
+                            "frac": round(fl / (statistics.median(times[v]) * 1e-6) / PEAK, 4)} for v in values}
+            out["products"][name] = ent
+            print(f"{name:9s} " + "  ".join(f"{a.knob}={v}: {ent[str(v)]['median_us']:8.1f} us ({ent[str(v)]['frac']:.3f})"
+                                              for v in values), flush=True)
+            del dy, xx, c, ws
     L.knob_set(a.knob, 0)
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)

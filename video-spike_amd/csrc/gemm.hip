@@ -1709,49 +1709,79 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
       b_off[p] = (uint32_t)(k * ldb * 2 + ((((lane & 31) ^ swz_mc<128>(k))) << 4));
     }
   }
-  // stage s's images: A at a_slot(s), B at b_slot(s) + AB (the B read offsets include + AB)
+  // Slot byte offsets: A of stage s at a_at(slot), B at b_at(slot) + AB (the B read offsets include + AB);
+  // slots cycle 0, 1 (A and B together) or, a3, A 0, 1, 2 and B 0, 1
   const bool a3 = g.a3 != 0;
-  auto a_slot = [&](int s) __attribute__((always_inline)) -> char* {
-    return a3 ? smem + (s % 3) * AB : smem + (s & 1) * STAGE;
-  };
-  auto b_slot = [&](int s) __attribute__((always_inline)) -> char* {
-    return a3 ? smem + 2 * AB + (s & 1) * AB : smem + (s & 1) * STAGE;
-  };
-  auto issue_a = [&](int s, int p0 = 0, int p1 = 4) __attribute__((always_inline)) {  // pieces [p0, p1)
-    if (dbg & 1) return;
-    const int k = s / g.nk, t = s - k * g.nk;
+  auto a_at = [&](int sl) __attribute__((always_inline)) { return a3 ? sl * AB : sl * STAGE; };
+  auto b_at = [&](int sl) __attribute__((always_inline)) { return a3 ? 2 * AB + sl * AB : sl * STAGE; };
+  auto a_nxt = [&](int sl) __attribute__((always_inline)) { return a3 ? (sl == 2 ? 0 : sl + 1) : (sl ^ 1); };
+  // The A and B DMA streams each issue stages 0, 1, 2, ... in order: scalar state advanced per stage
+  // (global base + 64 k, the tile's rows and bases recomputed once per tile), LDS destinations as
+  // wave-uniform 32-bit addresses (the round-5 form recomputed the tile by two divisions and converted
+  // each piece's generic LDS pointer -- ~300 scalar / vector instructions per stage and wave)
+  const uint32_t lds_w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(VS_LDS char*)smem) +
+                         (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 4096u;
+  const int64_t b_step = BKC ? 128 : (int64_t)128 * ldb;  // bytes per 64-deep stage of B
+  int sa_k = 0, sa_t = 0, sa_sl = 0, sb_k = 0, sb_t = 0, sb_sl = 0;
+  int64_t sa_rows = 0;
+  const char* sa_ptr = nullptr;
+  const char* sb_ptr = nullptr;
+  auto a_tile = [&]() __attribute__((always_inline)) {
     int m0, n0;
-    tile_of(k, m0, n0);
+    tile_of(sa_k, m0, n0);
     (void)n0;
-    char* st = a_slot(s) + wid * 4096;
-    const int64_t mrows = e.M - m0;  // rows past M re-read row M-1 (never stored)
-    const char* abase = sgpr_ptr((const char*)(A + (int64_t)m0 * lda + (int64_t)t * 64));
-    if (mrows >= 256) {
+    sa_rows = e.M - m0;  // rows past M re-read row M-1 (never stored)
+    sa_ptr = (const char*)(A + (int64_t)m0 * lda);
+  };
+  auto b_tile = [&]() __attribute__((always_inline)) {
+    int m0, n0;
+    tile_of(sb_k, m0, n0);
+    (void)m0;
+    sb_ptr = BKC ? (const char*)(B + (int64_t)n0 * ldb) : (const char*)(B + n0);
+  };
+  a_tile();
+  b_tile();
+  auto issue_a = [&]() __attribute__((always_inline)) {
+    if (!(dbg & 1)) {
+      const uint32_t l = lds_w + (uint32_t)a_at(sa_sl);
+      if (sa_rows >= 256) {
+        glds16x4_m0(sa_ptr, a_off[0], a_off[1], a_off[2], a_off[3], l, l + 1024, l + 2048, l + 3072);
+      } else {
+        uint32_t o[4];
 #pragma unroll
-      for (int p = p0; p < p1; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
-    } else {
-#pragma unroll
-      for (int p = p0; p < p1; ++p) {
-        const int r = wid * 32 + p * 8 + (lane >> 3), rc = r < mrows ? r : (int)mrows - 1;
-        glds16_asm_so(abase, (uint32_t)(rc * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4)), st + p * 1024);
+        for (int p = 0; p < 4; ++p) {
+          const int r = wid * 32 + p * 8 + (lane >> 3), rc = r < sa_rows ? r : (int)sa_rows - 1;
+          o[p] = (uint32_t)(rc * lda * 2 + ((((lane & 7) ^ ((r >> 1) & 7))) << 4));
+        }
+        glds16x4_m0(sa_ptr, o[0], o[1], o[2], o[3], l, l + 1024, l + 2048, l + 3072);
       }
     }
+    if (++sa_t == g.nk) {
+      sa_t = 0;
+      ++sa_k;
+      a_tile();
+    } else {
+      sa_ptr += 128;
+    }
+    sa_sl = a_nxt(sa_sl);
   };
-  auto issue_b = [&](int s) __attribute__((always_inline)) {
-    if (dbg & 1) return;
-    const int k = s / g.nk, t = s - k * g.nk;
-    int m0, n0;
-    tile_of(k, m0, n0);
-    (void)m0;
-    char* st = b_slot(s) + wid * 4096;
-    const char* bbase = sgpr_ptr(BKC ? (const char*)(B + (int64_t)n0 * ldb + (int64_t)t * 64)
-                                     : (const char*)(B + (int64_t)t * 64 * ldb + n0));
-#pragma unroll
-    for (int p = 0; p < 4; ++p) glds16_asm_so(bbase, b_off[p], st + AB + p * 1024);
+  auto issue_b = [&]() __attribute__((always_inline)) {
+    if (!(dbg & 1)) {
+      const uint32_t l = lds_w + (uint32_t)(b_at(sb_sl) + AB);
+      glds16x4_m0(sb_ptr, b_off[0], b_off[1], b_off[2], b_off[3], l, l + 1024, l + 2048, l + 3072);
+    }
+    if (++sb_t == g.nk) {
+      sb_t = 0;
+      ++sb_k;
+      b_tile();
+    } else {
+      sb_ptr += b_step;
+    }
+    sb_sl ^= 1;
   };
-  auto issue = [&](int s) __attribute__((always_inline)) {
-    issue_a(s);
-    issue_b(s);
+  auto issue = [&]() __attribute__((always_inline)) {
+    issue_a();
+    issue_b();
   };
 
   // ---- fragments (per lane, stage-invariant byte offsets; kk = 32-deep half of the stage)
@@ -1800,7 +1830,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     }
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][4];  // each tile's first k-step overwrites them (mfma16z); zeroed once so no path reads undef
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1814,15 +1844,34 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   // and wait for it with vmcnt(<stores issued since>), so the stores drain under the next tile's first
   // stage instead of stalling it (vmcnt retires loads, DMA and stores in order)
   constexpr bool ED = (EF & (VS_EPI_RESIDUAL | VS_EPI_MUL_AUX | VS_EPI_GELU_BWD)) == 0;
+  // The early-DMA variants' bias by SCALAR loads (constant address space, wave-uniform base): counted by
+  // lgkmcnt, so hipcc's wait for them never drains the in-flight DMA (a vector load's vmcnt wait does:
+  // vmcnt retires in order); each lane then picks its EW columns of the wave's 4 x EW by fc
   float ebias[ENV][EW];
   auto load_bias = [&](int k) __attribute__((always_inline)) {
     int m0, n0;
     tile_of(k, m0, n0);
     (void)m0;
+    if constexpr (ED) {
+      typedef const __attribute__((address_space(4))) float* cfp;
+      const cfp bp = (cfp)e.bias + __builtin_amdgcn_readfirstlane(n0 + wc * 64);
 #pragma unroll
-    for (int vv = 0; vv < ENV; ++vv) {
-      if constexpr (EW == 8) ld8(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
-      else ld4(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
+      for (int vv = 0; vv < ENV; ++vv) {
+        float sb[4 * EW];
+#pragma unroll
+        for (int q = 0; q < 4 * EW; ++q) sb[q] = bp[EVS * vv + q];
+#pragma unroll
+        for (int r = 0; r < EW; ++r)
+          ebias[vv][r] = fc == 0 ? sb[r] : fc == 1 ? sb[EW + r] : fc == 2 ? sb[2 * EW + r] : sb[3 * EW + r];
+      }
+    } else {
+      // the residual / GELU' variants drain vmcnt every stage anyway; scalar loads there cost SGPRs that
+      // their epilogue's operand addressing needs (fc2: SGPR spills to VGPR lanes at 256 VGPRs, 974 -> 1,177 us)
+#pragma unroll
+      for (int vv = 0; vv < ENV; ++vv) {
+        if constexpr (EW == 8) ld8(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
+        else ld4(e.bias, n0 + wc * 64 + EW * fc + EVS * vv, 0, ebias[vv]);
+      }
     }
   };
   // epilogue store instructions per lane (vmcnt units), all issued after the early DMA
@@ -1892,11 +1941,21 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
           }
           const int64_t n = ncol + VS * vv;
           if constexpr (GELU) {
+            if constexpr ((F & VS_EPI_GELU_GRAD) != 0) {  // packed pairs (the epilogue's dominant VALU)
 #pragma unroll
-            for (int r = 0; r < W; ++r) {
-              const float x = bf2f(f2bf(v[r]));
-              if constexpr ((F & VS_EPI_GELU_GRAD) != 0) v[r] = gelu_fast_both(x, t[r]);
-              else {
+              for (int r = 0; r < W; r += 2) {
+                const f32x2v x = {bf2f(f2bf(v[r])), bf2f(f2bf(v[r + 1]))};
+                f32x2v gr;
+                const f32x2v y = gelu_fast_both2(x, gr);
+                v[r] = y.x;
+                v[r + 1] = y.y;
+                t[r] = gr.x;
+                t[r + 1] = gr.y;
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < W; ++r) {
+                const float x = bf2f(f2bf(v[r]));
                 t[r] = v[r];
                 v[r] = gelu_fast(x);
               }
@@ -1908,8 +1967,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
             for (int r = 0; r < W; ++r) v[r] += opnd[ii][vv][r];
           }
           if (live && !(dbg & 2)) stv(e.c, m * e.ldc + n, e.out_bf16, v);
+          // ED: no re-zeroing (the next tile's first k-step MFMAs take a zero C operand); the residual /
+          // GELU' variants keep the zeroing pass: with the zero-C copy of the MFMA block fc2 (256 VGPRs)
+          // measured 974 -> 1,236 us
+          if constexpr (!ED) {
 #pragma unroll
-          for (int q = 0; q < W / 4; ++q) acc[i][(W / 4) * vv + q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < W / 4; ++q) acc[i][(W / 4) * vv + q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
         }
       }
     }
@@ -1924,20 +1988,31 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
         acc[rh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], af[i], acc[rh * 4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  // a tile's first k-step: C = 0 (an inline constant), so the accumulators need no zeroing pass
+  // (128 v_mov per wave and tile)
+  auto mfma16z = [&](const bf16x8 (&bc)[4], const bf16x8 (&af)[4], int rh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[rh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], af[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
 
   // prologue: stage 0 landed, its first fragments in registers
   bf16x8 a0[4], a1[4], b0[4], b1[4];
-  issue(0);
+  issue();  // stage 0
   if (a3 && total > 1) {
-    issue_a(1);
+    issue_a();  // A(1)
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A(0), B(0) landed; A(1) in flight
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  read_b(b_slot(0), 0, b0);
-  read_a(a_slot(0), 0, 0, a0);
+  read_b(smem + b_at(0), 0, b0);
+  read_a(smem + a_at(0), 0, 0, a0);
 
   // Stage s (slot s & 1), four phases; fragments of the next phase are read before this phase's MFMAs:
   //   P0: DMA stage s+1 into the other slot (every wave's reads of stage s-1 retired before the
@@ -1952,34 +2027,37 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
   // measured 1-11 % SLOWER on every dX product (profiles/r06_g256_a3s_ab.json)
   if (ED && total > 1) {
     if (a3) {
-      issue_b(1);
-      if (total > 2) issue_a(2);
+      issue_b();                  // B(1)
+      if (total > 2) issue_a();   // A(2)
     } else {
-      issue(1);
+      issue();                    // stage 1
     }
   }
   int nst = 0;  // ED: store instructions issued after the DMA in flight (the previous tile's epilogue)
+  int ra = 0, rb = 0, tk = 0, tt = 0;  // compute side: slots of stage s, its tile and k-step
   for (int s = 0; s < total; ++s) {
-    const char* cur = a_slot(s);
-    const char* curb = b_slot(s);
-    const bool last = (s + 1) % g.nk == 0;
+    const char* cur = smem + a_at(ra);
+    const char* curb = smem + b_at(rb);
+    const bool last = tt == g.nk - 1;
     const bool a_next = a3 && s + 2 < total;  // A(s+2) in flight at this stage's wait
     if (!ED) {
       if (a3) {
-        if (s + 1 < total) issue_b(s + 1);
-        if (a_next) issue_a(s + 2);
+        if (s + 1 < total) issue_b();  // B(s+1)
+        if (a_next) issue_a();         // A(s+2)
       } else if (s + 1 < total) {
-        issue(s + 1);
+        issue();                       // stage s+1
       }
     }
-    if (ED && EBIAS && last) load_bias(s / g.nk);
+    if (ED && EBIAS && last) load_bias(tk);
     read_a(cur, 0, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
-    mfma16(b0, a0, 0);
+    if (ED && tt == 0) mfma16z(b0, a0, 0);
+    else mfma16(b0, a0, 0);
     read_b(curb, 1, b1);
     read_a(cur, 1, 0, a0);
     __builtin_amdgcn_sched_barrier(0);
-    mfma16(b0, a1, 1);
+    if (ED && tt == 0) mfma16z(b0, a1, 1);
+    else mfma16(b0, a1, 1);
     read_a(cur, 1, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a0, 0);
@@ -2000,7 +2078,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (ED) {
-      if (EBIAS && last) {  // the compiler's wait for the bias loads lands here, before the next DMA
+      if (EBIAS && last) {  // the bias (scalar loads at this stage's start) in registers before the next DMA
 #pragma unroll
         for (int vv = 0; vv < ENV; ++vv)
 #pragma unroll
@@ -2008,28 +2086,34 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
       }
       // into the slots of stage s: every wave's reads of stage s retired
       if (a3) {
-        if (s + 2 < total) issue_b(s + 2);
-        if (s + 3 < total) issue_a(s + 3);
+        if (s + 2 < total) issue_b();  // B(s+2)
+        if (s + 3 < total) issue_a();  // A(s+3)
       } else if (s + 2 < total) {
-        issue(s + 2);
+        issue();                       // stage s+2
       }
     }
+    ra = a_nxt(ra);
+    rb ^= 1;
     if (s + 1 < total) {
-      read_b(b_slot(s + 1), 0, b0);
-      read_a(a_slot(s + 1), 0, 0, a0);
+      read_b(smem + b_at(rb), 0, b0);
+      read_a(smem + a_at(ra), 0, 0, a0);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma16(b1, a1, 1);
     nst = 0;
     if (last) {
-      epilogue(s / g.nk);
+      epilogue(tk);
       if constexpr (ED) {
         int m0, n0;
-        tile_of(s / g.nk, m0, n0);
+        tile_of(tk, m0, n0);
         (void)n0;
         // exact count only for a full tile (a ragged one skips the stores of all-dead rows) and real stores
         nst = (g.ed_ok && m0 + 256 <= e.M && !(dbg & 2)) ? (est < 63 ? est : 63) : 0;
       }
+      tt = 0;
+      ++tk;
+    } else {
+      ++tt;
     }
   }
 }
@@ -2080,16 +2164,28 @@ __global__ __launch_bounds__(512, 1) void gemm_dw256_kernel(const bf16_t* __rest
     a_off[p] = (uint32_t)(k * lda * 2 + c);
     b_off[p] = (uint32_t)(k * ldb * 2 + c);
   }
-  auto issue = [&](int item, int t, int slot_s) __attribute__((always_inline)) {
+  // The DMA stream's global bases are recomputed (two divisions) only when it moves to a new item and
+  // advanced by 64 token rows per stage otherwise; LDS destinations are wave-uniform 32-bit addresses
+  // (glds16x4_m0: no per-piece generic -> LDS conversion)
+  const uint32_t lds_w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)(VS_LDS char*)smem) +
+                         (uint32_t)__builtin_amdgcn_readfirstlane(wid) * 4096u;
+  const char* dA = nullptr;
+  const char* dB = nullptr;
+  auto item_bases = [&](int item, int t) __attribute__((always_inline)) {
     const int sp = item / g.tiles, tile = item - sp * g.tiles, mt = tile / g.tiles_n, nt = tile - mt * g.tiles_n;
     const int64_t k0 = (int64_t)(sp * g.kps + t) * 64;
-    char* st = smem + slot_s * STAGE + wid * 4096;
-    const char* abase = sgpr_ptr((const char*)(A + k0 * lda + (int64_t)mt * 256));
-    const char* bbase = sgpr_ptr((const char*)(B + k0 * ldb + (int64_t)nt * 256));
-#pragma unroll
-    for (int p = 0; p < 4; ++p) glds16_asm_so(abase, a_off[p], st + p * 1024);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) glds16_asm_so(bbase, b_off[p], st + AB + p * 1024);
+    dA = (const char*)(A + k0 * lda + (int64_t)mt * 256);
+    dB = (const char*)(B + k0 * ldb + (int64_t)nt * 256);
+  };
+  auto issue = [&](int item, int t, int slot_s) __attribute__((always_inline)) {
+    if (t == 0) item_bases(item, 0);
+    else {
+      dA += (int64_t)128 * lda;  // 64 token rows
+      dB += (int64_t)128 * ldb;
+    }
+    const uint32_t l = lds_w + (uint32_t)(slot_s * STAGE);
+    glds16x4_m0(dA, a_off[0], a_off[1], a_off[2], a_off[3], l, l + 1024, l + 2048, l + 3072);
+    glds16x4_m0(dB, b_off[0], b_off[1], b_off[2], b_off[3], l + AB, l + AB + 1024, l + AB + 2048, l + AB + 3072);
   };
 
   // ---- fragments: lane (fr, fc) reads k rows kr0 = 8 fc + (fr >> 2) and kr0 + 4, columns p4 .. p4+3
@@ -3017,7 +3113,7 @@ extern "C" int vs_gemm(const vs_gemm_desc* d, void* stream) {
 #endif
     g.stagger = knob(VS_KNOB_G256_STAGGER);
     g.ed_ok = 1;  // launch_bf16_g256_ef clears it for an instance with a private segment
-    g.a3 = knob(VS_KNOB_G256_A3) == 1;
+    g.a3 = knob(VS_KNOB_G256_A3) != 2;  // default on (round 6: every forward / dX product faster)
     count_path(VS_PATH_GEMM_G256);
     launch_bf16_g256(d, g, (unsigned)grid, e, s);
     VS_LAUNCH_CHECK();
