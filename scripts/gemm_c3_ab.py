@@ -64,11 +64,14 @@ def main():
                   ld_aux_in=N if aux_in is not None else 0)
         ref = None
         same = {}
+        paths = {}
         for v in values:
             L.knob_set(a.knob, v)
             c.fill_(7.0)
+            L.dispatch_reset()
             ops.gemm(x, wb, c, **kw)
             torch.cuda.synchronize()
+            paths[v] = [k for k, n in L.dispatch_counts().items() if n]
             if ref is None:
                 ref = c.clone()
             same[v] = bool(torch.equal(c, ref))
@@ -91,10 +94,10 @@ def main():
         for v in values:
             med = statistics.median(times[v])
             ent[str(v)] = {"median_us": round(med, 1), "min_us": round(min(times[v]), 1),
-                           "frac": round(fl / (med * 1e-6) / PEAK, 4), "bitwise_vs_first": same[v]}
+                           "frac": round(fl / (med * 1e-6) / PEAK, 4), "bitwise_vs_first": same[v], "path": paths[v]}
         out["products"][name] = ent
         print(f"{name:9s} " + "  ".join(f"{a.knob}={v}: {ent[str(v)]['median_us']:8.1f} us "
-                                          f"({ent[str(v)]['frac']:.3f}) {'=' if same[v] else 'DIFF'}"
+                                          f"({ent[str(v)]['frac']:.3f}) {'=' if same[v] else 'DIFF'} {paths[v]}"
                                           for v in values), flush=True)
         del x, w, wb, c, res, aux_out, aux_in, ref
     if a.dw:   # the weight-gradient products (dW = dY^T X over the 200,704 tokens, + bias gradient)

@@ -2379,7 +2379,7 @@ struct Dw256Plan {
 static Dw256Plan plan_dw256(int64_t M, int64_t N, int64_t K) {
   Dw256Plan p = {};
   // 768 x 768 (the projection's dW) measured no faster than the split-K dW tiles: 326 vs 308 us
-  if (M % 256 || N % 256 || K % 64 || K < 64 * 64 || M * N <= 768 * 768) return p;
+  if (M % 256 || N % 256 || K % 64 || K < 64 * 64 || (M * N <= 768 * 768 && knob(VS_KNOB_DW256_ALL) != 1)) return p;
   const int64_t tiles = (M / 256) * (N / 256), nk = K / 64;
   double best = 1e30;
   for (int64_t S0 = 1; S0 <= 256 && S0 * 8 <= nk; ++S0) {
