@@ -404,8 +404,64 @@ __global__ __launch_bounds__(256, 2) void conv_dw_kernel(ConvDw g) {
     load(rd, rx, 0);
     store(smem, rd, rx);
   }
-  __syncthreads();
-  for (int t = 0; t < nsteps; ++t) {
+  if constexpr (!M32) {
+    // Two steps of global loads in flight (round 6): step t+2's dy / gather rows are loaded into the
+    // register set not being stored this step, so a load has a whole step of MFMAs plus the next
+    // step's to land before its LDS store (one step ahead, the stores waited on L2 / HBM latency:
+    // wait_inst 0.62 of wave cycles, profiles/r05_pmc_convdw.json).  The two sets alternate by unrolling.
+    float4 rdb[2], rxb[XS];
+    if (nsteps > 1) load(rd, rx, 1);
+    __syncthreads();
+    constexpr int NS = BM / 4, HS = NS / 2;
+    auto body = [&](int t, float4 (&sd1)[2], float4 (&sx1)[XS], float4 (&ld2)[2], float4 (&lx2)[XS]) {
+      const float* sd_ = smem + (t & 1) * STAGE;
+      const float* sx = sd_ + SO;
+      if (t + 2 < nsteps) load(ld2, lx2, t + 2);
+      float af[NS][2], bfr[NS][NJ];
+      auto rd_ops = [&](int sub) {
+        const int mrow = 4 * sub + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[sub][i] = sd_[mrow * LDO + wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[sub][j] = sx[mrow * LD + wc * (BKK / 2) + j * 16 + (lane & 15)];
+      };
+      auto mm_ops = [&](int sub) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[sub][i], bfr[sub][j], acc[i][j], 0, 0, 0);
+      };
+#pragma unroll
+      for (int sub = 0; sub < HS; ++sub) rd_ops(sub);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = HS; sub < NS; ++sub) rd_ops(sub);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = 0; sub < HS; ++sub) mm_ops(sub);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sub = HS; sub < NS; ++sub) mm_ops(sub);
+      if (t + 1 < nsteps) store(smem + ((t + 1) & 1) * STAGE, sd1, sx1);
+      if ((t & 15) == 15) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            tot[i][j] += acc[i][j];
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+      __syncthreads();
+    };
+    for (int t = 0; t < nsteps; t += 2) {
+      body(t, rd, rx, rdb, rxb);                     // stores step t+1 from (rd, rx), loads t+2 into (rdb, rxb)
+      if (t + 1 < nsteps) body(t + 1, rdb, rxb, rd, rx);
+    }
+  }
+  if constexpr (M32) __syncthreads();
+  for (int t = 0; M32 && t < nsteps; ++t) {
     const float* sd_ = smem + (t & 1) * STAGE;
     const float* sx = sd_ + SO;
     const bool more = t + 1 < nsteps;
