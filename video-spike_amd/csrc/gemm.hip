@@ -1893,38 +1893,72 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
     constexpr int W = EW, NV = ENV;  // columns per vector, vectors per row fragment
     constexpr int VS = EVS;          // column step between a lane's vectors
     const int ncol = n0 + wc * 64 + W * fc;
-    auto ldv = [&](const void* p, int64_t i, int bf, float (&v)[W]) __attribute__((always_inline)) {
-      if constexpr (W == 8) ld8(p, i, bf, v);
-      else ld4(p, i, bf, v);
-    };
     auto stv = [&](void* p, int64_t i, int bf, const float (&v)[W]) __attribute__((always_inline)) {
       if constexpr (W == 8) st8(p, i, bf, v);
       else st4(p, i, bf, v);
     };
     if constexpr (BIAS && !ED) load_bias(k);  // ED: loaded at the start of the tile's last stage
-    constexpr int GR = 2;  // row fragments per operand group (32 VGPRs of f32 operands)
+    // Operand rows (residual f32, GELU' factor bf16: g256 runs bf16 operands only) as raw 16-B vectors,
+    // row fragment i+1's loads issued before fragment i's stores (round 6).  vmcnt retires in order, so
+    // a load issued after a fragment's stores waited for all of them: round 5 loaded per 32 rows, and
+    // each later group of the epilogue stalled on the previous group's store completion.
+    struct Raw {
+      float4 f[NV][W / 4];
+      uint4 h8[NV];
+      uint2 h4[NV];
+    };
+    auto ld_raw = [&](int i, Raw& rw) __attribute__((always_inline)) {
+      const int64_t m = m0 + wr * 128 + i * 16 + fr;
+      const int64_t mc = m < e.M ? m : e.M - 1;  // rows past M: any valid row (not stored)
 #pragma unroll
-    for (int h = 0; h < 8 / GR; ++h) {
-      float opnd[GR][NV][W];
-      if constexpr (RES || AUXIN) {
+      for (int vv = 0; vv < NV; ++vv) {
+        if constexpr (RES) {
 #pragma unroll
-        for (int ii = 0; ii < GR; ++ii) {
-          const int64_t m = m0 + wr * 128 + (GR * h + ii) * 16 + fr;
-          const int64_t mc = m < e.M ? m : e.M - 1;     // rows past M: any valid row (not stored)
-#pragma unroll
-          for (int vv = 0; vv < NV; ++vv) {
-            if constexpr (RES) ldv(e.residual, mc * e.ldr + ncol + VS * vv, 0, opnd[ii][vv]);
-            else ldv(e.aux_in, mc * e.ld_aux_in + ncol + VS * vv, e.op_bf16, opnd[ii][vv]);
-          }
+          for (int q = 0; q < W / 4; ++q) rw.f[vv][q] = *(const float4*)(e.residual + mc * e.ldr + ncol + VS * vv + 4 * q);
+        } else if constexpr (W == 8) {
+          rw.h8[vv] = *(const uint4*)((const bf16_t*)e.aux_in + mc * e.ld_aux_in + ncol + VS * vv);
+        } else {
+          rw.h4[vv] = *(const uint2*)((const bf16_t*)e.aux_in + mc * e.ld_aux_in + ncol + VS * vv);
         }
       }
+    };
+    auto unpack = [&](const Raw& rw, int vv, float (&o)[W]) __attribute__((always_inline)) {
+      if constexpr (RES) {
 #pragma unroll
-      for (int ii = 0; ii < GR; ++ii) {
-        const int i = GR * h + ii;
+        for (int q = 0; q < W / 4; ++q) {
+          o[4 * q] = rw.f[vv][q].x;
+          o[4 * q + 1] = rw.f[vv][q].y;
+          o[4 * q + 2] = rw.f[vv][q].z;
+          o[4 * q + 3] = rw.f[vv][q].w;
+        }
+      } else {
+        uint32_t w4[W / 2];
+        if constexpr (W == 8) {
+          w4[0] = rw.h8[vv].x; w4[1] = rw.h8[vv].y; w4[2] = rw.h8[vv].z; w4[3] = rw.h8[vv].w;
+        } else {
+          w4[0] = rw.h4[vv].x; w4[1] = rw.h4[vv].y;
+        }
+#pragma unroll
+        for (int q = 0; q < W / 2; ++q) {
+          o[2 * q] = __uint_as_float(w4[q] << 16);
+          o[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+        }
+      }
+    };
+    Raw rbuf[2];
+    if constexpr (RES || AUXIN) ld_raw(0, rbuf[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (RES || AUXIN) {
+        if (i + 1 < 8) ld_raw(i + 1, rbuf[(i + 1) & 1]);
+      }
+      {
         const int64_t m = m0 + wr * 128 + i * 16 + fr;
         const bool live = m < e.M;
 #pragma unroll
         for (int vv = 0; vv < NV; ++vv) {
+          float opv[W];
+          if constexpr (RES || AUXIN) unpack(rbuf[i & 1], vv, opv);
           float v[W], t[W];
 #pragma unroll
           for (int r = 0; r < W; ++r) {
@@ -1933,11 +1967,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
           }
           if constexpr ((F & VS_EPI_GELU_BWD) != 0) {
 #pragma unroll
-            for (int r = 0; r < W; ++r) v[r] *= gelu_fast_grad(opnd[ii][vv][r]);
+            for (int r = 0; r < W; ++r) v[r] *= gelu_fast_grad(opv[r]);
           }
           if constexpr ((F & VS_EPI_MUL_AUX) != 0) {
 #pragma unroll
-            for (int r = 0; r < W; ++r) v[r] *= opnd[ii][vv][r];
+            for (int r = 0; r < W; ++r) v[r] *= opv[r];
           }
           const int64_t n = ncol + VS * vv;
           if constexpr (GELU) {
@@ -1964,7 +1998,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_g256_kernel(const bf16_t* __
           }
           if constexpr (RES) {
 #pragma unroll
-            for (int r = 0; r < W; ++r) v[r] += opnd[ii][vv][r];
+            for (int r = 0; r < W; ++r) v[r] += opv[r];
           }
           if (live && !(dbg & 2)) stv(e.c, m * e.ldc + n, e.out_bf16, v);
           // ED: no re-zeroing (the next tile's first k-step MFMAs take a zero C operand); the residual /
