@@ -439,7 +439,8 @@ extern "C" int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, con
   const int lpr = ln_vec_lpr(cols);
   if (lpr && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(gamma) && aligned16(beta) &&
       (((uintptr_t)y) & (y_dtype == VS_BF16 ? 7 : 15)) == 0) {
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), 2048);
+    const int fk = knob(VS_KNOB_LN_FWD_BLOCKS);  // A/B knob: the forward's grid cap (default 2048)
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), fk > 0 ? fk : 2048);
 #define FV_(TO, L) \
   hipLaunchKernelGGL((ln_fwd_vec_kernel<TO, L, 3>), dim3(grid), dim3(256), 0, s, x, ldx, gamma, beta, eps, (TO*)y, ldy, mean, rstd, rows)
     if (y_dtype == VS_BF16) {
@@ -490,8 +491,11 @@ static int layernorm_bwd_t(int64_t rows, int64_t cols, const TD* dy, int64_t ldd
   if (lpr && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 && (!dres || (lddres % 4 == 0 && aligned16(dres))) &&
       (((uintptr_t)dy) & (BF ? 7 : 15)) == 0 && aligned16(x) && aligned16(dx) && aligned16(gamma) &&
       (!dx_lp || (((uintptr_t)dx_lp) & 7) == 0)) {
-    const int kc = knob(VS_KNOB_LN_BLOCKS);  // A/B knob: caps the grid (= partial rows) below 1024
-    const int cap = kc > 0 && kc <= kLnBwdBlocks ? kc : kLnBwdBlocks;
+    // grid cap (= partial rows) 512 by default: at ~160 VGPRs only 3 of these 4-wave blocks fit a CU, so
+    // 1,024 blocks ran as one full round plus a one-third-occupied tail (C3 LN': 535 -> 444 us per launch,
+    // C2 width 139 -> 120 us; profiles/r06_ln_ab.json); VS_KNOB_LN_BLOCKS overrides
+    const int kc = knob(VS_KNOB_LN_BLOCKS);
+    const int cap = kc > 0 && kc <= kLnBwdBlocks ? kc : 512;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), cap);
     float* part = (float*)workspace;
 #define BV_(L)                                                                                                       \

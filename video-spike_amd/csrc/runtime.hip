@@ -34,7 +34,7 @@ static const KnobDef kKnobs[VS_KNOB_COUNT] = {
     {"VSPIKE_DW_BM", 0},       {"VSPIKE_DW_BN", 0},        {"VSPIKE_DW_SPLITS", 0},    {"VSPIKE_DW_STAGES", 0},
     {"VSPIKE_LN_BLOCKS", 0},   {"VSPIKE_DH_F32", 0},       {"VSPIKE_NO_PATCH_FUSED", 0}, {"VSPIKE_NO_DW_GROUP", 0},
     {"VSPIKE_ATTN_VARIANT", 0}, {"VSPIKE_SLAB_WV", 0}, {"VSPIKE_WRES_WV", 0}, {"VSPIKE_WRES_DBG", 0}, {"VSPIKE_G256", 0}, {"VSPIKE_G256_GRID", 0}, {"VSPIKE_G256_DBG", 0}, {"VSPIKE_NO_DW256", 0}, {"VSPIKE_G256_STAGGER", 0}, {"VSPIKE_CONV_DW128", 0},
-    {"VSPIKE_CONV_MFMA", 0}, {"VSPIKE_G256_A3", 0}, {"VSPIKE_DW256_ALL", 0},
+    {"VSPIKE_CONV_MFMA", 0}, {"VSPIKE_G256_A3", 0}, {"VSPIKE_DW256_ALL", 0}, {"VSPIKE_LN_FWD_BLOCKS", 0},
     {nullptr, 0}};
 static std::atomic<int> g_knob[VS_KNOB_COUNT];
 static std::once_flag g_knob_once;

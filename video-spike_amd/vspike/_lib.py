@@ -41,7 +41,7 @@ PATH_COUNT = 26
 KNOB_NAMES = ("dw_old", "no_skinny", "no_slab", "no_big", "no_wres", "wres_gbwd", "no_wslab", "wslab", "wslab_g",
               "panel", "no_panel", "panel_grid", "no_fullk", "no_ring", "no_lnf_fuse", "no_ln_fuse", "dw_bm", "dw_bn",
               "dw_splits", "dw_stages", "ln_blocks", "dh_f32", "no_patch_fused", "no_dw_group", "attn_variant", "slab_wv", "wres_wv", "wres_dbg",
-              "g256", "g256_grid", "g256_dbg", "no_dw256", "g256_stagger", "conv_dw128", "conv_mfma", "g256_a3", "dw256_all")
+              "g256", "g256_grid", "g256_dbg", "no_dw256", "g256_stagger", "conv_dw128", "conv_mfma", "g256_a3", "dw256_all", "ln_fwd_blocks")
 KNOB_COUNT = 40
 
 c_i32, c_i64, c_u32, c_f32, c_p, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float,
