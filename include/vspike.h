@@ -639,7 +639,7 @@ int vs_g256_scratch_free(void);
 #define VS_KNOB_CONV_DW128  33   /* 1: Conv3d weight gradient on 128-wide k tiles where K >= 128 (measured slower than the 64-wide default) */
 #define VS_KNOB_CONV_MFMA   34   /* Conv3d weight gradient's f32 MFMA shape: 0 = 16x16x4 (default), 1 = 32x32x2 (measured slower) */
 #define VS_KNOB_DW256_ALL   36   /* 1: the 768 x 768 projection dW on the 256 x 256 dW kernel too (default: split-K dW tiles) */
-#define VS_KNOB_LN_FWD_BLOCKS 37 /* LayerNorm forward (vectorised) grid cap (0 = 2048) */
+#define VS_KNOB_LN_FWD_BLOCKS 37 /* LayerNorm forward (vectorised) grid cap (0 = default 768) */
 #define VS_KNOB_G256_A3     35   /* 256 x 256 forward / dX GEMM: the streamed A operand in three LDS slots (DMA two stages ahead, counted stage wait): 0 / 1 = on (default), 2 = off (two slots, round 5) */
 #define VS_KNOB_COUNT       40
 int vs_knob_get(int knob);               /* VS_EINVAL for an unknown id */

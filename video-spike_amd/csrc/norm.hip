@@ -439,8 +439,11 @@ extern "C" int vs_layernorm_fwd(int32_t y_dtype, int64_t rows, int64_t cols, con
   const int lpr = ln_vec_lpr(cols);
   if (lpr && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && aligned16(gamma) && aligned16(beta) &&
       (((uintptr_t)y) & (y_dtype == VS_BF16 ? 7 : 15)) == 0) {
-    const int fk = knob(VS_KNOB_LN_FWD_BLOCKS);  // A/B knob: the forward's grid cap (default 2048)
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), fk > 0 ? fk : 2048);
+    // grid cap 768 by default (was 2,048: 1,792 blocks fit the chip at 66 VGPRs, the rest ran as a tail;
+    // fewer, longer-lived blocks measured faster still: C3 width 189.5 -> 168.7 us, profiles/r06_lnf_ab.json;
+    // per-row work, so the outputs are bitwise the same); VS_KNOB_LN_FWD_BLOCKS overrides
+    const int fk = knob(VS_KNOB_LN_FWD_BLOCKS);
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(rows, 256 / lpr), fk > 0 ? fk : 768);
 #define FV_(TO, L) \
   hipLaunchKernelGGL((ln_fwd_vec_kernel<TO, L, 3>), dim3(grid), dim3(256), 0, s, x, ldx, gamma, beta, eps, (TO*)y, ldy, mean, rstd, rows)
     if (y_dtype == VS_BF16) {
